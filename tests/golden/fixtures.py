@@ -1,0 +1,53 @@
+"""Load a golden fixture and regenerate its inputs (weights, conditioning, mel, noise)
+from the seeds it records, checking the SHA-256 digests made at generation time."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+from wavernn_amd import synthetic as syn
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LOOP_CASES = ["loop_raw_tiny_b2", "loop_mol_tiny_b2", "loop_raw_b1", "loop_mol_b1",
+              "loop_raw_b3", "loop_mol_b4"]
+LONG_LOOP_CASES = ["loop_raw_1s", "loop_mol_1s"]
+GEN_CASES = ["gen_mol_unbatched", "gen_raw_batched_mulaw", "gen_mol_batched", "gen_raw_tiny_unbatched"]
+
+# MoL parity tolerance per sample under noise injection: ~50-100x the
+# 5e-8..1.8e-7 the C restatement shows against the reference.
+MOL_TOL = 1e-5
+
+
+def load(name: str) -> dict:
+    z = np.load(os.path.join(HERE, name + ".npz"), allow_pickle=False)
+    return {k: z[k] for k in z.files}
+
+
+def dims_of(fx: dict) -> syn.FatchordDims:
+    text = str(fx["dims"])
+    assert text.startswith("FatchordDims(")
+    return eval("syn." + text, {"syn": syn})  # repr of a frozen dataclass written by make_golden
+
+
+def loop_inputs(fx: dict):
+    d = dims_of(fx)
+    B, L = int(fx["B"]), int(fx["L"])
+    state = syn.make_fatchord_state(d, int(fx["wseed"]))
+    mels, aux = syn.make_conditioning(B, L, d.feat_dims, d.res_out_dims, int(fx["cseed"]))
+    noise = syn.make_noise(d.mode, B, L, d.n_classes, int(fx["nseed"]))
+    assert syn.state_digest(state) == str(fx["state_sha"]), "synthetic weight generator drifted"
+    assert syn.digest(mels, aux) == str(fx["cond_sha"]), "synthetic conditioning drifted"
+    assert syn.digest(noise) == str(fx["noise_sha"]), "synthetic noise drifted"
+    return d, state, mels, aux, noise
+
+
+def gen_inputs(fx: dict):
+    d = dims_of(fx)
+    state = syn.make_fatchord_state(d, int(fx["wseed"]))
+    mel = syn.make_mel(d.feat_dims, int(fx["T"]), int(fx["mseed"]))
+    noise = syn.make_noise(d.mode, int(fx["B"]), int(fx["Lf"]), d.n_classes, int(fx["nseed"]))
+    assert syn.state_digest(state) == str(fx["state_sha"])
+    assert syn.digest(mel) == str(fx["mel_sha"])
+    assert syn.digest(noise) == str(fx["noise_sha"])
+    return d, state, mel, noise

@@ -1,0 +1,57 @@
+"""Pin the oracle (CPU restatement) against the reference's own outputs (golden fixtures).
+
+RAW labels: bit-exact.  MoL samples: |Δ| <= MOL_TOL.  Upsample restatement: 1e-5 abs."""
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from tests.golden import fixtures as gf
+
+
+@pytest.mark.parametrize("name", gf.LOOP_CASES)
+def test_loop_matches_reference(name):
+    fx = gf.load(name)
+    d, state, mels, aux, noise = gf.loop_inputs(fx)
+    out, labels = orc.fatchord_loop(state, d.mode, mels, aux, noise)
+    if d.mode == "RAW":
+        np.testing.assert_array_equal(labels, fx["labels"].astype(np.int32))
+    else:
+        assert np.abs(out - fx["samples"]).max() <= gf.MOL_TOL
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("name", gf.LONG_LOOP_CASES)
+def test_long_loop_matches_reference(name):
+    fx = gf.load(name)
+    d, state, mels, aux, noise = gf.loop_inputs(fx)
+    out, labels = orc.fatchord_loop(state, d.mode, mels, aux, noise)
+    if d.mode == "RAW":
+        np.testing.assert_array_equal(labels, fx["labels"].astype(np.int32))
+    else:
+        assert np.abs(out - fx["samples"]).max() <= gf.MOL_TOL
+
+
+@pytest.mark.parametrize("name", gf.GEN_CASES)
+def test_generate_matches_reference(name):
+    fx = gf.load(name)
+    d, state, mel, noise = gf.gen_inputs(fx)
+    mp = orc.pad_tensor(mel.T[None], d.pad)[0].T
+    m, a = orc.upsample(mp, state, d.upsample_factors, d.res_blocks, d.pad)
+    s = int(fx["up_stride"])
+    assert np.abs(m[::s] - fx["up_mels"]).max() < 1e-5
+    assert np.abs(a[::s] - fx["up_aux"]).max() < 1e-5
+    out = orc.generate(state, d, mel, bool(fx["batched"]), int(fx["target"]), int(fx["overlap"]),
+                       bool(fx["mu_law"]), noise)
+    assert out.dtype == np.float64 and out.shape == fx["output"].shape
+    if d.mode == "RAW":
+        assert np.array_equal(out, fx["output"])
+    else:
+        assert np.abs(out - fx["output"]).max() <= gf.MOL_TOL
+
+
+def test_fold_unfold_identity_on_constant():
+    x = np.ones((1, 1000, 3), np.float32)
+    f = orc.fold_with_overlap(x, 200, 50)
+    assert f.shape == (4, 300, 3)
+    y = orc.xfade_and_unfold(f[:, :, 0].astype(np.float64), 50)
+    assert y.shape == (4 * 250 + 50,)
