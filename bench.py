@@ -1,0 +1,158 @@
+"""Headline benchmark: WaveRNN MoL (rnn_dims 512) generation on MI355X.
+
+Workload (BASELINE.json configs[1]): one 5 s utterance per GPU (synthetic 80-band mel,
+T = 401 frames → 110 275 loop steps, 110 000 output samples), unbatched (batch = 1), MoL
+sampling, random weights of the 800k-step MoL architecture (hparams.py).  A "step" of this
+benchmark is one full `WaveRNN.generate()` of that utterance (upsample → persistent HIP
+loop → float64 post-processing).  N GPUs = N ranks, one utterance each (weak scaling; the
+utterances are independent, there is no collective in the data path).
+
+Prints ONE JSON line on rank 0.  `roofline` is computed for the persistent loop kernel from
+HIP events around its launch; `cpu_baseline` times the C oracle (oracle/, the CPU restatement)
+on a bounded slice of the same workload on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from wavernn_amd import synthetic as syn  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
+COND_BYTES_PER_ROW_STEP = 836  # 208 fp32 conditioning + 1 fp32 output
+
+
+def loop_weight_bytes(d: syn.FatchordDims) -> int:
+    """fp32 bytes of every weight one loop step reads (I, rnn1, rnn2, fc1-3)."""
+    r, f, a, nc = d.rnn_dims, d.fc_dims, d.aux_dims, d.n_classes
+    n = (r * (d.feat_dims + a + 1) + r) + (3 * r * r * 2 + 6 * r) + (3 * r * (r + a) + 3 * r * r + 6 * r) \
+        + (f * (r + a) + f) + (f * (f + a) + f) + (nc * f + nc)
+    return 4 * n
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--seconds", type=float, default=5.0, help="utterance length")
+    ap.add_argument("--mode", default="MOL", choices=["MOL", "RAW"])
+    ap.add_argument("--batched", action="store_true", help="fold-batched generate (target 11000, overlap 550)")
+    ap.add_argument("--cpu-steps", type=int, default=12000, help="oracle steps timed for cpu_baseline (0: skip)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from wavernn_amd.fatchord_version import WaveRNN
+    d = syn.DEFAULT_MOL if args.mode == "MOL" else syn.DEFAULT_RAW
+    state = syn.make_fatchord_state(d, 0)
+    model = WaveRNN(**d.ctor_kwargs()).to(dev)
+    model.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in state.items()}, strict=True)
+    T = syn.frames_for_seconds(args.seconds, d.sample_rate, d.hop_length)
+    mel = torch.from_numpy(syn.make_mel(d.feat_dims, T, seed=1 + rank))[None]
+    target, overlap = 11000, 550
+
+    def step(i):
+        return model.generate(mel, None, args.batched, target, overlap, True, seed=1000 * rank + i, verbose=False)
+
+    for i in range(args.warmup):
+        step(-1 - i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    loop_ms = []
+    t0 = time.perf_counter()
+    n_samples = 0
+    for i in range(args.steps):
+        out = step(i)
+        n_samples += out.shape[0]
+        loop_ms.append(model.loop_handle().elapsed_ms())
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    stats = torch.tensor([elapsed, float(np.mean(loop_ms))], dtype=torch.float64, device=dev)
+    tot = torch.tensor([float(n_samples)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    elapsed, loop_ms_max = float(stats[0]), float(stats[1])
+    total_samples = float(tot[0])
+
+    if rank == 0:
+        cond, _ = model.conditioning(mel, args.batched, target, overlap)
+        L, B, _ = cond.shape
+        wbytes = loop_weight_bytes(d)
+        bytes_per_launch = L * (wbytes + B * COND_BYTES_PER_ROW_STEP)
+        achieved = bytes_per_launch / (loop_ms_max / 1e3) / 1e9
+        value = total_samples / elapsed
+        info = model.loop_handle().info
+        rec = {
+            "metric": "audio samples/sec/GPU (22.05 kHz MoL, rnn_dims=512) + real-time factor at batch=1"
+            if args.mode == "MOL" else "audio samples/sec (22.05 kHz RAW 9-bit, rnn_dims=512)",
+            "value": value,
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic mel (seeded uniform [0,1)), random weights of the 800k MoL architecture",
+            "config": {
+                "workload": f"fatchord WaveRNN {args.mode} generate(), {args.seconds:g} s utterance per GPU, "
+                            f"{'fold-batched target 11000/overlap 550' if args.batched else 'unbatched (batch=1)'}",
+                "mode": args.mode, "rnn_dims": d.rnn_dims, "fc_dims": d.fc_dims, "utterance_s": args.seconds,
+                "loop_steps": L, "rows": B, "samples_per_utterance": int(n_samples / args.steps),
+                "parallelism": f"utterance-sharded x{world}", "grid": info["grid"],
+            },
+            "rtf_per_gpu": value / world / d.sample_rate,
+            "loop_kernel_ms": loop_ms_max,
+            "us_per_loop_step": loop_ms_max * 1e3 / L,
+            "roofline": {
+                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                "note": "algorithmic bytes = all loop weights (fp32) per step + 836 B/row-step, per launch; "
+                        "weights are LDS-resident so actual HBM traffic is far lower",
+            },
+        }
+        if args.cpu_steps > 0 and world == 1:
+            from oracle import oracle
+            cpu = cond.transpose(0, 1).cpu().numpy()
+            n = min(args.cpu_steps, L)
+            mels_c = np.ascontiguousarray(cpu[:, :n, :d.feat_dims])
+            aux_c = np.ascontiguousarray(cpu[:, :n, d.feat_dims:])
+            noise = syn.make_noise(d.mode, B, n, d.n_classes, 7)
+            oracle.build()
+            t = time.perf_counter()
+            oracle.fatchord_loop(state, d.mode, mels_c, aux_c, noise)
+            dt = time.perf_counter() - t
+            rec["cpu_baseline"] = {"value": n * B / dt, "unit": "samples/s", "cores": 1, "kind": "port",
+                                   "sample": f"{n} of {L} loop steps x {B} row(s), same weights/conditioning, "
+                                             f"C oracle (oracle/wavernn_oracle.c, gcc -O3, 1 thread)",
+                                   "seconds": dt}
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,120 @@
+/*
+ * wavernn_amd.h — C-ABI of the MI355X-native WaveRNN generation path.
+ *
+ * The reference has no FFI: its hot path is the Python method
+ *   WaveRNN.generate(mels, save_path, batched, target, overlap, mu_law)
+ *   (/root/reference/models/fatchord_version.py:169-264)
+ * whose per-sample loop (:201-241) dispatches ~40 eager torch ops per step.  This ABI is
+ * what that method binds instead (wavernn_amd/fatchord_version.py does it via ctypes; see
+ * INTEGRATION.md for the binding a reference maintainer would add).  Each entry point names
+ * the reference code it replaces.
+ *
+ * Conventions: plain pointers and sizes only; return 0 or a negative WRNN_E* code; no
+ * exception crosses the ABI; device pointers are HIP device pointers on the handle's device;
+ * `stream` is a hipStream_t (NULL = default stream); calls are asynchronous on that stream
+ * except where stated; one handle per device, not thread-safe.
+ */
+#ifndef WAVERNN_AMD_H
+#define WAVERNN_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WRNN_ABI_VERSION 1
+
+enum wrnn_status {
+    WRNN_OK = 0,
+    WRNN_EINVAL = -1,        /* bad argument / shape (message in wrnn_last_error)            */
+    WRNN_EHIP = -2,          /* a HIP runtime call failed                                    */
+    WRNN_ENOWEIGHTS = -3,    /* wrnn_generate before every required tensor was set           */
+    WRNN_ETIMEOUT = -4,      /* a persistent-kernel wait exceeded its bound (kernel aborted)  */
+    WRNN_ENOMEM = -5,
+    WRNN_EUNSUPPORTED = -6,  /* dims / device the kernel cannot run (e.g. LDS or residency)  */
+};
+
+enum wrnn_mode {             /* fatchord_version.py:97-104 */
+    WRNN_MODE_RAW = 0,       /* softmax over 2**bits classes, Categorical sample (:231-237) */
+    WRNN_MODE_MOL = 1,       /* 30-way mixture of logistics (:225-229)                       */
+};
+
+typedef struct wrnn_ctx wrnn_t;
+
+/* Model dims — the WaveRNN constructor arguments that shape the loop
+ * (fatchord_version.py:93-123; aux_dims = res_out_dims / 4 at :110). */
+typedef struct {
+    int32_t abi_version;     /* must be WRNN_ABI_VERSION */
+    int32_t mode;            /* enum wrnn_mode */
+    int32_t rnn_dims;
+    int32_t fc_dims;
+    int32_t aux_dims;
+    int32_t feat_dims;       /* num_mels */
+    int32_t n_classes;       /* 2**bits (RAW) or 30 (MOL) */
+    int32_t grid;            /* workgroups of the persistent kernel; 0 = auto (one per CU) */
+    int32_t timeout_ms;      /* bound on any single in-kernel wait; 0 = default (2000 ms) */
+} wrnn_config;
+
+/* One named weight, named exactly as the reference state_dict key
+ * (e.g. "rnn1.weight_ih_l0"), fp32 row-major in the reference shape. */
+typedef struct {
+    const char *name;
+    const float *data;
+    int64_t numel;
+    int32_t on_device;       /* 1: `data` is a device pointer, 0: host pointer */
+} wrnn_tensor;
+
+/* Launch geometry chosen for the handle (read-only). */
+typedef struct {
+    int32_t grid;            /* workgroups (all co-resident, one persistent launch) */
+    int32_t units_rnn;       /* hidden units per workgroup (GRU rows ×3)            */
+    int32_t units_fc;        /* fc1/fc2 rows per workgroup                          */
+    int32_t units_cls;       /* fc3 rows per workgroup (RAW; MOL computes all 30)   */
+    int32_t max_rows;        /* batch rows one launch holds; more are chunked       */
+    int32_t lds_bytes;       /* dynamic LDS per workgroup at max_rows                */
+    int32_t slab_floats;     /* resident weight floats per workgroup                 */
+    int32_t num_cus;
+} wrnn_info;
+
+/* Create a handle on `device` (replaces WaveRNN.__init__ for the loop's dims,
+ * fatchord_version.py:93-129).  Synchronous.  On failure *out may still hold a handle so
+ * the caller can read wrnn_last_error(); release it with wrnn_destroy. */
+int wrnn_create(const wrnn_config *cfg, int device, wrnn_t **out);
+
+/* Load weights by reference state_dict name (replaces WaveRNN.load → load_state_dict,
+ * fatchord_version.py:414-417, for the loop's tensors: I.*, rnn1.*, rnn2.*, fc1-3.*).
+ * Copies and packs into the kernel's per-workgroup layout; the caller keeps ownership.
+ * Unknown names are ignored (load_state_dict(strict=False)).  Synchronous. */
+int wrnn_set_weights(wrnn_t *h, const wrnn_tensor *tensors, int n);
+
+/* Run the whole sample loop (fatchord_version.py:192-241) for B rows × L steps.
+ *   cond   [L][B][feat_dims + 4·aux_dims]  upsampled mel ‖ aux, time-major (device)
+ *   noise  [L][B][K] injected draws in reference order, or NULL for in-kernel Philox:
+ *          MOL K = 11 (u1[10], u2 ∈ (1e-5, 1−1e-5), utils/distribution.py:106,118);
+ *          RAW K = n_classes (q ~ Exp(1); Categorical.sample ≡ argmax(probs/q))
+ *   seed, row_offset  Philox key and global id of row 0 (draws are keyed by
+ *          (seed, row_offset + b, step, k), so sharding rows across calls/GPUs is invariant)
+ *   out    [B][L] fp32 samples (the values appended at :227/:236)          (device)
+ *   labels [B][L] int32 class labels, RAW only, or NULL                     (device)
+ * Asynchronous on `stream`; kernel-side failures surface through wrnn_check. */
+int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise,
+                  uint64_t seed, int64_t row_offset, float *out, int32_t *labels, void *stream);
+
+/* Synchronise `stream` and report a persistent-kernel abort (WRNN_ETIMEOUT) from the
+ * last wrnn_generate on it.  The reference raises synchronously; this is that check. */
+int wrnn_check(wrnn_t *h, void *stream);
+
+/* Device time (ms, HIP events on the launch stream) from the first to the last persistent
+ * loop launch of the last wrnn_generate — the kernel time the roofline is computed from.
+ * Waits for that launch to finish. */
+int wrnn_elapsed_ms(wrnn_t *h, float *ms);
+
+int wrnn_query(const wrnn_t *h, wrnn_info *info);
+const char *wrnn_last_error(const wrnn_t *h);
+void wrnn_destroy(wrnn_t *h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WAVERNN_AMD_H */

@@ -1,0 +1,80 @@
+"""ctypes binding of the C-ABI (include/wavernn_amd.h) in libwavernn_amd.so.
+
+The product path has no fallback: if the HIP library is missing or cannot be loaded this
+module raises, it never substitutes a CPU implementation."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_lib", "libwavernn_amd.so")
+
+ABI_VERSION = 1
+MODE_RAW, MODE_MOL = 0, 1
+STATUS = {0: "WRNN_OK", -1: "WRNN_EINVAL", -2: "WRNN_EHIP", -3: "WRNN_ENOWEIGHTS", -4: "WRNN_ETIMEOUT",
+          -5: "WRNN_ENOMEM", -6: "WRNN_EUNSUPPORTED"}
+
+# Every symbol include/wavernn_amd.h declares (tests check the .so exports all of them).
+EXPORTS = ("wrnn_create", "wrnn_set_weights", "wrnn_generate", "wrnn_check", "wrnn_elapsed_ms",
+           "wrnn_query", "wrnn_last_error", "wrnn_destroy")
+
+
+class WrnnError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{STATUS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class Config(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("abi_version", "mode", "rnn_dims", "fc_dims", "aux_dims",
+                                              "feat_dims", "n_classes", "grid", "timeout_ms")]
+
+
+class Tensor(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("data", ctypes.c_void_p), ("numel", ctypes.c_int64),
+                ("on_device", ctypes.c_int32)]
+
+
+class Info(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("grid", "units_rnn", "units_fc", "units_cls", "max_rows",
+                                              "lds_bytes", "slab_floats", "num_cus")]
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libwavernn_amd.so (built in-tree by __graft_entry__.build())."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build the HIP extension with "
+                          "`python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64, u64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint64
+    L.wrnn_create.argtypes = [ctypes.POINTER(Config), i32, ctypes.POINTER(vp)]
+    L.wrnn_create.restype = i32
+    L.wrnn_set_weights.argtypes = [vp, ctypes.POINTER(Tensor), i32]
+    L.wrnn_set_weights.restype = i32
+    L.wrnn_generate.argtypes = [vp, vp, i32, i32, vp, u64, i64, vp, vp, vp]
+    L.wrnn_generate.restype = i32
+    L.wrnn_check.argtypes = [vp, vp]
+    L.wrnn_check.restype = i32
+    L.wrnn_elapsed_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
+    L.wrnn_elapsed_ms.restype = i32
+    L.wrnn_query.argtypes = [vp, ctypes.POINTER(Info)]
+    L.wrnn_query.restype = i32
+    L.wrnn_last_error.argtypes = [vp]
+    L.wrnn_last_error.restype = ctypes.c_char_p
+    L.wrnn_destroy.argtypes = [vp]
+    L.wrnn_destroy.restype = None
+    _lib = L
+    return L
+
+
+def check(handle, code: int):
+    if code != 0:
+        msg = lib().wrnn_last_error(handle) if handle else b""
+        raise WrnnError(code, (msg or b"").decode(errors="replace"))

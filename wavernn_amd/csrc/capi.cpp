@@ -1,0 +1,381 @@
+// capi.cpp — host side of the C-ABI declared in include/wavernn_amd.h.
+//
+// Owns the device state of one WaveRNN loop: the per-workgroup weight slabs (packed from
+// reference state_dict tensors), the I-layer weights for the conditioning GEMM, the
+// conditioning-projection workspace, the hand-off granules and the control words.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/wavernn_amd.h"
+#include "fatchord_loop.h"
+
+namespace wrnn {
+hipError_t launch_ci_gemm(const float *cond, int CD, int Bt, int b0, int Bc, int L, const float *W, int ldw,
+                          const float *bias, int N, int K, float *cI, hipStream_t st);
+hipError_t launch_loop(const LoopArgs &a, size_t lds_bytes, hipStream_t st);
+hipError_t prepare_loop_kernel(int max_lds_bytes);
+hipError_t loop_occupancy(int *blocks_per_cu, size_t lds_bytes);
+}  // namespace wrnn
+
+using namespace wrnn;
+
+struct wrnn_ctx {
+    wrnn_config cfg{};
+    int device = 0;
+    int num_cus = 0;
+    int max_lds = 0;
+    int G = 0, U = 0, UF = 0, UC = 0, NMAX = 0, NK = 0, CD = 0;
+    int max_rows = 0;
+    SlabLayout s{};
+    std::map<std::string, std::vector<float>> w;   // loop tensors, host copies
+    bool ready = false;
+    float *d_slab = nullptr, *d_IW = nullptr, *d_Ib = nullptr;
+    float *d_cI = nullptr;
+    size_t cI_cap = 0;                              // floats
+    unsigned long long *d_xg = nullptr;
+    size_t xg_cap = 0;                              // granules
+    int *d_ctl = nullptr;
+    long long timeout_ticks = 0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+    std::string err;
+};
+
+namespace {
+
+const int kCtlWords = 8;
+
+int fail(wrnn_t *h, int code, const std::string &msg) {
+    if (h) h->err = msg;
+    return code;
+}
+
+#define HIP_TRY(h, expr)                                                                      \
+    do {                                                                                      \
+        hipError_t _e = (expr);                                                               \
+        if (_e != hipSuccess)                                                                 \
+            return fail((h), WRNN_EHIP, std::string(#expr) + ": " + hipGetErrorString(_e));   \
+    } while (0)
+
+struct Need {
+    const char *name;
+    int64_t rows, cols;
+};
+
+std::vector<Need> required(const wrnn_config &c) {
+    const int64_t R = c.rnn_dims, F = c.fc_dims, A = c.aux_dims, M = c.feat_dims, NC = c.n_classes;
+    return {{"I.weight", R, 1 + M + A},      {"I.bias", R, 1},
+            {"rnn1.weight_ih_l0", 3 * R, R}, {"rnn1.weight_hh_l0", 3 * R, R},
+            {"rnn1.bias_ih_l0", 3 * R, 1},   {"rnn1.bias_hh_l0", 3 * R, 1},
+            {"rnn2.weight_ih_l0", 3 * R, R + A}, {"rnn2.weight_hh_l0", 3 * R, R},
+            {"rnn2.bias_ih_l0", 3 * R, 1},   {"rnn2.bias_hh_l0", 3 * R, 1},
+            {"fc1.weight", F, R + A},        {"fc1.bias", F, 1},
+            {"fc2.weight", F, F + A},        {"fc2.bias", F, 1},
+            {"fc3.weight", NC, F},           {"fc3.bias", NC, 1}};
+}
+
+SlabLayout make_slab_layout(const wrnn_ctx &h) {
+    const int R = h.cfg.rnn_dims, F = h.cfg.fc_dims, A = h.cfg.aux_dims, NC = h.cfg.n_classes;
+    const bool mol = h.cfg.mode == WRNN_MODE_MOL;
+    SlabLayout s{};
+    int o = 0;
+    auto take = [&](int n) { int at = o; o += round4(n); return at; };
+    s.wih1 = take(3 * h.U * R);
+    s.whh1 = take(3 * h.U * R);
+    s.wih2 = take(3 * h.U * (R + A));
+    s.whh2 = take(3 * h.U * R);
+    s.bih1 = take(3 * h.U);
+    s.bhh1 = take(3 * h.U);
+    s.bih2 = take(3 * h.U);
+    s.bhh2 = take(3 * h.U);
+    s.w1 = take(h.UF * (R + A));
+    s.b1 = take(h.UF);
+    s.w2 = take(h.UF * (F + A));
+    s.b2 = take(h.UF);
+    s.w3 = take((mol ? NC : h.UC) * F);
+    s.b3 = take(mol ? NC : h.UC);
+    s.wi0 = take(R);
+    s.total = o;
+    return s;
+}
+
+// Pack workgroup w's rows: GRU gate rows (g·R + j) for owned units j, fc rows, fc3 rows.
+void pack_slab(const wrnn_ctx &h, int w, float *out) {
+    const int R = h.cfg.rnn_dims, F = h.cfg.fc_dims, A = h.cfg.aux_dims, NC = h.cfg.n_classes;
+    const bool mol = h.cfg.mode == WRNN_MODE_MOL;
+    const SlabLayout &s = h.s;
+    std::fill(out, out + s.total, 0.0f);
+    auto W = [&](const char *n) { return h.w.at(n).data(); };
+    for (int u = 0; u < h.U; ++u) {
+        const int j = w * h.U + u;
+        if (j >= R) continue;
+        for (int g = 0; g < 3; ++g) {
+            const int src = g * R + j, dst = g * h.U + u;
+            std::memcpy(out + s.wih1 + (size_t)dst * R, W("rnn1.weight_ih_l0") + (size_t)src * R, R * 4);
+            std::memcpy(out + s.whh1 + (size_t)dst * R, W("rnn1.weight_hh_l0") + (size_t)src * R, R * 4);
+            std::memcpy(out + s.wih2 + (size_t)dst * (R + A), W("rnn2.weight_ih_l0") + (size_t)src * (R + A),
+                        (R + A) * 4);
+            std::memcpy(out + s.whh2 + (size_t)dst * R, W("rnn2.weight_hh_l0") + (size_t)src * R, R * 4);
+            out[s.bih1 + dst] = W("rnn1.bias_ih_l0")[src];
+            out[s.bhh1 + dst] = W("rnn1.bias_hh_l0")[src];
+            out[s.bih2 + dst] = W("rnn2.bias_ih_l0")[src];
+            out[s.bhh2 + dst] = W("rnn2.bias_hh_l0")[src];
+        }
+    }
+    for (int r = 0; r < h.UF; ++r) {
+        const int j = w * h.UF + r;
+        if (j >= F) continue;
+        std::memcpy(out + s.w1 + (size_t)r * (R + A), W("fc1.weight") + (size_t)j * (R + A), (R + A) * 4);
+        std::memcpy(out + s.w2 + (size_t)r * (F + A), W("fc2.weight") + (size_t)j * (F + A), (F + A) * 4);
+        out[s.b1 + r] = W("fc1.bias")[j];
+        out[s.b2 + r] = W("fc2.bias")[j];
+    }
+    if (mol) {
+        std::memcpy(out + s.w3, W("fc3.weight"), (size_t)NC * F * 4);
+        std::memcpy(out + s.b3, W("fc3.bias"), (size_t)NC * 4);
+    } else {
+        for (int r = 0; r < h.UC; ++r) {
+            const int j = w * h.UC + r;
+            if (j >= NC) continue;
+            std::memcpy(out + s.w3 + (size_t)r * F, W("fc3.weight") + (size_t)j * F, F * 4);
+            out[s.b3 + r] = W("fc3.bias")[j];
+        }
+    }
+    const float *IW = W("I.weight");
+    const int nin = 1 + h.cfg.feat_dims + A;
+    for (int j = 0; j < R; ++j) out[s.wi0 + j] = IW[(size_t)j * nin];
+}
+
+size_t lds_bytes_for(const wrnn_ctx &h, int Bc) {
+    return (size_t)lds_layout(h.s.total, Bc, h.cfg.rnn_dims, h.cfg.fc_dims, h.cfg.aux_dims, h.cfg.n_classes, h.NK)
+               .total * sizeof(float);
+}
+
+}  // namespace
+
+extern "C" {
+
+int wrnn_create(const wrnn_config *cfg, int device, wrnn_t **out) {
+    if (!out || !cfg) return WRNN_EINVAL;
+    *out = nullptr;
+    if (cfg->abi_version != WRNN_ABI_VERSION) return WRNN_EINVAL;
+    auto *h = new (std::nothrow) wrnn_ctx();
+    if (!h) return WRNN_ENOMEM;
+    *out = h;
+    h->cfg = *cfg;
+    h->device = device;
+    const wrnn_config &c = h->cfg;
+    const bool mol = c.mode == WRNN_MODE_MOL;
+    if (c.mode != WRNN_MODE_MOL && c.mode != WRNN_MODE_RAW) return fail(h, WRNN_EINVAL, "unknown mode");
+    if (c.rnn_dims <= 0 || c.fc_dims <= 0 || c.aux_dims <= 0 || c.feat_dims <= 0 || c.n_classes <= 0)
+        return fail(h, WRNN_EINVAL, "dims must be positive");
+    if (c.rnn_dims % 4 || c.fc_dims % 4 || c.aux_dims % 4)
+        return fail(h, WRNN_EUNSUPPORTED, "rnn_dims, fc_dims and aux_dims must be multiples of 4");
+    if (mol && c.n_classes != 30) return fail(h, WRNN_EINVAL, "MOL mode has n_classes = 30 (10 logistics)");
+    if (!mol && c.n_classes > 64 * kClsPerLaneMax)
+        return fail(h, WRNN_EUNSUPPORTED, "RAW n_classes > 512 (bits > 9) not supported");
+    HIP_TRY(h, hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIP_TRY(h, hipGetDeviceProperties(&prop, device));
+    h->num_cus = prop.multiProcessorCount;
+    h->max_lds = std::max<int>((int)prop.sharedMemPerBlock, (int)prop.maxSharedMemoryPerMultiProcessor);
+    h->max_lds = std::min(h->max_lds, 160 * 1024);
+    const int R = c.rnn_dims, F = c.fc_dims;
+    const int gtarget = c.grid > 0 ? c.grid : h->num_cus;
+    h->U = (R + gtarget - 1) / gtarget;
+    h->G = (R + h->U - 1) / h->U;
+    h->UF = (F + h->G - 1) / h->G;
+    h->UC = mol ? 0 : (c.n_classes + h->G - 1) / h->G;
+    h->NMAX = std::max(R, std::max(F, c.n_classes));
+    h->NK = mol ? 11 : c.n_classes;
+    h->CD = c.feat_dims + 4 * c.aux_dims;
+    h->s = make_slab_layout(*h);
+    // rows per launch: LDS, and the per-thread gather register budget
+    h->max_rows = 0;
+    for (int b = 1; b <= 64; ++b) {
+        if (lds_bytes_for(*h, b) > (size_t)h->max_lds) break;
+        if ((size_t)b * h->NMAX > (size_t)kPollThreads * kGatherMax) break;
+        h->max_rows = b;
+    }
+    if (h->max_rows < 1)
+        return fail(h, WRNN_EUNSUPPORTED, "weight slab + one row of state exceeds LDS (" +
+                                              std::to_string(lds_bytes_for(*h, 1)) + " B)");
+    HIP_TRY(h, prepare_loop_kernel(h->max_lds));
+    int per_cu = 0;
+    HIP_TRY(h, loop_occupancy(&per_cu, lds_bytes_for(*h, h->max_rows)));
+    if (per_cu * h->num_cus < h->G)
+        return fail(h, WRNN_EUNSUPPORTED, "persistent grid of " + std::to_string(h->G) +
+                                              " workgroups is not co-resident (" + std::to_string(per_cu) +
+                                              "/CU × " + std::to_string(h->num_cus) + " CUs)");
+    h->timeout_ticks = (long long)(c.timeout_ms > 0 ? c.timeout_ms : 2000) * 100000LL;   // 100 MHz
+    HIP_TRY(h, hipMalloc(&h->d_ctl, kCtlWords * sizeof(int)));
+    HIP_TRY(h, hipMemset(h->d_ctl, 0, kCtlWords * sizeof(int)));
+    HIP_TRY(h, hipEventCreate(&h->ev0));
+    HIP_TRY(h, hipEventCreate(&h->ev1));
+    return WRNN_OK;
+}
+
+int wrnn_set_weights(wrnn_t *h, const wrnn_tensor *tensors, int n) {
+    if (!h || (n > 0 && !tensors)) return WRNN_EINVAL;
+    HIP_TRY(h, hipSetDevice(h->device));
+    const auto need = required(h->cfg);
+    for (int i = 0; i < n; ++i) {
+        const wrnn_tensor &t = tensors[i];
+        if (!t.name || !t.data) return fail(h, WRNN_EINVAL, "null tensor name/data");
+        auto it = std::find_if(need.begin(), need.end(), [&](const Need &q) { return t.name == std::string(q.name); });
+        if (it == need.end()) continue;   // load_state_dict(strict=False): ignore others
+        if (t.numel != it->rows * it->cols)
+            return fail(h, WRNN_EINVAL, std::string(t.name) + ": expected " + std::to_string(it->rows * it->cols) +
+                                            " elements, got " + std::to_string(t.numel));
+        std::vector<float> v((size_t)t.numel);
+        if (t.on_device)
+            HIP_TRY(h, hipMemcpy(v.data(), t.data, (size_t)t.numel * 4, hipMemcpyDeviceToHost));
+        else
+            std::memcpy(v.data(), t.data, (size_t)t.numel * 4);
+        h->w[t.name] = std::move(v);
+    }
+    for (const auto &q : need)
+        if (!h->w.count(q.name)) { h->ready = false; return WRNN_OK; }   // partial load so far
+    // pack and upload
+    std::vector<float> slab((size_t)h->G * h->s.total);
+    for (int w = 0; w < h->G; ++w) pack_slab(*h, w, slab.data() + (size_t)w * h->s.total);
+    if (!h->d_slab) HIP_TRY(h, hipMalloc(&h->d_slab, slab.size() * 4));
+    HIP_TRY(h, hipMemcpy(h->d_slab, slab.data(), slab.size() * 4, hipMemcpyHostToDevice));
+    const auto &IW = h->w.at("I.weight");
+    const auto &Ib = h->w.at("I.bias");
+    if (!h->d_IW) HIP_TRY(h, hipMalloc(&h->d_IW, IW.size() * 4));
+    if (!h->d_Ib) HIP_TRY(h, hipMalloc(&h->d_Ib, Ib.size() * 4));
+    HIP_TRY(h, hipMemcpy(h->d_IW, IW.data(), IW.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(h, hipMemcpy(h->d_Ib, Ib.data(), Ib.size() * 4, hipMemcpyHostToDevice));
+    h->ready = true;
+    return WRNN_OK;
+}
+
+int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed,
+                  int64_t row_offset, float *out, int32_t *labels, void *stream) {
+    if (!h) return WRNN_EINVAL;
+    if (!h->ready) return fail(h, WRNN_ENOWEIGHTS, "weights not (fully) set");
+    if (B <= 0 || L <= 0 || !cond || !out) return fail(h, WRNN_EINVAL, "need B > 0, L > 0, cond and out");
+    if (labels && h->cfg.mode != WRNN_MODE_RAW) return fail(h, WRNN_EINVAL, "labels are a RAW-mode output");
+    HIP_TRY(h, hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    const wrnn_config &c = h->cfg;
+    const int R = c.rnn_dims;
+    const int Bc_max = std::min(B, h->max_rows);
+    // workspaces (grow-only)
+    const size_t need_cI = (size_t)L * Bc_max * R;
+    if (need_cI > h->cI_cap) {
+        if (h->d_cI) HIP_TRY(h, hipFree(h->d_cI));
+        h->d_cI = nullptr;
+        HIP_TRY(h, hipMalloc(&h->d_cI, need_cI * 4));
+        h->cI_cap = need_cI;
+    }
+    const size_t need_xg = (size_t)kHops * Bc_max * h->NMAX;
+    if (need_xg > h->xg_cap) {
+        if (h->d_xg) HIP_TRY(h, hipFree(h->d_xg));
+        h->d_xg = nullptr;
+        HIP_TRY(h, hipMalloc(&h->d_xg, need_xg * 8));
+        h->xg_cap = need_xg;
+    }
+    HIP_TRY(h, hipMemsetAsync(h->d_ctl, 0, kCtlWords * sizeof(int), st));
+    for (int b0 = 0; b0 < B; b0 += h->max_rows) {
+        const int Bc = std::min(h->max_rows, B - b0);
+        HIP_TRY(h, launch_ci_gemm(cond, h->CD, B, b0, Bc, L, h->d_IW, 1 + c.feat_dims + c.aux_dims, h->d_Ib, R,
+                                  c.feat_dims + c.aux_dims, h->d_cI, st));
+        HIP_TRY(h, hipMemsetAsync(h->d_xg, 0, (size_t)kHops * Bc * h->NMAX * 8, st));
+        LoopArgs a{};
+        a.slab = h->d_slab;
+        a.cI = h->d_cI;
+        a.cond = cond;
+        a.noise = noise;
+        a.out = out;
+        a.labels = labels;
+        a.xg = h->d_xg;
+        a.ctl = h->d_ctl;
+        a.seed = seed;
+        a.row0 = row_offset + b0;
+        a.timeout_ticks = h->timeout_ticks;
+        a.L = L;
+        a.Bc = Bc;
+        a.Bt = B;
+        a.b0 = b0;
+        a.R = R;
+        a.F = c.fc_dims;
+        a.A = c.aux_dims;
+        a.CD = h->CD;
+        a.feat = c.feat_dims;
+        a.NC = c.n_classes;
+        a.NK = h->NK;
+        a.mol = c.mode == WRNN_MODE_MOL;
+        a.U = h->U;
+        a.UF = h->UF;
+        a.UC = h->UC;
+        a.G = h->G;
+        a.NMAX = h->NMAX;
+        a.s = h->s;
+        if (b0 == 0) HIP_TRY(h, hipEventRecord(h->ev0, st));
+        HIP_TRY(h, launch_loop(a, lds_bytes_for(*h, Bc), st));
+    }
+    HIP_TRY(h, hipEventRecord(h->ev1, st));
+    h->timed = true;
+    return WRNN_OK;
+}
+
+int wrnn_check(wrnn_t *h, void *stream) {
+    if (!h) return WRNN_EINVAL;
+    HIP_TRY(h, hipSetDevice(h->device));
+    HIP_TRY(h, hipStreamSynchronize((hipStream_t)stream));
+    int ctl[kCtlWords];
+    HIP_TRY(h, hipMemcpy(ctl, h->d_ctl, sizeof(ctl), hipMemcpyDeviceToHost));
+    if (ctl[1] != 0) {
+        static const char *hops[] = {"h1", "h2", "f1", "f2", "logits"};
+        const int hop = ctl[3];
+        return fail(h, WRNN_ETIMEOUT,
+                    "persistent kernel aborted: wait on hand-off '" + std::string(hop >= 0 && hop < 5 ? hops[hop] : "?") +
+                        "' at step " + std::to_string(ctl[2]) + " in workgroup " + std::to_string(ctl[4]) +
+                        " exceeded the timeout (grid not co-resident, or a fault)");
+    }
+    return WRNN_OK;
+}
+
+int wrnn_elapsed_ms(wrnn_t *h, float *ms) {
+    if (!h || !ms) return WRNN_EINVAL;
+    if (!h->timed) return fail(h, WRNN_EINVAL, "no wrnn_generate recorded yet");
+    HIP_TRY(h, hipEventSynchronize(h->ev1));
+    HIP_TRY(h, hipEventElapsedTime(ms, h->ev0, h->ev1));
+    return WRNN_OK;
+}
+
+int wrnn_query(const wrnn_t *h, wrnn_info *info) {
+    if (!h || !info) return WRNN_EINVAL;
+    info->grid = h->G;
+    info->units_rnn = h->U;
+    info->units_fc = h->UF;
+    info->units_cls = h->UC;
+    info->max_rows = h->max_rows;
+    info->lds_bytes = (int)lds_bytes_for(*h, h->max_rows);
+    info->slab_floats = h->s.total;
+    info->num_cus = h->num_cus;
+    return WRNN_OK;
+}
+
+const char *wrnn_last_error(const wrnn_t *h) { return h ? h->err.c_str() : "null handle"; }
+
+void wrnn_destroy(wrnn_t *h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    if (h->ev0) (void)hipEventDestroy(h->ev0);
+    if (h->ev1) (void)hipEventDestroy(h->ev1);
+    for (void *p : {(void *)h->d_slab, (void *)h->d_IW, (void *)h->d_Ib, (void *)h->d_cI, (void *)h->d_xg,
+                    (void *)h->d_ctl})
+        if (p) (void)hipFree(p);
+    delete h;
+}
+
+}  // extern "C"

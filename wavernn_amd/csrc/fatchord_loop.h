@@ -1,0 +1,75 @@
+// Shared between the host launcher (capi.cpp) and the device code (fatchord_loop.hip).
+#pragma once
+#include <stdint.h>
+
+namespace wrnn {
+
+// Wave roles.  vmcnt is in-order per wave, so a wave that polls hand-off granules must not
+// have slow loads (next step's conditioning) or its own publish stores outstanding:
+//   waves 0,1  poll (gather); compute only when a stage has more than 2 work items
+//   waves 2,3  compute + publish
+//   wave  4    loader: LDS-DMA of step t+1's record, Philox noise, output stores.  It never
+//              reads LDS while its DMA is in flight (hipcc would drain vmcnt before the read).
+constexpr int kCompute = 256;          // waves 0..3
+constexpr int kWaves = kCompute / 64;
+constexpr int kThreads = kCompute + 64;
+constexpr int kLoaderWave = 4;
+constexpr int kPollThreads = 128;
+constexpr int kGatherMax = 8;          // granules per polling thread per hand-off
+constexpr int kClsPerLaneMax = 8;      // RAW softmax classes per lane (n_classes <= 512)
+constexpr int kHops = 5;               // h1, h2, f1, f2, logits(RAW)
+
+enum Hop { HOP_H1 = 0, HOP_H2 = 1, HOP_F1 = 2, HOP_F2 = 3, HOP_LOGITS = 4 };
+
+// Per-workgroup slab offsets (floats) of the resident weights.
+struct SlabLayout {
+    int wih1, whh1, wih2, whh2, bih1, bhh1, bih2, bhh2, w1, b1, w2, b2, w3, b3, wi0, total;
+};
+
+struct LoopArgs {
+    const float *slab;            // [G][slab.total]
+    const float *cI;              // [L][Bc][R]   I-layer conditioning projection (+bias)
+    const float *cond;            // [L][Bt][CD]  mel ‖ aux
+    const float *noise;           // [L][Bt][NK] or nullptr (Philox)
+    float *out;                   // [Bt][L]
+    int32_t *labels;              // [Bt][L] or nullptr
+    unsigned long long *xg;       // [kHops][Bc * NMAX] granules {tag:32 | value:32}
+    int *ctl;                     // [0] abort, [1] error code, [2] step, [3] hop, [4] wg
+    unsigned long long seed;
+    long long row0;               // global row id of chunk row 0 (Philox key)
+    long long timeout_ticks;      // s_memrealtime ticks (100 MHz)
+    int L, Bc, Bt, b0;
+    int R, F, A, CD, feat, NC, NK, mol;
+    int U, UF, UC, G, NMAX;
+    SlabLayout s;
+};
+
+// Dynamic-LDS layout (floats) for Bc rows; shared by host sizing and the kernel.
+struct LdsLayout {
+    int slab, h1, h2, xa, fa, f2, lg, pre, xprev, lbl, flag, total;
+    int ncp, pp;
+};
+
+__host__ __device__ inline int round4(int x) { return (x + 3) & ~3; }
+
+__host__ __device__ inline LdsLayout lds_layout(int slab_total, int Bc, int R, int F, int A, int NC, int NK) {
+    LdsLayout l;
+    l.ncp = round4(NC);
+    l.pp = round4(R + 3 * A + NK);
+    int o = 0;
+    l.slab = o;  o += round4(slab_total);
+    l.h1 = o;    o += Bc * R;
+    l.h2 = o;    o += Bc * R;
+    l.xa = o;    o += Bc * (R + A);
+    l.fa = o;    o += Bc * (F + A);
+    l.f2 = o;    o += Bc * F;
+    l.lg = o;    o += Bc * l.ncp;
+    l.pre = o;   o += 2 * Bc * l.pp;
+    l.xprev = o; o += round4(Bc);
+    l.lbl = o;   o += round4(Bc);
+    l.flag = o;  o += 4;
+    l.total = o;
+    return l;
+}
+
+}  // namespace wrnn

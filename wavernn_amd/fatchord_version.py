@@ -1,0 +1,316 @@
+"""Drop-in `WaveRNN` for models/fatchord_version.py whose generate() runs on MI355X.
+
+Same constructor, submodule names, state_dict keys (so `load()` takes the reference's
+`*.pyt` checkpoints), `get_step`, `load`, `save` and `generate(mels, save_path, batched,
+target, overlap, mu_law)` contract as the reference (fatchord_version.py:92-435).  What
+changes is where the sample loop runs: instead of the host-driven per-step loop
+(:201-241), generate() packs the upsampled conditioning time-major and calls ONE persistent
+HIP kernel through the C-ABI (`FatchordLoop`).  There is no CPU fallback: the model must
+live on a GPU and the HIP library must be built, otherwise generate() raises.
+
+Pre-processing (pad, UpsampleNetwork, fold) runs as torch ops on the GPU; post-processing
+(mu-law, cross-fade/unfold, fade-out) is the reference's float64 numpy arithmetic.
+"""
+from __future__ import annotations
+
+import time
+from pathlib import Path
+from typing import Optional, Union
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import dsp
+from .loop import LOOP_KEYS, FatchordLoop, noise_width
+
+
+# --------------------------------------------------------------------- upsample network
+class ResBlock(nn.Module):
+    """1×1 conv → BN → ReLU → 1×1 conv → BN, plus identity (fatchord_version.py:13-28)."""
+
+    def __init__(self, dims):
+        super().__init__()
+        self.conv1 = nn.Conv1d(dims, dims, kernel_size=1, bias=False)
+        self.conv2 = nn.Conv1d(dims, dims, kernel_size=1, bias=False)
+        self.batch_norm1 = nn.BatchNorm1d(dims)
+        self.batch_norm2 = nn.BatchNorm1d(dims)
+
+    def forward(self, x):
+        y = F.relu(self.batch_norm1(self.conv1(x)))
+        return self.batch_norm2(self.conv2(y)) + x
+
+
+class MelResNet(nn.Module):
+    """Valid conv (k = 2·pad+1) → BN → ReLU → res blocks → 1×1 conv (fatchord_version.py:31-48)."""
+
+    def __init__(self, res_blocks, in_dims, compute_dims, res_out_dims, pad):
+        super().__init__()
+        self.conv_in = nn.Conv1d(in_dims, compute_dims, kernel_size=2 * pad + 1, bias=False)
+        self.batch_norm = nn.BatchNorm1d(compute_dims)
+        self.layers = nn.ModuleList([ResBlock(compute_dims) for _ in range(res_blocks)])
+        self.conv_out = nn.Conv1d(compute_dims, res_out_dims, kernel_size=1)
+
+    def forward(self, x):
+        x = F.relu(self.batch_norm(self.conv_in(x)))
+        for layer in self.layers:
+            x = layer(x)
+        return self.conv_out(x)
+
+
+class Stretch2d(nn.Module):
+    """Nearest-neighbour repeat along (freq, time) (fatchord_version.py:51-61)."""
+
+    def __init__(self, x_scale, y_scale):
+        super().__init__()
+        self.x_scale, self.y_scale = x_scale, y_scale
+
+    def forward(self, x):
+        return x.repeat_interleave(self.y_scale, dim=2).repeat_interleave(self.x_scale, dim=3)
+
+
+class UpsampleNetwork(nn.Module):
+    """MelResNet aux features stretched ×hop, and the mel upsampled by per-factor
+    stretch + (1, 2s+1) box convs, cropped by pad·hop each side (fatchord_version.py:64-89).
+    Returns (mels [B][L][feat], aux [B][L][res_out]) as contiguous time-major tensors."""
+
+    def __init__(self, feat_dims, upsample_scales, compute_dims, res_blocks, res_out_dims, pad):
+        super().__init__()
+        total_scale = int(np.prod(upsample_scales))
+        self.indent = pad * total_scale
+        self.resnet = MelResNet(res_blocks, feat_dims, compute_dims, res_out_dims, pad)
+        self.resnet_stretch = Stretch2d(total_scale, 1)
+        self.up_layers = nn.ModuleList()
+        for scale in upsample_scales:
+            k = 2 * scale + 1
+            conv = nn.Conv2d(1, 1, kernel_size=(1, k), padding=(0, scale), bias=False)
+            conv.weight.data.fill_(1.0 / k)
+            self.up_layers.append(Stretch2d(scale, 1))
+            self.up_layers.append(conv)
+
+    def forward(self, m):
+        aux = self.resnet_stretch(self.resnet(m).unsqueeze(1)).squeeze(1)
+        m = m.unsqueeze(1)
+        for f in self.up_layers:
+            m = f(m)
+        m = m.squeeze(1)[:, :, self.indent:-self.indent]
+        return m.transpose(1, 2), aux.transpose(1, 2)
+
+
+# ------------------------------------------------------------------------------ model
+class WaveRNN(nn.Module):
+    def __init__(self, rnn_dims, fc_dims, bits, pad, upsample_factors, feat_dims, compute_dims,
+                 res_out_dims, res_blocks, hop_length, sample_rate, mode='RAW'):
+        super().__init__()
+        self.mode = mode
+        self.pad = pad
+        if mode == 'RAW':
+            self.n_classes = 2 ** bits
+        elif mode == 'MOL':
+            self.n_classes = 30
+        else:
+            raise RuntimeError("Unknown model mode value - ", mode)
+        self.rnn_dims = rnn_dims
+        self.fc_dims = fc_dims
+        self.feat_dims = feat_dims
+        self.aux_dims = res_out_dims // 4
+        self.hop_length = hop_length
+        self.sample_rate = sample_rate
+        self.upsample = UpsampleNetwork(feat_dims, upsample_factors, compute_dims, res_blocks, res_out_dims, pad)
+        self.I = nn.Linear(feat_dims + self.aux_dims + 1, rnn_dims)
+        self.rnn1 = nn.GRU(rnn_dims, rnn_dims, batch_first=True)
+        self.rnn2 = nn.GRU(rnn_dims + self.aux_dims, rnn_dims, batch_first=True)
+        self.fc1 = nn.Linear(rnn_dims + self.aux_dims, fc_dims)
+        self.fc2 = nn.Linear(fc_dims + self.aux_dims, fc_dims)
+        self.fc3 = nn.Linear(fc_dims, self.n_classes)
+        self.register_buffer('step', torch.zeros(1, dtype=torch.long))
+        self.num_params()
+        self._loop: Optional[FatchordLoop] = None
+        self._loop_key = None
+        self.last_gen_seconds = 0.0
+
+    # -------------------------------------------------------------- training forward
+    def forward(self, x, mels):
+        """Teacher-forced forward (fatchord_version.py:131-167); training is out of scope for
+        the MI355X path, this keeps the module usable with the reference's train loop."""
+        self.step += 1
+        b = x.size(0)
+        h1 = torch.zeros(1, b, self.rnn_dims, device=x.device)
+        h2 = torch.zeros(1, b, self.rnn_dims, device=x.device)
+        mels, aux = self.upsample(mels)
+        a1, a2, a3, a4 = aux.split(self.aux_dims, dim=2)
+        x = self.I(torch.cat([x.unsqueeze(-1), mels, a1], dim=2))
+        res = x
+        x, _ = self.rnn1(x, h1)
+        x = x + res
+        res = x
+        x, _ = self.rnn2(torch.cat([x, a2], dim=2), h2)
+        x = x + res
+        x = F.relu(self.fc1(torch.cat([x, a3], dim=2)))
+        x = F.relu(self.fc2(torch.cat([x, a4], dim=2)))
+        return self.fc3(x)
+
+    # -------------------------------------------------------------------- loop handle
+    def _loop_params(self):
+        sd = dict(self.named_parameters())
+        return {k: sd[k] for k in LOOP_KEYS}
+
+    def loop_handle(self, grid: int = 0) -> FatchordLoop:
+        """The device handle, (re)packed whenever the loop weights changed (load, training)."""
+        device = next(self.parameters()).device
+        if device.type != 'cuda':
+            raise RuntimeError("WaveRNN.generate runs on the MI355X HIP path: move the model to a GPU "
+                               "(model.to('cuda')); there is no CPU fallback")
+        params = self._loop_params()
+        key = (device.index or 0, grid) + tuple((p.data_ptr(), p._version) for p in params.values())
+        if self._loop is None or self._loop_key is None or self._loop_key[:2] != key[:2]:
+            if self._loop is not None:
+                self._loop.close()
+            self._loop = FatchordLoop(self.mode, self.rnn_dims, self.fc_dims, self.aux_dims, self.feat_dims,
+                                      self.n_classes, device=device.index or 0, grid=grid)
+            self._loop_key = None
+        if self._loop_key != key:
+            self._loop.set_weights(params)
+            self._loop_key = key
+        return self._loop
+
+    # ---------------------------------------------------------------------- generate
+    def conditioning(self, mels, batched, target, overlap):
+        """pad → upsample → (fold) → time-major [L][B][feat + 4·aux] (fatchord_version.py:183-190)."""
+        device = next(self.parameters()).device
+        mels = torch.as_tensor(mels, device=device).to(torch.float32)
+        wave_len = (mels.size(-1) - 1) * self.hop_length
+        mels = self.pad_tensor(mels.transpose(1, 2), pad=self.pad, side='both')
+        mels, aux = self.upsample(mels.transpose(1, 2))
+        if batched:
+            mels = self.fold_with_overlap(mels, target, overlap)
+            aux = self.fold_with_overlap(aux, target, overlap)
+        cond = torch.cat([mels, aux], dim=2).transpose(0, 1).contiguous()
+        return cond, wave_len
+
+    def generate(self, mels, save_path: Union[str, Path, None], batched, target, overlap, mu_law, *,
+                 noise=None, seed: Optional[int] = None, verbose: bool = True):
+        """fatchord_version.py:169-264 with the loop on the GPU.
+
+        Keyword-only extensions: `noise` [L][B][K] injects the sampler draws in reference order
+        (parity testing); otherwise draws come from in-kernel Philox keyed by `seed` (default:
+        drawn from torch's global RNG, so torch.manual_seed governs reproducibility)."""
+        self.eval()
+        mu_law = mu_law if self.mode == 'RAW' else False
+        start = time.time()
+        with torch.no_grad():
+            cond, wave_len = self.conditioning(mels, batched, target, overlap)
+            seq_len, b_size, _ = cond.shape
+            loop = self.loop_handle()
+            nz = None
+            if noise is not None:
+                nz = torch.as_tensor(noise, dtype=torch.float32).to(cond.device).contiguous()
+            if seed is None:
+                seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+            out, _ = loop.generate(cond, noise=nz, seed=seed)
+            output = out.cpu().numpy().astype(np.float64)
+        self.last_gen_seconds = time.time() - start
+        if verbose:
+            self.gen_display(seq_len - 1, seq_len, b_size, start)
+        if mu_law:
+            output = dsp.decode_mu_law(output, self.n_classes, False)
+        if batched:
+            output = self.xfade_and_unfold(output, target, overlap)
+        else:
+            output = output[0]
+        fade_out = np.linspace(1, 0, 20 * self.hop_length)
+        output = output[:wave_len]
+        output[-20 * self.hop_length:] *= fade_out
+        dsp.save_wav(output, save_path, self.sample_rate)
+        self.train()
+        return output
+
+    def gen_display(self, i, seq_len, b_size, start):
+        gen_rate = (i + 1) / max(time.time() - start, 1e-9) * b_size / 1000
+        print(f'| {i + 1}/{seq_len} steps × {b_size} rows | Gen Rate: {gen_rate:.1f}kHz |')
+
+    def get_gru_cell(self, gru):
+        """nn.GRUCell view of a single-layer GRU's weights (fatchord_version.py:273-279)."""
+        cell = nn.GRUCell(gru.input_size, gru.hidden_size).to(gru.weight_hh_l0.device)
+        cell.weight_hh.data = gru.weight_hh_l0.data
+        cell.weight_ih.data = gru.weight_ih_l0.data
+        cell.bias_hh.data = gru.bias_hh_l0.data
+        cell.bias_ih.data = gru.bias_ih_l0.data
+        return cell
+
+    @staticmethod
+    def pad_tensor(x, pad, side='both'):
+        """Zero-pad the time axis of [b][t][c] (fatchord_version.py:281-291)."""
+        b, t, c = x.size()
+        total = t + 2 * pad if side == 'both' else t + pad
+        padded = torch.zeros(b, total, c, device=x.device, dtype=x.dtype)
+        if side in ('before', 'both'):
+            padded[:, pad:pad + t, :] = x
+        elif side == 'after':
+            padded[:, :t, :] = x
+        return padded
+
+    @staticmethod
+    def fold_count(total_len, target, overlap):
+        n = (total_len - overlap) // (target + overlap)
+        remaining = total_len - (n * (overlap + target) + overlap)
+        return n + (1 if remaining != 0 else 0), remaining
+
+    def fold_with_overlap(self, x, target, overlap):
+        """[1][L][F] → [num_folds][target + 2·overlap][F]; consecutive folds share `overlap`
+        steps, the tail is zero-padded (fatchord_version.py:293-340)."""
+        _, total_len, features = x.size()
+        num_folds, remaining = self.fold_count(total_len, target, overlap)
+        if remaining != 0:
+            x = self.pad_tensor(x, target + 2 * overlap - remaining, side='after')
+        win = target + 2 * overlap
+        folds = x[0].unfold(0, win, target + overlap)          # [n][F][win] views
+        return folds[:num_folds].transpose(1, 2).contiguous()
+
+    @staticmethod
+    def xfade_and_unfold(y, target, overlap):
+        """Equal-power cross-fade of folds and overlap-add back to 1-D float64
+        (fatchord_version.py:342-405; `fade_out` keeps the reference's leading ones)."""
+        num_folds, length = y.shape
+        target = length - 2 * overlap
+        total_len = num_folds * (target + overlap) + overlap
+        silence_len = overlap // 2
+        fade_len = overlap - silence_len
+        t = np.linspace(-1, 1, fade_len, dtype=np.float64)
+        fade_in = np.concatenate([np.zeros(silence_len, dtype=np.float64), np.sqrt(0.5 * (1 + t))])
+        fade_out = np.concatenate([np.ones(silence_len, dtype=np.float64), np.sqrt(0.5 * (1 - t))])
+        y = np.array(y, dtype=np.float64, copy=True)
+        y[:, :overlap] *= fade_in
+        y[:, -overlap:] *= fade_out
+        unfolded = np.zeros(total_len, dtype=np.float64)
+        for i in range(num_folds):
+            s = i * (target + overlap)
+            unfolded[s:s + length] += y[i]
+        return unfolded
+
+    # ------------------------------------------------------------------ bookkeeping
+    def get_step(self):
+        return self.step.data.item()
+
+    def log(self, path, msg):
+        with open(path, 'a') as f:
+            print(msg, file=f)
+
+    def load(self, path: Union[str, Path]):
+        """Reference checkpoint (a state_dict saved with torch.save) → this model.  Loaded
+        with weights_only=True: a checkpoint never executes code."""
+        device = next(self.parameters()).device
+        self.load_state_dict(torch.load(path, map_location=device, weights_only=True), strict=False)
+
+    def save(self, path: Union[str, Path]):
+        torch.save(self.state_dict(), path)
+
+    def num_params(self, print_out=True):
+        n = sum(p.numel() for p in self.parameters() if p.requires_grad) / 1_000_000
+        if print_out:
+            print('Trainable Parameters: %.3fM' % n)
+        return n
+
+    def noise_width(self) -> int:
+        return noise_width(self.mode, self.n_classes)
