@@ -51,4 +51,7 @@ if __name__ == "__main__":
     run(syn.DEFAULT_MOL, 1, 5000)
     run(syn.DEFAULT_MOL, 1, 5000, philox=True)
     for g in (64, 128):
-        run(syn.DEFAULT_MOL, 1, 3000, grid=g)
+        try:
+            run(syn.DEFAULT_MOL, 1, 3000, grid=g)
+        except Exception as e:  # grids whose slab does not fit LDS are rejected up front
+            print(f"grid {g}: {e}")

@@ -1,0 +1,15 @@
+#!/bin/bash
+# One GPU session: parity suite, headline bench, rocprofv3 kernel-trace summary.
+# Stops at the first step that ends abnormally (fault/abort/timeout), per the pool rules.
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+R=$(pwd)
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -m gpu -q -x > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest_gpu rc=$rc"
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 600 python bench.py "$@" > gpurun_out/bench.log 2>&1
+rc=$?; echo "bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
+export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o bench --output-format csv -- \
+    python "$R/bench.py" --steps 2 --warmup 1 --cpu-steps 0 > gpurun_out/prof.log 2>&1
+rc=$?; echo "rocprof rc=$rc"; exit $rc

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -153,7 +154,8 @@ void pack_slab(const wrnn_ctx &h, int w, float *out) {
 }
 
 size_t lds_bytes_for(const wrnn_ctx &h, int Bc) {
-    return (size_t)lds_layout(h.s.total, Bc, h.cfg.rnn_dims, h.cfg.fc_dims, h.cfg.aux_dims, h.cfg.n_classes, h.NK)
+    return (size_t)lds_layout(h.s.total, Bc, h.cfg.rnn_dims, h.cfg.fc_dims, h.cfg.aux_dims, h.cfg.n_classes, h.NK,
+                              h.U, h.UF)
                .total * sizeof(float);
 }
 
@@ -276,7 +278,11 @@ int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise
         HIP_TRY(h, hipMalloc(&h->d_cI, need_cI * 4));
         h->cI_cap = need_cI;
     }
-    const size_t need_xg = (size_t)kHops * Bc_max * h->NMAX;
+    // hand-off replicas (WRNN_REPLICAS, default 8), each padded to a 64 KiB boundary
+    const char *rep_env = std::getenv("WRNN_REPLICAS");
+    const int reps = std::max(1, std::min(64, rep_env ? std::atoi(rep_env) : 8));
+    const long long rep_stride = (((long long)Bc_max * h->NMAX * 8 + 65535) / 65536) * 65536 / 8;
+    const size_t need_xg = (size_t)kHops * reps * rep_stride;
     if (need_xg > h->xg_cap) {
         if (h->d_xg) HIP_TRY(h, hipFree(h->d_xg));
         h->d_xg = nullptr;
@@ -284,11 +290,19 @@ int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise
         h->xg_cap = need_xg;
     }
     HIP_TRY(h, hipMemsetAsync(h->d_ctl, 0, kCtlWords * sizeof(int), st));
+    // diagnostics: WRNN_DEBUG_STAMPS=<steps> WRNN_DEBUG_FILE=<path> dumps per-stage stamps
+    const char *dbg_env = std::getenv("WRNN_DEBUG_STAMPS");
+    const int dbg_steps = dbg_env ? std::min(L, std::atoi(dbg_env)) : 0;
+    unsigned *d_dbg = nullptr;
+    if (dbg_steps > 0) {
+        HIP_TRY(h, hipMalloc(&d_dbg, (size_t)h->G * dbg_steps * kStamps * 4));
+        HIP_TRY(h, hipMemsetAsync(d_dbg, 0, (size_t)h->G * dbg_steps * kStamps * 4, st));
+    }
     for (int b0 = 0; b0 < B; b0 += h->max_rows) {
         const int Bc = std::min(h->max_rows, B - b0);
         HIP_TRY(h, launch_ci_gemm(cond, h->CD, B, b0, Bc, L, h->d_IW, 1 + c.feat_dims + c.aux_dims, h->d_Ib, R,
                                   c.feat_dims + c.aux_dims, h->d_cI, st));
-        HIP_TRY(h, hipMemsetAsync(h->d_xg, 0, (size_t)kHops * Bc * h->NMAX * 8, st));
+        HIP_TRY(h, hipMemsetAsync(h->d_xg, 0, need_xg * 8, st));
         LoopArgs a{};
         a.slab = h->d_slab;
         a.cI = h->d_cI;
@@ -297,6 +311,12 @@ int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise
         a.out = out;
         a.labels = labels;
         a.xg = h->d_xg;
+        a.reps = reps;
+        {
+            const char *dp = std::getenv("WRNN_DELAY_POLL");
+            a.delay_poll = dp ? std::atoi(dp) : 1;
+        }
+        a.rep_stride = rep_stride;
         a.ctl = h->d_ctl;
         a.seed = seed;
         a.row0 = row_offset + b0;
@@ -319,11 +339,26 @@ int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise
         a.G = h->G;
         a.NMAX = h->NMAX;
         a.s = h->s;
+        a.dbg = (b0 == 0) ? d_dbg : nullptr;
+        a.dbg_steps = dbg_steps;
         if (b0 == 0) HIP_TRY(h, hipEventRecord(h->ev0, st));
         HIP_TRY(h, launch_loop(a, lds_bytes_for(*h, Bc), st));
     }
     HIP_TRY(h, hipEventRecord(h->ev1, st));
     h->timed = true;
+    if (d_dbg) {
+        std::vector<unsigned> host((size_t)h->G * dbg_steps * kStamps);
+        HIP_TRY(h, hipStreamSynchronize(st));
+        HIP_TRY(h, hipMemcpy(host.data(), d_dbg, host.size() * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(h, hipFree(d_dbg));
+        const char *path = std::getenv("WRNN_DEBUG_FILE");
+        if (FILE *f = std::fopen(path ? path : "wrnn_stamps.bin", "wb")) {
+            int hdr[3] = {h->G, dbg_steps, kStamps};
+            std::fwrite(hdr, sizeof(hdr), 1, f);
+            std::fwrite(host.data(), 4, host.size(), f);
+            std::fclose(f);
+        }
+    }
     return WRNN_OK;
 }
 

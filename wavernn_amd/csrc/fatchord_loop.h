@@ -33,7 +33,7 @@ struct LoopArgs {
     const float *noise;           // [L][Bt][NK] or nullptr (Philox)
     float *out;                   // [Bt][L]
     int32_t *labels;              // [Bt][L] or nullptr
-    unsigned long long *xg;       // [kHops][Bc * NMAX] granules {tag:32 | value:32}
+    unsigned long long *xg;       // [kHops][reps][rep_stride] granules {tag:32 | value:32}
     int *ctl;                     // [0] abort, [1] error code, [2] step, [3] hop, [4] wg
     unsigned long long seed;
     long long row0;               // global row id of chunk row 0 (Philox key)
@@ -42,32 +42,48 @@ struct LoopArgs {
     int R, F, A, CD, feat, NC, NK, mol;
     int U, UF, UC, G, NMAX;
     SlabLayout s;
+    int delay_poll;               // pollers wait for this WG's own publish before polling
+    int reps;                     // replicas of every hand-off vector (consumer w polls w % reps)
+    long long rep_stride;         // granules between replicas
+    // diagnostics (WRNN_DEBUG_STAMPS): per-stage s_memrealtime stamps, [G][dbg_steps][kStamps]
+    unsigned *dbg;
+    int dbg_steps;
 };
+constexpr int kStamps = 16;
 
 // Dynamic-LDS layout (floats) for Bc rows; shared by host sizing and the kernel.
 struct LdsLayout {
-    int slab, h1, h2, xa, fa, f2, lg, pre, xprev, lbl, flag, total;
-    int ncp, pp;
+    int slab, h1, h2, xa, f1, f2, lg, pre, pc, q, xprev, lbl, flag, stamp, total;
+    int ncp, pp, pcu;
 };
 
 __host__ __device__ inline int round4(int x) { return (x + 3) & ~3; }
 
-__host__ __device__ inline LdsLayout lds_layout(int slab_total, int Bc, int R, int F, int A, int NC, int NK) {
+// Per (row, unit) precomputed terms, kept in LDS between the stage that makes them (off the
+// critical path, while a hand-off is in flight) and the stage that consumes them.
+enum PcSlot { PC_P1 = 0, PC_GH1 = 3, PC_P2 = 6, PC_GH2 = 9, PC_V1 = 12, PC_V2 = 13, PC_N = 16 };
+
+__host__ __device__ inline LdsLayout lds_layout(int slab_total, int Bc, int R, int F, int A, int NC, int NK,
+                                               int U, int UF) {
     LdsLayout l;
     l.ncp = round4(NC);
     l.pp = round4(R + 3 * A + NK);
+    l.pcu = (U > UF ? U : UF);                 // pc entries per row (unit u and fc row u share)
     int o = 0;
     l.slab = o;  o += round4(slab_total);
     l.h1 = o;    o += Bc * R;
     l.h2 = o;    o += Bc * R;
-    l.xa = o;    o += Bc * (R + A);
-    l.fa = o;    o += Bc * (F + A);
+    l.xa = o;    o += Bc * (R + A);            // [x_I + h1 | a3]
+    l.f1 = o;    o += Bc * F;
     l.f2 = o;    o += Bc * F;
     l.lg = o;    o += Bc * l.ncp;
-    l.pre = o;   o += 2 * Bc * l.pp;
+    l.pre = o;   o += 3 * Bc * l.pp;           // ring of 3 step records
+    l.pc = o;    o += Bc * l.pcu * PC_N;
+    l.q = o;     o += round4(6 * U);           // Q1, Q2: W_ih·W_I[:,0] per gate row
     l.xprev = o; o += round4(Bc);
     l.lbl = o;   o += round4(Bc);
-    l.flag = o;  o += 4;
+    l.flag = o;  o += 8;                       // abort word + per-hop publish counters
+    l.stamp = o; o += kStamps;
     l.total = o;
     return l;
 }

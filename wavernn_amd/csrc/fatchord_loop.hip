@@ -86,6 +86,7 @@ template <int NR>
 __device__ __forceinline__ void dots(const float *__restrict__ w0, int wstride, const float *__restrict__ x,
                                      int K4, int lane, float (&acc)[NR]) {
     const float4 *x4 = reinterpret_cast<const float4 *>(x);
+#pragma unroll 4
     for (int c = lane; c < K4; c += 64) {
         const float4 xv = x4[c];
 #pragma unroll
@@ -101,7 +102,16 @@ __device__ __forceinline__ void dots(const float *__restrict__ w0, int wstride, 
     }
 }
 
-__device__ __forceinline__ float sigmoid_(float x) { return 1.0f / (1.0f + expf(-x)); }
+// Gate nonlinearities on the critical path use the hardware exp2 (v_exp_f32) and reciprocal:
+// ≈1e-7 absolute error, inside the parity tolerance (the reference's SLEEF/MKL paths are not
+// correctly rounded either).  Samplers keep the accurate libm functions.
+__device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+__device__ __forceinline__ float sigmoid_(float x) { return __builtin_amdgcn_rcpf(1.0f + fast_exp(-x)); }
+__device__ __forceinline__ float tanh_(float x) {
+    const float e = fast_exp(-2.0f * fabsf(x));            // in (0, 1]: no overflow
+    const float t = (1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e);
+    return copysignf(t, x);
+}
 
 // ------------------------------------------------------------------------------ Philox
 __device__ __forceinline__ uint32_t philox_word(unsigned long long seed, unsigned long long row,
@@ -143,13 +153,16 @@ __device__ __noinline__ void record_abort(int *ctl, int code, int step, int hop,
     __hip_atomic_store(&ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Gather n = Bc·N granules of one hop into LDS rows (row b at dst + b·ld); called by the
-// kPollThreads polling threads only.  Each thread keeps all its outstanding polls in flight
-// per pass.  On timeout, or when another workgroup has aborted, sets *lds_abort.
-__device__ void gather(const unsigned long long *g, int n, int N, float *dst, int ld, uint32_t tag,
-                       int *ctl, long long timeout, int step, int hop, int *lds_abort) {
+// Gather n = Bc·N granules of one hop; store(b, j, v) puts each value where it belongs.
+// Called by the `npoll` polling threads only; each keeps all its polls of a pass in flight.
+// On timeout, or when another workgroup has aborted, sets *lds_abort.
+template <typename Store>
+__device__ __forceinline__ void gather(const unsigned long long *g, int n, int N, uint32_t tag, int *ctl,
+                                       long long timeout, int step, int hop, int *lds_abort, Store store,
+                                       unsigned *dbg_slot = nullptr) {
+    constexpr int npoll = kPollThreads;
     const int tid = threadIdx.x;
-    const int mine = (n - tid + kPollThreads - 1) / kPollThreads;  // tid < kPollThreads
+    const int mine = (n - tid + npoll - 1) / npoll;   // tid < npoll
     unsigned long long v[kGatherMax];
     const uint32_t all = (mine <= 0) ? 0u : (mine >= 32 ? 0xFFFFFFFFu : ((1u << mine) - 1u));
     uint32_t done = 0;
@@ -159,15 +172,17 @@ __device__ void gather(const unsigned long long *g, int n, int N, float *dst, in
 #pragma unroll
         for (int k = 0; k < kGatherMax; ++k)
             if (k < mine && !(done & (1u << k)))
-                v[k] = __hip_atomic_load(g + tid + k * kPollThreads, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                v[k] = __hip_atomic_load(g + tid + k * npoll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
         for (int k = 0; k < kGatherMax; ++k)
             if (k < mine && !(done & (1u << k)) && (uint32_t)(v[k] >> 32) == tag) {
-                const int i = tid + k * kPollThreads;
-                const int b = i / N, j = i - b * N;
-                dst[b * ld + j] = __uint_as_float((uint32_t)v[k]);
+                const int i = tid + k * npoll;
+                const int b = i / N;
+                store(b, i - b * N, __uint_as_float((uint32_t)v[k]));
                 done |= 1u << k;
             }
+        if (dbg_slot && spins == 0 && threadIdx.x == 0)
+            dbg_slot[1] = (unsigned)(__builtin_amdgcn_s_memrealtime() - t0);
         if (done == all) break;
         if ((++spins & 31u) == 0) {
             const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - t0) > timeout;
@@ -180,28 +195,71 @@ __device__ void gather(const unsigned long long *g, int n, int N, float *dst, in
         }
         __builtin_amdgcn_s_sleep(1);
     }
+    if (dbg_slot && threadIdx.x == 0) dbg_slot[0] = spins + 1;
 }
 
-// Stage work item `it` → wave: items 0,1 go to the publishing waves 2,3 first.
+// Stage work item `it` → wave: items 0,1 go to the non-polling waves 2,3 first.
 __device__ __forceinline__ int first_item(int wave) { return (wave + 2) & (kWaves - 1); }
 
-// One GRU cell (ATen gru_cell order, verified bit-exact vs torch.nn.GRUCell on CPU):
-// r = σ(hr + ir), z = σ(hz + iz), n = tanh(in + hn·r), h' = (h − n)·z + n.
-__device__ __forceinline__ float gru_unit(const float *S, int o_wih, int o_whh, int o_bih, int o_bhh, int U,
-                                          int u, const float *x, int KI, const float *h, int R, float h_old,
-                                          int lane) {
-    float ai[3] = {0.f, 0.f, 0.f}, ah[3] = {0.f, 0.f, 0.f};
-    dots<3>(S + o_wih + u * KI, U * KI, x, KI / 4, lane, ai);
-    dots<3>(S + o_whh + u * R, U * R, h, R / 4, lane, ah);
-    float gi[3], gh[3];
-#pragma unroll
-    for (int g = 0; g < 3; ++g) {
-        gi[g] = wave_sum(ai[g]) + S[o_bih + g * U + u];
-        gh[g] = wave_sum(ah[g]) + S[o_bhh + g * U + u];
+// ---- 16-lane row dots: a wave holds four DPP rows; row r (= lane >> 4) computes one dot,
+// lane li (= lane & 15) of the row takes float4 chunks li, li+16, …
+__device__ __forceinline__ float row_sum16(float v) {
+    v += WRNN_DPP(v, 0xB1);    // quad_perm [1,0,3,2]
+    v += WRNN_DPP(v, 0x4E);    // quad_perm [2,3,0,1]
+    v += WRNN_DPP(v, 0x141);   // row_half_mirror
+    v += WRNN_DPP(v, 0x140);   // row_mirror
+    return v;                  // the row's sum, identical bits in all 16 lanes
+}
+
+__device__ __forceinline__ float row_dot(const float *__restrict__ w, const float *__restrict__ x, int K4, int li) {
+    const float4 *w4 = reinterpret_cast<const float4 *>(w);
+    const float4 *x4 = reinterpret_cast<const float4 *>(x);
+    float acc = 0.0f;
+#pragma unroll 8
+    for (int c = li; c < K4; c += 16) {
+        const float4 a = w4[c], b = x4[c];
+        acc = fmaf(a.x, b.x, acc);
+        acc = fmaf(a.y, b.y, acc);
+        acc = fmaf(a.z, b.z, acc);
+        acc = fmaf(a.w, b.w, acc);
     }
-    const float r = sigmoid_(gh[0] + gi[0]);
-    const float z = sigmoid_(gh[1] + gi[1]);
-    const float n = tanhf(gi[2] + gh[2] * r);
+    return row_sum16(acc);
+}
+
+// Two rows against one x in a single pass (ILP for the 30-row MoL head).
+__device__ __forceinline__ float2 row_dot2(const float *__restrict__ w0, const float *__restrict__ w1,
+                                          const float *__restrict__ x, int K4, int li) {
+    const float4 *a4 = reinterpret_cast<const float4 *>(w0);
+    const float4 *b4 = reinterpret_cast<const float4 *>(w1);
+    const float4 *x4 = reinterpret_cast<const float4 *>(x);
+    float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll 8
+    for (int c = li; c < K4; c += 16) {
+        const float4 a = a4[c], b = b4[c], v = x4[c];
+        s0 = fmaf(a.x, v.x, s0); s0 = fmaf(a.y, v.y, s0); s0 = fmaf(a.z, v.z, s0); s0 = fmaf(a.w, v.w, s0);
+        s1 = fmaf(b.x, v.x, s1); s1 = fmaf(b.y, v.y, s1); s1 = fmaf(b.z, v.z, s1); s1 = fmaf(b.w, v.w, s1);
+    }
+    return make_float2(row_sum16(s0), row_sum16(s1));
+}
+
+__device__ __forceinline__ float lane_bcast(float v, int src) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src));
+}
+
+// Whole-wave dot (one dot, 64 lanes): lane l takes chunks l, l+64, …
+__device__ __forceinline__ float wave_dot(const float *__restrict__ w, const float *__restrict__ x, int K4, int lane) {
+    float acc[1] = {0.f};
+    dots<1>(w, 0, x, K4, lane, acc);
+    return wave_sum(acc[0]);
+}
+
+__device__ __forceinline__ float gru_gate_math(float gi_r, float gi_z, float gi_n, float gh_r, float gh_z,
+                                               float gh_n, float h_old) {
+    // ATen gru_cell order (bit-exact vs torch.nn.GRUCell on CPU in the oracle):
+    // r = σ(hr + ir), z = σ(hz + iz), n = tanh(in + hn·r), h' = (h − n)·z + n
+    const float r = sigmoid_(gh_r + gi_r);
+    const float z = sigmoid_(gh_z + gi_z);
+    const float n = tanh_(gi_n + gh_n * r);
     return (h_old - n) * z + n;
 }
 
@@ -213,90 +271,217 @@ __device__ __forceinline__ void bar() {
     asm volatile("" ::: "memory");
 }
 
+// Diagnostic stamp (only when a.dbg != 0): thread 0 records s_memrealtime into LDS slot k;
+// the loader wave flushes the slots of step t-1 to a.dbg at the top of step t.
+#define STAMP(k)                                                                               \
+    do {                                                                                       \
+        if (dbg_on && tid == 0) stamp[k] = (unsigned)__builtin_amdgcn_s_memrealtime();         \
+    } while (0)
+#define STAMP_WAVE(k)                                                                          \
+    do {                                                                                       \
+        if (dbg_on && lane == 0) stamp[k] = (unsigned)__builtin_amdgcn_s_memrealtime();        \
+    } while (0)
+
 #define WRNN_GPTR(p) ((__attribute__((address_space(1))) void *)(p))
 #define WRNN_LPTR(p) ((__attribute__((address_space(3))) void *)(p))
 
 // ------------------------------------------------------------------------ the loop kernel
+//
+// Per step t the critical path is   x_{t-1} → GRU1 gates → [hop A: h1] → W_ih2[:, :R]·h1 →
+// GRU2 gates → [hop B: h2] → W1[:, :R]·h2 → [hop C: f1] → W2[:, :F]·f1 → [hop D: f2] →
+// fc3 + sample → x_t.  Everything else is linear in values known one stage earlier and is
+// computed while a hand-off is in flight (fp32 re-association of the reference sums; parity
+// is checked against the oracle/reference within the stated tolerance):
+//   P1 = W_ih1·cI_t, Q1 = W_ih1·W_I[:,0]      → gi1 = P1 + x_{t-1}·Q1 + b_ih1
+//   GH1 = W_hh1·h1_{t-1}                       → gh1 = GH1 + b_hh1
+//   P2 = W_ih2·[cI_t; a2_t], Q2 = W_ih2[:, :R]·W_I[:,0]
+//                                              → gi2 = W_ih2[:, :R]·h1_t + P2 + x_{t-1}·Q2 + b_ih2
+//   GH2 = W_hh2·h2_{t-1}                       → gh2 = GH2 + b_hh2
+//   V1 = W1·[x_I + h1; a3] + b1                → f1 = relu(W1[:, :R]·h2 + V1)
+//   V2 = W2[:, F:]·a4 + b2                     → f2 = relu(W2[:, :F]·f1 + V2)
 __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, row = lane >> 4;
     const int w = blockIdx.x;
-    const int R = a.R, F = a.F, A = a.A, Bc = a.Bc, NK = a.NK;
-    const LdsLayout ll = lds_layout(a.s.total, Bc, R, F, A, a.NC, NK);
-    float *S = smem + ll.slab;
-    float *h1 = smem + ll.h1, *h2 = smem + ll.h2, *xa = smem + ll.xa, *fa = smem + ll.fa;
-    float *f2 = smem + ll.f2, *lg = smem + ll.lg, *pre = smem + ll.pre, *xprev = smem + ll.xprev;
+    const int R = a.R, F = a.F, A = a.A, Bc = a.Bc, NK = a.NK, U = a.U, UF = a.UF;
+    const LdsLayout ll = lds_layout(a.s.total, Bc, R, F, A, a.NC, NK, U, UF);
+    const float *S = smem + ll.slab;
+    float *h1 = smem + ll.h1, *h2 = smem + ll.h2, *xa = smem + ll.xa, *f1 = smem + ll.f1;
+    float *f2 = smem + ll.f2, *lg = smem + ll.lg, *pre = smem + ll.pre, *pc = smem + ll.pc;
+    float *q = smem + ll.q, *xprev = smem + ll.xprev;
     int *lbl = reinterpret_cast<int *>(smem + ll.lbl);
     int *abort_flag = reinterpret_cast<int *>(smem + ll.flag);
-    const int RA = R + A, FA = F + A, PP = ll.pp, P = R + 3 * A + NK;
-    const int Uv = min(a.U, R - w * a.U);                 // valid units here
-    const int UFv = max(0, min(a.UF, F - w * a.UF));
+    int *pubcnt = abort_flag + 1;                 // [kHops] items this WG has published so far
+    unsigned *stamp = reinterpret_cast<unsigned *>(smem + ll.stamp);
+    const int RA = R + A, PP = ll.pp, P = R + 3 * A + NK;
+    const int Uv = min(U, R - w * U);                 // valid units here
+    const int UFv = max(0, min(UF, F - w * UF));
     const int UCv = a.mol ? 0 : max(0, min(a.UC, a.NC - w * a.UC));
+    const int nU = Bc * Uv, nF = Bc * UFv, nC = Bc * UCv;
     const bool loader = wave == kLoaderWave;
     const bool compute = !loader;
     const bool poller = tid < kPollThreads;
+    const bool dbg_on = a.dbg != nullptr;
+    const bool writer = loader && w == 0 && lane < Bc;
+    const int it0 = first_item(wave);
 
-    // ---- prologue: weights → LDS, zero state, step-0 record [cI (R) | a2 a3 a4 (3A) | noise (NK)]
+    auto rec = [&](int t) { return pre + (t % 3) * Bc * PP; };          // [cI | a2 a3 a4 | noise]
+    auto PC = [&](int b, int u) { return pc + (b * ll.pcu + u) * PC_N; };
+
+    // ---- prologue: weights → LDS, zero state, records of steps 0 and 1
     {
         const float4 *src = reinterpret_cast<const float4 *>(a.slab + (size_t)w * a.s.total);
-        float4 *dst = reinterpret_cast<float4 *>(S);
+        float4 *dst = reinterpret_cast<float4 *>(smem + ll.slab);
         for (int i = tid; i < a.s.total / 4; i += kThreads) dst[i] = src[i];
         for (int i = tid; i < Bc * R; i += kThreads) { h1[i] = 0.0f; h2[i] = 0.0f; }
         if (tid < Bc) { xprev[tid] = 0.0f; lbl[tid] = 0; }   // x = zeros (fatchord_version.py:196)
-        if (tid == 0) *abort_flag = 0;
-        for (int i = tid; i < Bc * P; i += kThreads) {
-            const int b = i / P, q = i - b * P;
-            const size_t row = (size_t)a.b0 + b;              // t = 0
-            float v;
-            if (q < R) v = a.cI[(size_t)b * R + q];
-            else if (q < R + 3 * A) v = a.cond[row * a.CD + a.feat + A + (q - R)];
-            else if (a.noise) v = a.noise[row * NK + (q - R - 3 * A)];
-            else v = philox_noise(a.seed, (unsigned long long)(a.row0 + b), 0u, (uint32_t)(q - R - 3 * A), a.mol);
-            pre[b * PP + q] = v;
+        if (tid < 1 + kHops) abort_flag[tid] = 0;
+        for (int t = 0; t < min(2, a.L); ++t)
+            for (int i = tid; i < Bc * P; i += kThreads) {
+                const int b = i / P, k = i - b * P;
+                const size_t rowi = (size_t)t * a.Bt + a.b0 + b;
+                float v;
+                if (k < R) v = a.cI[((size_t)t * Bc + b) * R + k];
+                else if (k < R + 3 * A) v = a.cond[rowi * a.CD + a.feat + A + (k - R)];
+                else if (a.noise) v = a.noise[rowi * NK + (k - R - 3 * A)];
+                else v = philox_noise(a.seed, (unsigned long long)(a.row0 + b), (uint32_t)t, (uint32_t)(k - R - 3 * A), a.mol);
+                rec(t)[b * PP + k] = v;
+            }
+    }
+    __syncthreads();
+    if (a.mol)   // step 0's sampler terms (the loader prepares every later step's)
+        for (int i = tid; i < Bc * 11; i += kThreads) {
+            const int b = i / 11, k = i - b * 11;
+            float *pz = rec(0) + b * PP + R + 3 * A + k;
+            const float uu = *pz;
+            *pz = k < 10 ? logf(-logf(uu)) : (logf(uu) - logf(1.0f - uu));
+        }
+
+    const float *wi0 = S + a.s.wi0;
+    // P1/P2 of step t for GRU item (b,u): six dots in two rounds of four 16-lane rows
+    auto precompute_P = [&](int t, int b, int u) {
+        const float *r_ = rec(t) + b * PP;           // [cI_t (R) | a2_t (A) | …]
+        float v1, v2;
+        {   // rows 0..2: P1[g] = W_ih1[g]·cI ; row 3: P2[0] = W_ih2[0]·[cI; a2]
+            const float *wr = row < 3 ? S + a.s.wih1 + (row * U + u) * R : S + a.s.wih2 + u * RA;
+            v1 = row_dot(wr, r_, (row < 3 ? R : RA) / 4, li);
+        }
+        {   // rows 0,1: P2[1], P2[2]
+            const int g = 1 + (row & 1);
+            v2 = row_dot(S + a.s.wih2 + (g * U + u) * RA, r_, RA / 4, li);
+        }
+        const float p10 = lane_bcast(v1, 0), p11 = lane_bcast(v1, 16), p12 = lane_bcast(v1, 32);
+        const float p20 = lane_bcast(v1, 48), p21 = lane_bcast(v2, 0), p22 = lane_bcast(v2, 16);
+        if (lane == 0) {
+            float *p = PC(b, u);
+            p[PC_P1 + 0] = p10;
+            p[PC_P1 + 1] = p11;
+            p[PC_P1 + 2] = p12;
+            p[PC_P2 + 0] = p20;
+            p[PC_P2 + 1] = p21;
+            p[PC_P2 + 2] = p22;
+        }
+    };
+
+    // constants Q1/Q2 per unit and step-0 P terms (GH = W_hh·0 = 0)
+    if (compute) {
+        for (int u = wave; u < Uv; u += kWaves) {
+            float v1, v2;
+            {
+                const float *wr = row < 3 ? S + a.s.wih1 + (row * U + u) * R : S + a.s.wih2 + u * RA;
+                v1 = row_dot(wr, wi0, R / 4, li);
+            }
+            v2 = row_dot(S + a.s.wih2 + ((1 + (row & 1)) * U + u) * RA, wi0, R / 4, li);
+            const float q0 = lane_bcast(v1, 0), q1 = lane_bcast(v1, 16), q2 = lane_bcast(v1, 32);
+            const float q3 = lane_bcast(v1, 48), q4 = lane_bcast(v2, 0), q5 = lane_bcast(v2, 16);
+            if (lane == 0) {
+                q[0 * U + u] = q0;
+                q[1 * U + u] = q1;
+                q[2 * U + u] = q2;
+                q[3 * U + u] = q3;
+                q[4 * U + u] = q4;
+                q[5 * U + u] = q5;
+            }
+        }
+        for (int it = it0; it < nU; it += kWaves) {
+            const int b = it / Uv, u = it - b * Uv;
+            precompute_P(0, b, u);
+            if (lane == 0) {
+                float *p = PC(b, u);
+                for (int g = 0; g < 3; ++g) { p[PC_GH1 + g] = 0.0f; p[PC_GH2 + g] = 0.0f; }
+            }
         }
     }
     __syncthreads();
 
-    const float *wi0 = S + a.s.wi0;
-    const size_t hop_stride = (size_t)Bc * a.NMAX;
+    // every hop vector exists in a.reps replicas (spread over memory channels); a value is
+    // published to all of them by lanes 0..reps-1 at once, workgroup w polls replica w % reps
+    const size_t hop_stride = (size_t)a.reps * a.rep_stride;
+    const size_t pub_off = (size_t)(lane < a.reps ? lane : 0) * a.rep_stride;
+    const size_t poll_off = (size_t)(w % a.reps) * a.rep_stride;
     unsigned long long *xgH1 = a.xg + HOP_H1 * hop_stride, *xgH2 = a.xg + HOP_H2 * hop_stride;
     unsigned long long *xgF1 = a.xg + HOP_F1 * hop_stride, *xgF2 = a.xg + HOP_F2 * hop_stride;
     unsigned long long *xgLG = a.xg + HOP_LOGITS * hop_stride;
-    const int it0 = first_item(wave);
-    const bool writer = loader && w == 0 && lane < Bc;
+    const bool pub_lane = lane < a.reps;
+    // Delayed polling (a.delay_poll): the polling threads start their global polls only once
+    // this workgroup's own values of the hop are out — fewer useless passes, less traffic.
+    auto count_pub = [&](int hop) {
+        if (lane == 0) __hip_atomic_fetch_add(&pubcnt[hop], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto wait_own = [&](int hop, int t, int items) {
+        if (!a.delay_poll || items == 0) return;
+        const int want = (t + 1) * items;
+        while (__hip_atomic_load(&pubcnt[hop], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
+            __builtin_amdgcn_s_sleep(1);
+    };
 
     for (int t = 0; t < a.L; ++t) {
         const uint32_t tag = (uint32_t)t + 1u;
-        const float *cur = pre + (t & 1) * Bc * PP;
-        float *nxt = pre + ((t + 1) & 1) * Bc * PP;
-        const bool has_next = (t + 1) < a.L;
+        const float *cur = rec(t);
+        STAMP(0);
 
         if (loader) {
+            if (dbg_on && t > 0 && t - 1 < a.dbg_steps && lane < kStamps)
+                a.dbg[((size_t)w * a.dbg_steps + (t - 1)) * kStamps + lane] = stamp[lane];
             // outputs of step t-1 (LDS reads happen before any DMA is in flight)
             if (writer && t > 0) {
                 const size_t o = (size_t)(a.b0 + lane) * a.L + (t - 1);
                 a.out[o] = xprev[lane];
                 if (a.labels) a.labels[o] = lbl[lane];
             }
-            if (has_next) {
-                const int t1 = t + 1;
+            // MoL: turn step t+1's draws into the sampler's terms now, off the critical path:
+            // u1 → log(-log(u1)) (distribution.py:107), u2 → log(u2) − log(1 − u2) (:119).
+            // Same fp32 operations as at sampling time, only earlier.
+            if (a.mol && t + 1 < a.L) {
+                float *nz1 = rec(t + 1);
+                for (int i = lane; i < Bc * 11; i += 64) {
+                    const int b = i / 11, k = i - b * 11;
+                    float *pz = nz1 + b * PP + R + 3 * A + k;
+                    const float uu = *pz;
+                    *pz = k < 10 ? logf(-logf(uu)) : (logf(uu) - logf(1.0f - uu));
+                }
+            }
+            // record of step t+2 → ring (lands while this step's hand-offs are in flight)
+            const int t2 = t + 2;
+            if (t2 < a.L) {
+                float *slot = rec(t2);
                 for (int b = 0; b < Bc; ++b) {
-                    float *dst = nxt + b * PP;
-                    const size_t row = (size_t)t1 * a.Bt + a.b0 + b;
+                    float *dst = slot + b * PP;
+                    const size_t rowi = (size_t)t2 * a.Bt + a.b0 + b;
                     if (!a.noise)   // Philox draws: plain LDS writes, issued before the DMAs
                         for (int k = lane; k < NK; k += 64)
                             dst[R + 3 * A + k] = philox_noise(a.seed, (unsigned long long)(a.row0 + b),
-                                                              (uint32_t)t1, (uint32_t)k, a.mol);
-                    const float *ci = a.cI + ((size_t)t1 * Bc + b) * R;
+                                                              (uint32_t)t2, (uint32_t)k, a.mol);
+                    const float *ci = a.cI + ((size_t)t2 * Bc + b) * R;
                     for (int c = 0; c < R; c += 256)
                         if (c + lane * 4 < R)
                             __builtin_amdgcn_global_load_lds(WRNN_GPTR(ci + c + lane * 4), WRNN_LPTR(dst + c), 16, 0, 0);
-                    const float *ax = a.cond + row * a.CD + a.feat + A;
+                    const float *ax = a.cond + rowi * a.CD + a.feat + A;
                     for (int c = 0; c < 3 * A; c += 64)
                         if (c + lane < 3 * A)
                             __builtin_amdgcn_global_load_lds(WRNN_GPTR(ax + c + lane), WRNN_LPTR(dst + R + c), 4, 0, 0);
                     if (a.noise) {
-                        const float *nz = a.noise + row * NK;
+                        const float *nz = a.noise + rowi * NK;
                         for (int c = 0; c < NK; c += 64)
                             if (c + lane < NK)
                                 __builtin_amdgcn_global_load_lds(WRNN_GPTR(nz + c + lane),
@@ -306,121 +491,168 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
             }
         }
 
-        // S1: x = I([x_{t-1}; m_t; a1_t]) = cI_t + W_I[:,0]·x_{t-1}; stage a2 and a4
-        if (compute) {
-            for (int i = tid; i < Bc * R; i += kCompute) {
-                const int b = i / R, j = i - b * R;
-                xa[b * RA + j] = fmaf(wi0[j], xprev[b], cur[b * PP + j]);
+        // ---- GRU1 (fatchord_version.py:208-210): gates only, every matvec precomputed
+        if (compute)
+            for (int it = it0; it < nU; it += kWaves) {
+                const int b = it / Uv, u = it - b * Uv, j = w * U + u;
+                const float x = xprev[b];
+                const float *p = PC(b, u);
+                float gi[3], gh[3];
+#pragma unroll
+                for (int g = 0; g < 3; ++g) {
+                    gi[g] = fmaf(x, q[g * U + u], p[PC_P1 + g]) + S[a.s.bih1 + g * U + u];
+                    gh[g] = p[PC_GH1 + g] + S[a.s.bhh1 + g * U + u];
+                }
+                const float hn = gru_gate_math(gi[0], gi[1], gi[2], gh[0], gh[1], gh[2], h1[b * R + j]);
+                if (pub_lane) publish(xgH1 + pub_off + b * R + j, tag, hn);
+                count_pub(HOP_H1);
+                if (it == it0) STAMP_WAVE(12);
             }
-            for (int i = tid; i < Bc * A; i += kCompute) {
-                const int b = i / A, j = i - b * A;
-                xa[b * RA + R + j] = cur[b * PP + R + j];               // a2
-                fa[b * FA + F + j] = cur[b * PP + R + 2 * A + j];       // a4
+        // hop A: h1_t; the pollers also form x = x_I + h1 (:212) and stage a3 next to it
+        if (poller) {
+            wait_own(HOP_H1, t, nU);
+            gather(xgH1 + poll_off, Bc * R, R, tag, a.ctl, a.timeout_ticks, t, HOP_H1, abort_flag,
+                   [&](int b, int j, float v) {
+                       h1[b * R + j] = v;
+                       xa[b * RA + j] = fmaf(wi0[j], xprev[b], cur[b * PP + j]) + v;
+                   });
+            for (int i = tid; i < Bc * A; i += kPollThreads) {
+                const int b = i / A, k = i - b * A;
+                xa[b * RA + R + k] = cur[b * PP + R + A + k];
             }
         }
         bar();
-
-        // S2: h1 = GRUCell1(x, h1) for owned units → publish      (fatchord_version.py:210)
-        if (compute)
-            for (int it = it0; it < Bc * Uv; it += kWaves) {
-                const int b = it / Uv, u = it - b * Uv, j = w * a.U + u;
-                const float hn = gru_unit(S, a.s.wih1, a.s.whh1, a.s.bih1, a.s.bhh1, a.U, u, xa + b * RA, R,
-                                          h1 + b * R, R, h1[b * R + j], lane);
-                if (lane == 0) publish(xgH1 + b * R + j, tag, hn);
-            }
-        bar();   // all reads of h1(t-1) done before the gather overwrites it
-        if (poller) gather(xgH1, Bc * R, R, h1, R, tag, a.ctl, a.timeout_ticks, t, HOP_H1, abort_flag);
-        bar();
+        STAMP(1);
         if (*abort_flag) return;
 
-        // S3: x = x + h1                                             (:212)
-        if (compute)
-            for (int i = tid; i < Bc * R; i += kCompute) {
-                const int b = i / R, j = i - b * R;
-                xa[b * RA + j] = xa[b * RA + j] + h1[i];
-            }
-        bar();
-
-        // S4: h2 = GRUCell2([x; a2], h2) for owned units → publish (:213-214)
-        if (compute)
-            for (int it = it0; it < Bc * Uv; it += kWaves) {
-                const int b = it / Uv, u = it - b * Uv, j = w * a.U + u;
-                const float hn = gru_unit(S, a.s.wih2, a.s.whh2, a.s.bih2, a.s.bhh2, a.U, u, xa + b * RA, RA,
-                                          h2 + b * R, R, h2[b * R + j], lane);
-                if (lane == 0) publish(xgH2 + b * R + j, tag, hn);
-            }
-        bar();
-        if (poller) gather(xgH2, Bc * R, R, h2, R, tag, a.ctl, a.timeout_ticks, t, HOP_H2, abort_flag);
-        bar();
-        if (*abort_flag) return;
-
-        // S5: x = x + h2; stage a3                                    (:216-217)
+        // ---- GRU2 (:213-214): W_ih2[:, :R]·h1 on the critical path, then GH1_{t+1} and V1
         if (compute) {
-            for (int i = tid; i < Bc * R; i += kCompute) {
-                const int b = i / R, j = i - b * R;
-                xa[b * RA + j] = xa[b * RA + j] + h2[i];
+            for (int it = it0; it < nU; it += kWaves) {
+                const int b = it / Uv, u = it - b * Uv, j = w * U + u;
+                const float v = row_dot(S + a.s.wih2 + ((row < 3 ? row : 0) * U + u) * RA, h1 + b * R, R / 4, li);
+                const float x = xprev[b];
+                const float *p = PC(b, u);
+                float gi[3], gh[3];
+#pragma unroll
+                for (int g = 0; g < 3; ++g) {
+                    gi[g] = (lane_bcast(v, 16 * g) + fmaf(x, q[(3 + g) * U + u], p[PC_P2 + g])) + S[a.s.bih2 + g * U + u];
+                    gh[g] = p[PC_GH2 + g] + S[a.s.bhh2 + g * U + u];
+                }
+                const float hn = gru_gate_math(gi[0], gi[1], gi[2], gh[0], gh[1], gh[2], h2[b * R + j]);
+                if (pub_lane) publish(xgH2 + pub_off + b * R + j, tag, hn);
+                count_pub(HOP_H2);
+                if (it == it0) STAMP_WAVE(13);
             }
-            for (int i = tid; i < Bc * A; i += kCompute) {
-                const int b = i / A, j = i - b * A;
-                xa[b * RA + R + j] = cur[b * PP + R + A + j];
+            for (int it = it0; it < nU; it += kWaves) {     // GH1_{t+1} = W_hh1·h1_t
+                const int b = it / Uv, u = it - b * Uv;
+                const float v = row_dot(S + a.s.whh1 + ((row < 3 ? row : 0) * U + u) * R, h1 + b * R, R / 4, li);
+                const float g0 = lane_bcast(v, 0), g1 = lane_bcast(v, 16), g2 = lane_bcast(v, 32);
+                if (lane == 0) {
+                    float *p = PC(b, u);
+                    p[PC_GH1 + 0] = g0;
+                    p[PC_GH1 + 1] = g1;
+                    p[PC_GH1 + 2] = g2;
+                }
+            }
+            for (int it = it0; it < nF; it += kWaves) {     // V1 = W1·[x + h1; a3] + b1
+                const int b = it / UFv, r = it - b * UFv;
+                const float v = wave_dot(S + a.s.w1 + r * RA, xa + b * RA, RA / 4, lane);
+                if (lane == 0) PC(b, r)[PC_V1] = v + S[a.s.b1 + r];
             }
         }
+        if (poller) wait_own(HOP_H2, t, nU);
+        if (poller)
+            gather(xgH2 + poll_off, Bc * R, R, tag, a.ctl, a.timeout_ticks, t, HOP_H2, abort_flag,
+                   [&](int b, int j, float v) { h2[b * R + j] = v; }, dbg_on ? stamp + 14 : nullptr);
         bar();
-
-        // S6: f1 = relu(fc1([x; a3])) owned rows → publish           (:217-218)
-        if (compute)
-            for (int it = it0; it < Bc * UFv; it += kWaves) {
-                const int b = it / UFv, r = it - b * UFv, j = w * a.UF + r;
-                float acc[1] = {0.f};
-                dots<1>(S + a.s.w1 + r * RA, 0, xa + b * RA, RA / 4, lane, acc);
-                const float v = wave_sum(acc[0]) + S[a.s.b1 + r];
-                if (lane == 0) publish(xgF1 + b * F + j, tag, v > 0.0f ? v : 0.0f);
-            }
-        if (poller) gather(xgF1, Bc * F, F, fa, FA, tag, a.ctl, a.timeout_ticks, t, HOP_F1, abort_flag);
-        bar();
+        STAMP(2);
         if (*abort_flag) return;
 
-        // S7: f2 = relu(fc2([f1; a4])) owned rows → publish          (:220-221)
-        if (compute)
-            for (int it = it0; it < Bc * UFv; it += kWaves) {
-                const int b = it / UFv, r = it - b * UFv, j = w * a.UF + r;
-                float acc[1] = {0.f};
-                dots<1>(S + a.s.w2 + r * FA, 0, fa + b * FA, FA / 4, lane, acc);
-                const float v = wave_sum(acc[0]) + S[a.s.b2 + r];
-                if (lane == 0) publish(xgF2 + b * F + j, tag, v > 0.0f ? v : 0.0f);
+        // ---- fc1 (:216-218): W1[:, :R]·h2 + V1, then GH2_{t+1} and V2
+        if (compute) {
+            for (int it = it0; it < nF; it += kWaves) {
+                const int b = it / UFv, r = it - b * UFv, j = w * UF + r;
+                const float v = wave_dot(S + a.s.w1 + r * RA, h2 + b * R, R / 4, lane) + PC(b, r)[PC_V1];
+                if (pub_lane) publish(xgF1 + pub_off + b * F + j, tag, v > 0.0f ? v : 0.0f);
+                count_pub(HOP_F1);
             }
-        if (poller) gather(xgF2, Bc * F, F, f2, F, tag, a.ctl, a.timeout_ticks, t, HOP_F2, abort_flag);
+            for (int it = it0; it < nU; it += kWaves) {     // GH2_{t+1} = W_hh2·h2_t
+                const int b = it / Uv, u = it - b * Uv;
+                const float v = row_dot(S + a.s.whh2 + ((row < 3 ? row : 0) * U + u) * R, h2 + b * R, R / 4, li);
+                const float g0 = lane_bcast(v, 0), g1 = lane_bcast(v, 16), g2 = lane_bcast(v, 32);
+                if (lane == 0) {
+                    float *p = PC(b, u);
+                    p[PC_GH2 + 0] = g0;
+                    p[PC_GH2 + 1] = g1;
+                    p[PC_GH2 + 2] = g2;
+                }
+            }
+            for (int it = it0; it < nF; it += kWaves) {     // V2 = W2[:, F:]·a4 + b2
+                const int b = it / UFv, r = it - b * UFv;
+                const float v = wave_dot(S + a.s.w2 + r * (F + A) + F, cur + b * PP + R + 2 * A, A / 4, lane);
+                if (lane == 0) PC(b, r)[PC_V2] = v + S[a.s.b2 + r];
+            }
+        }
+        if (poller) wait_own(HOP_F1, t, nF);
+        if (poller)
+            gather(xgF1 + poll_off, Bc * F, F, tag, a.ctl, a.timeout_ticks, t, HOP_F1, abort_flag,
+                   [&](int b, int j, float v) { f1[b * F + j] = v; });
         bar();
+        STAMP(3);
         if (*abort_flag) return;
 
-        // S8: logits = fc3(f2)                                        (:223)
+        // ---- fc2 (:220-221): W2[:, :F]·f1 + V2, then P1/P2 of step t+1
+        if (compute) {
+            for (int it = it0; it < nF; it += kWaves) {
+                const int b = it / UFv, r = it - b * UFv, j = w * UF + r;
+                const float v = wave_dot(S + a.s.w2 + r * (F + A), f1 + b * F, F / 4, lane) + PC(b, r)[PC_V2];
+                if (pub_lane) publish(xgF2 + pub_off + b * F + j, tag, v > 0.0f ? v : 0.0f);
+                count_pub(HOP_F2);
+            }
+            if (t + 1 < a.L)
+                for (int it = it0; it < nU; it += kWaves) {
+                    const int b = it / Uv, u = it - b * Uv;
+                    precompute_P(t + 1, b, u);
+                }
+        }
+        if (poller) wait_own(HOP_F2, t, nF);
+        if (poller)
+            gather(xgF2 + poll_off, Bc * F, F, tag, a.ctl, a.timeout_ticks, t, HOP_F2, abort_flag,
+                   [&](int b, int j, float v) { f2[b * F + j] = v; });
+        bar();
+        STAMP(4);
+        if (*abort_flag) return;
+
+        // ---- fc3 (:223)
         if (a.mol) {
-            // all 30 rows redundantly in every workgroup (bit-identical everywhere)
+            // all rows redundantly in every workgroup (bit-identical everywhere); 16-lane rows
             const int NC = a.NC;
             if (compute)
-                for (int it = wave; it < Bc * NC; it += kWaves) {
-                    const int b = it / NC, c = it - b * NC;
-                    float acc[1] = {0.f};
-                    dots<1>(S + a.s.w3 + c * F, 0, f2 + b * F, F / 4, lane, acc);
-                    const float v = wave_sum(acc[0]) + S[a.s.b3 + c];
-                    if (lane == 0) lg[b * ll.ncp + c] = v;
-                }
+                for (int b = 0; b < Bc; ++b)
+                    for (int c0 = wave * 4; c0 < NC; c0 += 2 * kWaves * 4) {
+                        const int ca = min(c0 + row, NC - 1), cb = min(c0 + kWaves * 4 + row, NC - 1);
+                        const float2 v = row_dot2(S + a.s.w3 + ca * F, S + a.s.w3 + cb * F, f2 + b * F, F / 4, li);
+                        if (li == 0 && c0 + row < NC) lg[b * ll.ncp + ca] = v.x + S[a.s.b3 + ca];
+                        if (li == 0 && c0 + kWaves * 4 + row < NC) lg[b * ll.ncp + cb] = v.y + S[a.s.b3 + cb];
+                    }
         } else {
             if (compute)
-                for (int it = it0; it < Bc * UCv; it += kWaves) {
+                for (int it = it0; it < nC; it += kWaves) {
                     const int b = it / UCv, r = it - b * UCv, j = w * a.UC + r;
-                    float acc[1] = {0.f};
-                    dots<1>(S + a.s.w3 + r * F, 0, f2 + b * F, F / 4, lane, acc);
-                    const float v = wave_sum(acc[0]) + S[a.s.b3 + r];
-                    if (lane == 0) publish(xgLG + b * a.NC + j, tag, v);
+                    const float v = wave_dot(S + a.s.w3 + r * F, f2 + b * F, F / 4, lane) + S[a.s.b3 + r];
+                    if (pub_lane) publish(xgLG + pub_off + b * a.NC + j, tag, v);
+                    count_pub(HOP_LOGITS);
                 }
+            if (poller) wait_own(HOP_LOGITS, t, nC);
             if (poller)
-                gather(xgLG, Bc * a.NC, a.NC, lg, ll.ncp, tag, a.ctl, a.timeout_ticks, t, HOP_LOGITS, abort_flag);
+                gather(xgLG + poll_off, Bc * a.NC, a.NC, tag, a.ctl, a.timeout_ticks, t, HOP_LOGITS, abort_flag,
+                       [&](int b, int j, float v) { lg[b * ll.ncp + j] = v; });
         }
         bar();
+        STAMP(5);
         if (*abort_flag) return;
 
-        // S9: sample one row per wave → x_t                          (:225-237)
+        // ---- sample one row per wave → x_t                          (:225-237)
         if (compute)
             for (int b = it0; b < Bc; b += kWaves) {
                 const float *l = lg + b * ll.ncp;
@@ -430,18 +662,17 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
                 if (a.mol) {
                     // utils/distribution.py:87-123
                     float v = -INFINITY;
-                    if (lane < 10) v = l[lane] - logf(-logf(u[lane]));
+                    if (lane < 10) v = l[lane] - u[lane];          // u[k] = log(-log(u1_k)), prepared by the loader
                     int k = 0;
-                    float best = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
+                    float best = lane_bcast(v, 0);
 #pragma unroll
                     for (int j = 1; j < 10; ++j) {
-                        const float vj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), j));
+                        const float vj = lane_bcast(v, j);
                         if (vj > best) { best = vj; k = j; }
                     }
                     const float mean = l[10 + k];
                     const float ls = fmaxf(l[20 + k], -32.23619130191664f);
-                    const float u2 = u[10];
-                    x = mean + expf(ls) * (logf(u2) - logf(1.0f - u2));
+                    x = mean + expf(ls) * u[10];                      // u[10] = log(u2) − log(1 − u2)
                     x = x < -1.0f ? -1.0f : x;
                     x = x > 1.0f ? 1.0f : x;
                 } else {
@@ -456,18 +687,18 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
                         m = fmaxf(m, e[k]);
                     }
                     m = wave_max(m);
-                    float s = 0.0f;
+                    float s1 = 0.0f;
 #pragma unroll
                     for (int k = 0; k < kClsPerLaneMax; ++k) {
                         const int c = lane + 64 * k;
                         e[k] = (c < NC) ? expf(e[k] - m) : 0.0f;
-                        s += e[k];
+                        s1 += e[k];
                     }
-                    s = wave_sum(s);
+                    s1 = wave_sum(s1);
                     float s2 = 0.0f;
 #pragma unroll
                     for (int k = 0; k < kClsPerLaneMax; ++k) {
-                        e[k] = e[k] / s;
+                        e[k] = e[k] / s1;
                         s2 += e[k];
                     }
                     s2 = wave_sum(s2);
@@ -484,9 +715,10 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
                 if (lane == 0) { xprev[b] = x; lbl[b] = label; }
             }
 
-        // loader: its DMA for step t+1 must have landed before the end-of-step barrier
+        // loader: its DMA for step t+2 has landed before this step ends
         if (loader) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         bar();
+        STAMP(6);
     }
     if (writer && a.L > 0) {
         const size_t o = (size_t)(a.b0 + lane) * a.L + (a.L - 1);

@@ -176,17 +176,24 @@ class WaveRNN(nn.Module):
         return self._loop
 
     # ---------------------------------------------------------------------- generate
+    @torch.no_grad()
     def conditioning(self, mels, batched, target, overlap):
-        """pad → upsample → (fold) → time-major [L][B][feat + 4·aux] (fatchord_version.py:183-190)."""
-        device = next(self.parameters()).device
-        mels = torch.as_tensor(mels, device=device).to(torch.float32)
-        wave_len = (mels.size(-1) - 1) * self.hop_length
-        mels = self.pad_tensor(mels.transpose(1, 2), pad=self.pad, side='both')
-        mels, aux = self.upsample(mels.transpose(1, 2))
-        if batched:
-            mels = self.fold_with_overlap(mels, target, overlap)
-            aux = self.fold_with_overlap(aux, target, overlap)
-        cond = torch.cat([mels, aux], dim=2).transpose(0, 1).contiguous()
+        """pad → upsample → (fold) → time-major [L][B][feat + 4·aux] (fatchord_version.py:183-190).
+        Runs the upsample network in eval mode (BatchNorm running statistics) like generate()."""
+        was_training = self.training
+        self.eval()
+        try:
+            device = next(self.parameters()).device
+            mels = torch.as_tensor(mels, device=device).to(torch.float32)
+            wave_len = (mels.size(-1) - 1) * self.hop_length
+            mels = self.pad_tensor(mels.transpose(1, 2), pad=self.pad, side='both')
+            mels, aux = self.upsample(mels.transpose(1, 2))
+            if batched:
+                mels = self.fold_with_overlap(mels, target, overlap)
+                aux = self.fold_with_overlap(aux, target, overlap)
+            cond = torch.cat([mels, aux], dim=2).transpose(0, 1).contiguous()
+        finally:
+            self.train(was_training)
         return cond, wave_len
 
     def generate(self, mels, save_path: Union[str, Path, None], batched, target, overlap, mu_law, *,
