@@ -48,7 +48,7 @@ def main():
     ap.add_argument("--seconds", type=float, default=5.0, help="utterance length")
     ap.add_argument("--mode", default="MOL", choices=["MOL", "RAW"])
     ap.add_argument("--batched", action="store_true", help="fold-batched generate (target 11000, overlap 550)")
-    ap.add_argument("--cpu-steps", type=int, default=12000, help="oracle steps timed for cpu_baseline (0: skip)")
+    ap.add_argument("--cpu-steps", type=int, default=50000, help="oracle steps timed for cpu_baseline (0: skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -66,10 +66,10 @@ def test_loop_vs_oracle_fresh_seeds(mode, B):
         assert np.abs(out.cpu().numpy() - ref).max() <= gf.MOL_TOL
 
 
-@pytest.mark.parametrize("grid", [64, 128])
+@pytest.mark.parametrize("grid", [128, 200])
 def test_grid_sizes_agree(grid):
-    """Fewer workgroups (more units each) give the same labels: the partition is arithmetic-neutral
-    up to fp32 reduction order; RAW labels must not move."""
+    """Other partitions (4 units per workgroup; 3 units with a ragged last workgroup) give the
+    same labels: the partition only changes fp32 reduction order, RAW labels must not move."""
     fx = gf.load("loop_raw_b1")
     d, state, mels, aux, noise = gf.loop_inputs(fx)
     loop = _loop(d, grid=grid)
