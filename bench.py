@@ -68,8 +68,16 @@ def main():
     mel = torch.from_numpy(syn.make_mel(d.feat_dims, T, seed=1 + rank))[None]
     target, overlap = 11000, 550
 
+    from wavernn_amd import sharding
+
     def step(i):
-        return model.generate(mel, None, args.batched, target, overlap, True, seed=1000 * rank + i, verbose=False)
+        # every rank vocodes its own utterance (global index = i·world + rank, Philox keyed by
+        # it); the finished audio is gathered to rank 0 — the path's only collective
+        g = i * world + rank
+        out = model.generate(mel, None, args.batched, target, overlap, True, seed=1000 + g, verbose=False)
+        if world > 1:
+            sharding.gather_audio({rank: out}, world, dev)
+        return out
 
     for i in range(args.warmup):
         step(-1 - i)

@@ -54,6 +54,11 @@ def main(mode="MOL", B=1, L=2000, grid=0):
         g1 = (pub - st[:, :, 0]) * 10e-3
         g2 = (pub2 - st[:, :, 1]) * 10e-3
         print(f"  critical compute: gru1 (start->publish) {np.median(g1):.3f} us, gru2 (hop A done->publish) {np.median(g2):.3f} us")
+        s9 = (st[:, :, 9] - st[:, :, 1]) * 10e-3
+        s10 = (st[:, :, 10] - st[:, :, 9]) * 10e-3
+        s11 = (st[:, :, 11] - st[:, :, 10]) * 10e-3
+        s13 = (st[:, :, 13] - st[:, :, 11]) * 10e-3
+        print(f"  gru2 detail: bar->start {np.median(s9):.3f}  row_dot {np.median(s10):.3f}  gates {np.median(s11):.3f}  publish {np.median(s13):.3f} us")
         print(f"  hop B polling: passes median {np.median(st[:, :, 14]):.1f} (p90 {np.percentile(st[:, :, 14], 90):.0f}), "
               f"first pass {np.median(st[:, :, 15]) * 10e-3:.3f} us")
         start_skew = (st[:, :, 0] - st[:, :, 0].min(0, keepdims=True)) * 10e-3

@@ -281,7 +281,9 @@ int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise
     // hand-off replicas (WRNN_REPLICAS, default 8), each padded to a 64 KiB boundary
     const char *rep_env = std::getenv("WRNN_REPLICAS");
     const int reps = std::max(1, std::min(64, rep_env ? std::atoi(rep_env) : 8));
-    const long long rep_stride = (((long long)Bc_max * h->NMAX * 8 + 65535) / 65536) * 65536 / 8;
+    const char *gs_env = std::getenv("WRNN_GSTRIDE");
+    const int gstride = std::max(1, std::min(16, gs_env ? std::atoi(gs_env) : 8));
+    const long long rep_stride = (((long long)Bc_max * h->NMAX * 8 * gstride + 65535) / 65536) * 65536 / 8;
     const size_t need_xg = (size_t)kHops * reps * rep_stride;
     if (need_xg > h->xg_cap) {
         if (h->d_xg) HIP_TRY(h, hipFree(h->d_xg));
@@ -312,6 +314,7 @@ int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise
         a.labels = labels;
         a.xg = h->d_xg;
         a.reps = reps;
+        a.gstride = gstride;
         {
             const char *dp = std::getenv("WRNN_DELAY_POLL");
             a.delay_poll = dp ? std::atoi(dp) : 1;

@@ -43,6 +43,7 @@ struct LoopArgs {
     int U, UF, UC, G, NMAX;
     SlabLayout s;
     int delay_poll;               // pollers wait for this WG's own publish before polling
+    int gstride;                  // granule spacing (8 B units): 8 = every value on its own 64-B line
     int reps;                     // replicas of every hand-off vector (consumer w polls w % reps)
     long long rep_stride;         // granules between replicas
     // diagnostics (WRNN_DEBUG_STAMPS): per-stage s_memrealtime stamps, [G][dbg_steps][kStamps]
@@ -82,7 +83,7 @@ __host__ __device__ inline LdsLayout lds_layout(int slab_total, int Bc, int R, i
     l.q = o;     o += round4(6 * U);           // Q1, Q2: W_ih·W_I[:,0] per gate row
     l.xprev = o; o += round4(Bc);
     l.lbl = o;   o += round4(Bc);
-    l.flag = o;  o += 8;                       // abort word + per-hop publish counters
+    l.flag = o;  o += 4 + kHops * kWaves + 4;  // abort word + per-hop, per-wave publish flags
     l.stamp = o; o += kStamps;
     l.total = o;
     return l;

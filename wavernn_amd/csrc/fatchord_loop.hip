@@ -158,7 +158,7 @@ __device__ __noinline__ void record_abort(int *ctl, int code, int step, int hop,
 // On timeout, or when another workgroup has aborted, sets *lds_abort.
 template <typename Store>
 __device__ __forceinline__ void gather(const unsigned long long *g, int n, int N, uint32_t tag, int *ctl,
-                                       long long timeout, int step, int hop, int *lds_abort, Store store,
+                                       long long timeout, int step, int hop, int *lds_abort, int gs, Store store,
                                        unsigned *dbg_slot = nullptr) {
     constexpr int npoll = kPollThreads;
     const int tid = threadIdx.x;
@@ -172,7 +172,7 @@ __device__ __forceinline__ void gather(const unsigned long long *g, int n, int N
 #pragma unroll
         for (int k = 0; k < kGatherMax; ++k)
             if (k < mine && !(done & (1u << k)))
-                v[k] = __hip_atomic_load(g + tid + k * npoll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                v[k] = __hip_atomic_load(g + (size_t)(tid + k * npoll) * gs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
         for (int k = 0; k < kGatherMax; ++k)
             if (k < mine && !(done & (1u << k)) && (uint32_t)(v[k] >> 32) == tag) {
@@ -299,24 +299,30 @@ __device__ __forceinline__ void bar() {
 //   GH2 = W_hh2·h2_{t-1}                       → gh2 = GH2 + b_hh2
 //   V1 = W1·[x_I + h1; a3] + b1                → f1 = relu(W1[:, :R]·h2 + V1)
 //   V2 = W2[:, F:]·a4 + b2                     → f2 = relu(W2[:, :F]·f1 + V2)
+// Template parameters fix the model dims at compile time for the shipped configurations
+// (0 = take the runtime value from LoopArgs): constant trip counts and strides free the
+// registers that let every LDS load of a dot issue before the first FMA waits on one.
+template <int kR, int kF, int kA, int kNC, bool MOL, int kU, int kUF, int kUC>
 __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, row = lane >> 4;
     const int w = blockIdx.x;
-    const int R = a.R, F = a.F, A = a.A, Bc = a.Bc, NK = a.NK, U = a.U, UF = a.UF;
-    const LdsLayout ll = lds_layout(a.s.total, Bc, R, F, A, a.NC, NK, U, UF);
+    const int R = kR ? kR : a.R, F = kF ? kF : a.F, A = kA ? kA : a.A, NC = kNC ? kNC : a.NC;
+    const int U = kU ? kU : a.U, UF = kUF ? kUF : a.UF, UC = MOL ? 0 : (kUC ? kUC : a.UC);
+    const int Bc = a.Bc, NK = MOL ? 11 : NC;
+    const LdsLayout ll = lds_layout(a.s.total, Bc, R, F, A, NC, NK, U, UF);
     const float *S = smem + ll.slab;
     float *h1 = smem + ll.h1, *h2 = smem + ll.h2, *xa = smem + ll.xa, *f1 = smem + ll.f1;
     float *f2 = smem + ll.f2, *lg = smem + ll.lg, *pre = smem + ll.pre, *pc = smem + ll.pc;
     float *q = smem + ll.q, *xprev = smem + ll.xprev;
     int *lbl = reinterpret_cast<int *>(smem + ll.lbl);
     int *abort_flag = reinterpret_cast<int *>(smem + ll.flag);
-    int *pubcnt = abort_flag + 1;                 // [kHops] items this WG has published so far
+    int *pubflag = abort_flag + 4;                // [kHops][kWaves]: step+1 once a wave has published
     unsigned *stamp = reinterpret_cast<unsigned *>(smem + ll.stamp);
     const int RA = R + A, PP = ll.pp, P = R + 3 * A + NK;
     const int Uv = min(U, R - w * U);                 // valid units here
     const int UFv = max(0, min(UF, F - w * UF));
-    const int UCv = a.mol ? 0 : max(0, min(a.UC, a.NC - w * a.UC));
+    const int UCv = MOL ? 0 : max(0, min(UC, NC - w * UC));
     const int nU = Bc * Uv, nF = Bc * UFv, nC = Bc * UCv;
     const bool loader = wave == kLoaderWave;
     const bool compute = !loader;
@@ -335,7 +341,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
         for (int i = tid; i < a.s.total / 4; i += kThreads) dst[i] = src[i];
         for (int i = tid; i < Bc * R; i += kThreads) { h1[i] = 0.0f; h2[i] = 0.0f; }
         if (tid < Bc) { xprev[tid] = 0.0f; lbl[tid] = 0; }   // x = zeros (fatchord_version.py:196)
-        if (tid < 1 + kHops) abort_flag[tid] = 0;
+        if (tid < 4 + kHops * kWaves) abort_flag[tid] = 0;
         for (int t = 0; t < min(2, a.L); ++t)
             for (int i = tid; i < Bc * P; i += kThreads) {
                 const int b = i / P, k = i - b * P;
@@ -344,12 +350,12 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
                 if (k < R) v = a.cI[((size_t)t * Bc + b) * R + k];
                 else if (k < R + 3 * A) v = a.cond[rowi * a.CD + a.feat + A + (k - R)];
                 else if (a.noise) v = a.noise[rowi * NK + (k - R - 3 * A)];
-                else v = philox_noise(a.seed, (unsigned long long)(a.row0 + b), (uint32_t)t, (uint32_t)(k - R - 3 * A), a.mol);
+                else v = philox_noise(a.seed, (unsigned long long)(a.row0 + b), (uint32_t)t, (uint32_t)(k - R - 3 * A), MOL);
                 rec(t)[b * PP + k] = v;
             }
     }
     __syncthreads();
-    if (a.mol)   // step 0's sampler terms (the loader prepares every later step's)
+    if (MOL)   // step 0's sampler terms (the loader prepares every later step's)
         for (int i = tid; i < Bc * 11; i += kThreads) {
             const int b = i / 11, k = i - b * 11;
             float *pz = rec(0) + b * PP + R + 3 * A + k;
@@ -425,14 +431,16 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
     const bool pub_lane = lane < a.reps;
     // Delayed polling (a.delay_poll): the polling threads start their global polls only once
     // this workgroup's own values of the hop are out — fewer useless passes, less traffic.
-    auto count_pub = [&](int hop) {
-        if (lane == 0) __hip_atomic_fetch_add(&pubcnt[hop], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    // A wave marks a hop published after its LAST item of that hop (plain LDS store).
+    auto mark_pub = [&](int hop, int t) {
+        if (lane == 0) reinterpret_cast<volatile int *>(pubflag)[hop * kWaves + wave] = t + 1;
     };
     auto wait_own = [&](int hop, int t, int items) {
         if (!a.delay_poll || items == 0) return;
-        const int want = (t + 1) * items;
-        while (__hip_atomic_load(&pubcnt[hop], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
-            __builtin_amdgcn_s_sleep(1);
+        for (int v = 0; v < kWaves; ++v) {
+            if (first_item(v) >= items) continue;            // wave v publishes nothing here
+            while (reinterpret_cast<volatile int *>(pubflag)[hop * kWaves + v] < t + 1) __builtin_amdgcn_s_sleep(1);
+        }
     };
 
     for (int t = 0; t < a.L; ++t) {
@@ -452,7 +460,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
             // MoL: turn step t+1's draws into the sampler's terms now, off the critical path:
             // u1 → log(-log(u1)) (distribution.py:107), u2 → log(u2) − log(1 − u2) (:119).
             // Same fp32 operations as at sampling time, only earlier.
-            if (a.mol && t + 1 < a.L) {
+            if (MOL && t + 1 < a.L) {
                 float *nz1 = rec(t + 1);
                 for (int i = lane; i < Bc * 11; i += 64) {
                     const int b = i / 11, k = i - b * 11;
@@ -471,7 +479,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
                     if (!a.noise)   // Philox draws: plain LDS writes, issued before the DMAs
                         for (int k = lane; k < NK; k += 64)
                             dst[R + 3 * A + k] = philox_noise(a.seed, (unsigned long long)(a.row0 + b),
-                                                              (uint32_t)t2, (uint32_t)k, a.mol);
+                                                              (uint32_t)t2, (uint32_t)k, MOL);
                     const float *ci = a.cI + ((size_t)t2 * Bc + b) * R;
                     for (int c = 0; c < R; c += 256)
                         if (c + lane * 4 < R)
@@ -504,14 +512,14 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
                     gh[g] = p[PC_GH1 + g] + S[a.s.bhh1 + g * U + u];
                 }
                 const float hn = gru_gate_math(gi[0], gi[1], gi[2], gh[0], gh[1], gh[2], h1[b * R + j]);
-                if (pub_lane) publish(xgH1 + pub_off + b * R + j, tag, hn);
-                count_pub(HOP_H1);
+                if (pub_lane) publish(xgH1 + pub_off + (size_t)(b * R + j) * a.gstride, tag, hn);
                 if (it == it0) STAMP_WAVE(12);
             }
+        if (compute) mark_pub(HOP_H1, t);
         // hop A: h1_t; the pollers also form x = x_I + h1 (:212) and stage a3 next to it
         if (poller) {
             wait_own(HOP_H1, t, nU);
-            gather(xgH1 + poll_off, Bc * R, R, tag, a.ctl, a.timeout_ticks, t, HOP_H1, abort_flag,
+            gather(xgH1 + poll_off, Bc * R, R, tag, a.ctl, a.timeout_ticks, t, HOP_H1, abort_flag, a.gstride,
                    [&](int b, int j, float v) {
                        h1[b * R + j] = v;
                        xa[b * RA + j] = fmaf(wi0[j], xprev[b], cur[b * PP + j]) + v;
@@ -529,7 +537,9 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
         if (compute) {
             for (int it = it0; it < nU; it += kWaves) {
                 const int b = it / Uv, u = it - b * Uv, j = w * U + u;
+                if (it == it0) STAMP_WAVE(9);
                 const float v = row_dot(S + a.s.wih2 + ((row < 3 ? row : 0) * U + u) * RA, h1 + b * R, R / 4, li);
+                if (it == it0) STAMP_WAVE(10);
                 const float x = xprev[b];
                 const float *p = PC(b, u);
                 float gi[3], gh[3];
@@ -539,10 +549,11 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
                     gh[g] = p[PC_GH2 + g] + S[a.s.bhh2 + g * U + u];
                 }
                 const float hn = gru_gate_math(gi[0], gi[1], gi[2], gh[0], gh[1], gh[2], h2[b * R + j]);
-                if (pub_lane) publish(xgH2 + pub_off + b * R + j, tag, hn);
-                count_pub(HOP_H2);
+                if (it == it0) STAMP_WAVE(11);
+                if (pub_lane) publish(xgH2 + pub_off + (size_t)(b * R + j) * a.gstride, tag, hn);
                 if (it == it0) STAMP_WAVE(13);
             }
+            mark_pub(HOP_H2, t);
             for (int it = it0; it < nU; it += kWaves) {     // GH1_{t+1} = W_hh1·h1_t
                 const int b = it / Uv, u = it - b * Uv;
                 const float v = row_dot(S + a.s.whh1 + ((row < 3 ? row : 0) * U + u) * R, h1 + b * R, R / 4, li);
@@ -562,7 +573,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
         }
         if (poller) wait_own(HOP_H2, t, nU);
         if (poller)
-            gather(xgH2 + poll_off, Bc * R, R, tag, a.ctl, a.timeout_ticks, t, HOP_H2, abort_flag,
+            gather(xgH2 + poll_off, Bc * R, R, tag, a.ctl, a.timeout_ticks, t, HOP_H2, abort_flag, a.gstride,
                    [&](int b, int j, float v) { h2[b * R + j] = v; }, dbg_on ? stamp + 14 : nullptr);
         bar();
         STAMP(2);
@@ -573,9 +584,9 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
             for (int it = it0; it < nF; it += kWaves) {
                 const int b = it / UFv, r = it - b * UFv, j = w * UF + r;
                 const float v = wave_dot(S + a.s.w1 + r * RA, h2 + b * R, R / 4, lane) + PC(b, r)[PC_V1];
-                if (pub_lane) publish(xgF1 + pub_off + b * F + j, tag, v > 0.0f ? v : 0.0f);
-                count_pub(HOP_F1);
+                if (pub_lane) publish(xgF1 + pub_off + (size_t)(b * F + j) * a.gstride, tag, v > 0.0f ? v : 0.0f);
             }
+            mark_pub(HOP_F1, t);
             for (int it = it0; it < nU; it += kWaves) {     // GH2_{t+1} = W_hh2·h2_t
                 const int b = it / Uv, u = it - b * Uv;
                 const float v = row_dot(S + a.s.whh2 + ((row < 3 ? row : 0) * U + u) * R, h2 + b * R, R / 4, li);
@@ -595,7 +606,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
         }
         if (poller) wait_own(HOP_F1, t, nF);
         if (poller)
-            gather(xgF1 + poll_off, Bc * F, F, tag, a.ctl, a.timeout_ticks, t, HOP_F1, abort_flag,
+            gather(xgF1 + poll_off, Bc * F, F, tag, a.ctl, a.timeout_ticks, t, HOP_F1, abort_flag, a.gstride,
                    [&](int b, int j, float v) { f1[b * F + j] = v; });
         bar();
         STAMP(3);
@@ -606,9 +617,9 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
             for (int it = it0; it < nF; it += kWaves) {
                 const int b = it / UFv, r = it - b * UFv, j = w * UF + r;
                 const float v = wave_dot(S + a.s.w2 + r * (F + A), f1 + b * F, F / 4, lane) + PC(b, r)[PC_V2];
-                if (pub_lane) publish(xgF2 + pub_off + b * F + j, tag, v > 0.0f ? v : 0.0f);
-                count_pub(HOP_F2);
+                if (pub_lane) publish(xgF2 + pub_off + (size_t)(b * F + j) * a.gstride, tag, v > 0.0f ? v : 0.0f);
             }
+            mark_pub(HOP_F2, t);
             if (t + 1 < a.L)
                 for (int it = it0; it < nU; it += kWaves) {
                     const int b = it / Uv, u = it - b * Uv;
@@ -617,16 +628,15 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
         }
         if (poller) wait_own(HOP_F2, t, nF);
         if (poller)
-            gather(xgF2 + poll_off, Bc * F, F, tag, a.ctl, a.timeout_ticks, t, HOP_F2, abort_flag,
+            gather(xgF2 + poll_off, Bc * F, F, tag, a.ctl, a.timeout_ticks, t, HOP_F2, abort_flag, a.gstride,
                    [&](int b, int j, float v) { f2[b * F + j] = v; });
         bar();
         STAMP(4);
         if (*abort_flag) return;
 
         // ---- fc3 (:223)
-        if (a.mol) {
+        if (MOL) {
             // all rows redundantly in every workgroup (bit-identical everywhere); 16-lane rows
-            const int NC = a.NC;
             if (compute)
                 for (int b = 0; b < Bc; ++b)
                     for (int c0 = wave * 4; c0 < NC; c0 += 2 * kWaves * 4) {
@@ -638,14 +648,14 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
         } else {
             if (compute)
                 for (int it = it0; it < nC; it += kWaves) {
-                    const int b = it / UCv, r = it - b * UCv, j = w * a.UC + r;
+                    const int b = it / UCv, r = it - b * UCv, j = w * UC + r;
                     const float v = wave_dot(S + a.s.w3 + r * F, f2 + b * F, F / 4, lane) + S[a.s.b3 + r];
-                    if (pub_lane) publish(xgLG + pub_off + b * a.NC + j, tag, v);
-                    count_pub(HOP_LOGITS);
+                    if (pub_lane) publish(xgLG + pub_off + (size_t)(b * NC + j) * a.gstride, tag, v);
                 }
+            if (compute) mark_pub(HOP_LOGITS, t);
             if (poller) wait_own(HOP_LOGITS, t, nC);
             if (poller)
-                gather(xgLG + poll_off, Bc * a.NC, a.NC, tag, a.ctl, a.timeout_ticks, t, HOP_LOGITS, abort_flag,
+                gather(xgLG + poll_off, Bc * NC, NC, tag, a.ctl, a.timeout_ticks, t, HOP_LOGITS, abort_flag, a.gstride,
                        [&](int b, int j, float v) { lg[b * ll.ncp + j] = v; });
         }
         bar();
@@ -659,7 +669,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
                 const float *u = cur + b * PP + R + 3 * A;               // this step's noise
                 float x;
                 int label = 0;
-                if (a.mol) {
+                if (MOL) {
                     // utils/distribution.py:87-123
                     float v = -INFINITY;
                     if (lane < 10) v = l[lane] - u[lane];          // u[k] = log(-log(u1_k)), prepared by the loader
@@ -677,8 +687,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
                     x = x > 1.0f ? 1.0f : x;
                 } else {
                     // softmax → Categorical renormalise → argmax(p / q)
-                    const int NC = a.NC;
-                    float e[kClsPerLaneMax];
+                                        float e[kClsPerLaneMax];
                     float m = -INFINITY;
 #pragma unroll
                     for (int k = 0; k < kClsPerLaneMax; ++k) {
@@ -786,18 +795,43 @@ hipError_t launch_ci_gemm(const float *cond, int CD, int Bt, int b0, int Bc, int
     return hipGetLastError();
 }
 
+// Shipped instantiations: the 800k-step hparams (rnn 512, fc 512, aux 32) at one workgroup
+// per CU of a 256-CU MI355X (2 units/workgroup), and a fully runtime-dimensioned fallback.
+#define WRNN_K_MOL512 fatchord_loop_kernel<512, 512, 32, 30, true, 2, 2, 0>
+#define WRNN_K_RAW512 fatchord_loop_kernel<512, 512, 32, 512, false, 2, 2, 2>
+#define WRNN_K_MOLGEN fatchord_loop_kernel<0, 0, 0, 0, true, 0, 0, 0>
+#define WRNN_K_RAWGEN fatchord_loop_kernel<0, 0, 0, 0, false, 0, 0, 0>
+
+static const void *pick_loop_kernel(const LoopArgs &a) {
+    const bool d512 = a.R == 512 && a.F == 512 && a.A == 32 && a.U == 2 && a.UF == 2;
+    if (a.mol) return d512 && a.NC == 30 ? (const void *)WRNN_K_MOL512 : (const void *)WRNN_K_MOLGEN;
+    return d512 && a.NC == 512 && a.UC == 2 ? (const void *)WRNN_K_RAW512 : (const void *)WRNN_K_RAWGEN;
+}
+
 hipError_t launch_loop(const LoopArgs &a, size_t lds_bytes, hipStream_t st) {
-    hipLaunchKernelGGL(fatchord_loop_kernel, dim3(a.G), dim3(kThreads), lds_bytes, st, a);
-    return hipGetLastError();
+    const void *k = pick_loop_kernel(a);
+    LoopArgs args = a;
+    void *params[] = {&args};
+    return hipLaunchKernel(k, dim3(a.G), dim3(kThreads), params, lds_bytes, st);
 }
 
 hipError_t prepare_loop_kernel(int max_lds_bytes) {
-    return hipFuncSetAttribute((const void *)fatchord_loop_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               max_lds_bytes);
+    for (const void *k : {(const void *)WRNN_K_MOL512, (const void *)WRNN_K_RAW512, (const void *)WRNN_K_MOLGEN,
+                          (const void *)WRNN_K_RAWGEN}) {
+        hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds_bytes);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t loop_occupancy(int *blocks_per_cu, size_t lds_bytes) {
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fatchord_loop_kernel, kThreads, lds_bytes);
+    // the generic instantiations use the most registers: bound residency by them
+    int a = 0, b = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, WRNN_K_MOLGEN, kThreads, lds_bytes);
+    if (e != hipSuccess) return e;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, WRNN_K_RAWGEN, kThreads, lds_bytes);
+    *blocks_per_cu = a < b ? a : b;
+    return e;
 }
 
 }  // namespace wrnn

@@ -1,0 +1,77 @@
+"""Utterance sharding across GPUs (one process per GPU, torch.distributed).
+
+The reference generates one utterance at a time on one device (gen_wavernn.py:11-35 loops
+over the test set).  Utterances are independent, so the MI355X path shards them: utterance i
+runs on rank i % world, with its sampler draws keyed by the global utterance index (Philox
+seed = base_seed + i), so the audio does not depend on how many GPUs ran the job.  The only
+collective is the final gather of finished audio to rank 0 (RCCL over xGMI under the "nccl"
+backend; gloo on CPU for tests) — there is no exchange inside the sample loop.
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def shard_indices(n_items: int, rank: int, world: int) -> List[int]:
+    """Round-robin assignment: item i → rank i % world."""
+    return list(range(rank, n_items, world))
+
+
+def gather_audio(local: Dict[int, np.ndarray], n_items: int, device: torch.device,
+                 group=None) -> Optional[List[np.ndarray]]:
+    """Collect {global index: float64 audio} from every rank on rank 0, in global order.
+
+    Shapes differ per utterance, so each rank packs its outputs into a [n_slots, L_max] fp32
+    tensor plus an int64 [n_slots, 2] (index, length) table; two all-gathers move them.  fp32
+    on the wire is exact for the float32 samples the loop produced; the float64 host
+    post-processing is re-applied by the caller if it needs it (here the values are the
+    already post-processed float64 audio cast to fp32, as save_wav writes)."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    n_slots = (n_items + world - 1) // world
+    lens = torch.tensor([max((len(v) for v in local.values()), default=0)], dtype=torch.int64, device=device)
+    dist.all_reduce(lens, op=dist.ReduceOp.MAX, group=group)
+    L = int(lens.item())
+    data = torch.zeros(n_slots, max(L, 1), dtype=torch.float32, device=device)
+    meta = torch.full((n_slots, 2), -1, dtype=torch.int64, device=device)
+    for s, (idx, audio) in enumerate(sorted(local.items())):
+        data[s, :len(audio)] = torch.as_tensor(np.asarray(audio, dtype=np.float32), device=device)
+        meta[s, 0], meta[s, 1] = idx, len(audio)
+    if dist.get_backend(group) == "nccl":
+        all_data = torch.empty(world * n_slots, data.shape[1], dtype=data.dtype, device=device)
+        all_meta = torch.empty(world * n_slots, 2, dtype=meta.dtype, device=device)
+        dist.all_gather_into_tensor(all_data, data, group=group)
+        dist.all_gather_into_tensor(all_meta, meta, group=group)
+    else:
+        dl = [torch.empty_like(data) for _ in range(world)]
+        ml = [torch.empty_like(meta) for _ in range(world)]
+        dist.all_gather(dl, data, group=group)
+        dist.all_gather(ml, meta, group=group)
+        all_data, all_meta = torch.cat(dl), torch.cat(ml)
+    if rank != 0:
+        return None
+    out: List[Optional[np.ndarray]] = [None] * n_items
+    all_data = all_data.cpu().numpy()
+    for row, (idx, n) in enumerate(all_meta.cpu().numpy()):
+        if idx >= 0:
+            out[int(idx)] = all_data[row, :int(n)].astype(np.float64)
+    return out  # type: ignore[return-value]
+
+
+def generate_sharded(model, mels: Sequence, batched: bool, target: int, overlap: int, mu_law: bool,
+                     base_seed: int = 0, device: Optional[torch.device] = None, group=None,
+                     generate_fn: Optional[Callable] = None) -> Optional[List[np.ndarray]]:
+    """Generate every mel in `mels` across the process group; rank 0 returns the list of
+    float64 waveforms in input order, other ranks return None."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if device is None:
+        device = next(model.parameters()).device
+    gen = generate_fn or (lambda i, m: model.generate(m, None, batched, target, overlap, mu_law,
+                                                      seed=base_seed + i, verbose=False))
+    local = {i: gen(i, mels[i]) for i in shard_indices(len(mels), rank, world)}
+    return gather_audio(local, len(mels), device, group)
