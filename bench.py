@@ -29,6 +29,16 @@ sys.path.insert(0, REPO)
 from wavernn_amd import synthetic as syn  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
+PMC_PROFILE = os.path.join(REPO, "profiles", "r01_v3_pmc_traffic.json")
+
+
+def pmc_traffic_bytes(mode: str, batched: bool, seconds: float):
+    """HBM-side bytes per launch from the committed rocprofv3 PMC passes (FETCH_SIZE +
+    WRITE_SIZE, separate passes) for this exact workload, or None."""
+    if mode != "MOL" or batched or abs(seconds - 5.0) > 1e-9 or not os.path.exists(PMC_PROFILE):
+        return None
+    c = json.load(open(PMC_PROFILE))["counters"]
+    return 1024.0 * (c["FETCH_SIZE"]["value_kib"] + c["WRITE_SIZE"]["value_kib"])
 COND_BYTES_PER_ROW_STEP = 836  # 208 fp32 conditioning + 1 fp32 output (SURVEY.md §8(d))
 
 
@@ -137,9 +147,12 @@ def main():
             "us_per_loop_step": loop_ms_max * 1e3 / L,
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                "note": "algorithmic bytes = all loop weights (fp32) per step + 836 B/row-step, per launch; "
-                        "weights are LDS-resident so actual HBM traffic is far lower",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": pmc_traffic_bytes(args.mode, args.batched, args.seconds),
+                "note": "achieved = algorithmic bytes (all loop weights fp32 per step + 836 B/row-step) per launch "
+                        "/ launch time (HIP events); weights are LDS-resident, the kernel is hand-off-latency bound. "
+                        "traffic = FETCH_SIZE+WRITE_SIZE bytes per launch from profiles/r01_v3_pmc_traffic.json: "
+                        "granule polling/publishing, not weight streaming",
             },
         }
         if args.cpu_steps > 0 and world == 1:
