@@ -23,7 +23,9 @@ __device__ __forceinline__ void store16_sc1(unsigned long long *p, unsigned long
     asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 
-template <int SLEEP>
+// v4: the poll pass issues NG unconditional loads (addresses clamped into range), then checks
+// them: one memory round trip per pass instead of one per guarded load.
+template <int NG>
 __global__ __launch_bounds__(256) void hop_kernel_v3(unsigned long long *buf, long long rep_stride, int per_wg, int pad,
                                                      int reps, int rounds, unsigned long long *out, int full, int delay,
                                                      int pollers) {
@@ -33,39 +35,28 @@ __global__ __launch_bounds__(256) void hop_kernel_v3(unsigned long long *buf, lo
     for (int r = 0; r < rounds; ++r) {
         const unsigned tag = r + 1;
         if (wave == 3) {
-            if (full) {
-                const int lanes_per_rep = pad / 2;
-                const int rep = lane / lanes_per_rep, q = lane % lanes_per_rep;
-                if (rep < reps) {
-                    const unsigned long long x = ((unsigned long long)tag << 32);
-                    store16_sc1(buf + rep * rep_stride + (size_t)blockIdx.x * pad + 2 * q, x | (2 * q), x | (2 * q + 1));
-                }
-            } else if (lane < reps) {
+            if (lane < reps)
                 for (int u = 0; u < per_wg; ++u)
                     __hip_atomic_store(buf + lane * rep_stride + (size_t)blockIdx.x * pad + u,
                                        ((unsigned long long)tag << 32) | u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
         } else if (wave < pollers) {
-            for (int d = 0; d < delay; ++d) __builtin_amdgcn_s_sleep(1);
             const unsigned long long *g = buf + (size_t)(blockIdx.x % reps) * rep_stride;
             const int np = 64 * pollers;
-            const int mine = (N + np - 1) / np;
-            unsigned long long v[16];
-            unsigned done = 0, all = (1u << mine) - 1;
-            while (done != all) {
+            const unsigned long long *addr[NG];
 #pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    const int i = tid + k * np;
-                    if (k < mine && !(done & (1u << k)) && i < N)
-                        v[k] = __hip_atomic_load(g + (size_t)(i / per_wg) * pad + (i % per_wg), __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-                }
+            for (int k = 0; k < NG; ++k) {
+                int i = tid + k * np;
+                i = i < N ? i : (tid < N ? tid : 0);
+                addr[k] = g + (size_t)(i / per_wg) * pad + (i % per_wg);
+            }
+            for (;;) {
+                unsigned long long v[NG];
 #pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    const int i = tid + k * np;
-                    if (k < mine && !(done & (1u << k)) && (i >= N || (unsigned)(v[k] >> 32) >= tag)) done |= 1u << k;
-                }
-                if (SLEEP && done != all) __builtin_amdgcn_s_sleep(1);
+                for (int k = 0; k < NG; ++k) v[k] = __hip_atomic_load(addr[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                bool ok = true;
+#pragma unroll
+                for (int k = 0; k < NG; ++k) ok &= (unsigned)(v[k] >> 32) >= tag;
+                if (ok) break;
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -138,22 +129,26 @@ int main() {
     hipMalloc(&out, 256 * 8);
     std::vector<unsigned long long> h(256);
     const int rounds = 1000;
-    printf("%5s %5s %4s %6s %10s\n", "grid", "perwg", "pad", "pollw", "us/hop");
-    for (int per_wg : {1, 2})
+    printf("%5s %5s %4s %4s %6s %10s\n", "grid", "perwg", "pad", "reps", "pollw", "us/hop");
+    for (int reps : {1, 8})
         for (int pad : {0, 8})
-            for (int grid : {2, 4, 8, 16, 32, 64, 128, 256}) {
-                const int padv = pad ? pad : per_wg;
-                const int pw = grid * per_wg > 128 ? 2 : 1;
-                const long long stride = ((long long)grid * padv * 8 + 65535) / 65536 * 65536 / 8;
-                hipMemset(buf, 0, bytes);
-                hipLaunchKernelGGL(hop_kernel_v3<0>, dim3(grid), dim3(256), 0, 0, buf, stride, per_wg, padv, 1, rounds, out,
-                                   0, 0, pw);
-                hipDeviceSynchronize();
-                hipMemcpy(h.data(), out, grid * 8, hipMemcpyDeviceToHost);
-                double mx = 0;
-                for (int i = 0; i < grid; ++i) mx = h[i] > mx ? h[i] : mx;
-                printf("%5d %5d %4d %6d %10.3f\n", grid, per_wg, padv, pw, mx * 10e-3 / rounds);
-                fflush(stdout);
+            for (int grid : {2, 8, 32, 64, 128, 256}) {
+                const int per_wg = grid == 256 ? 2 : (grid >= 64 ? 512 / grid : 2);
+                const int padv = pad ? (pad > per_wg ? pad : per_wg) : per_wg;
+                const int N = grid * per_wg;
+                for (int pw : {1, 2}) {
+                    const int ng = (N + 64 * pw - 1) / (64 * pw);
+                    const long long stride = ((long long)grid * padv * 8 + 65535) / 65536 * 65536 / 8;
+                    hipMemset(buf, 0, bytes);
+                    auto k = ng <= 1 ? hop_kernel_v3<1> : ng <= 2 ? hop_kernel_v3<2> : ng <= 4 ? hop_kernel_v3<4> : hop_kernel_v3<8>;
+                    hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, 0, buf, stride, per_wg, padv, reps, rounds, out, 0, 0, pw);
+                    hipDeviceSynchronize();
+                    hipMemcpy(h.data(), out, grid * 8, hipMemcpyDeviceToHost);
+                    double mx = 0;
+                    for (int i = 0; i < grid; ++i) mx = h[i] > mx ? h[i] : mx;
+                    printf("%5d %5d %4d %4d %6d %10.3f\n", grid, per_wg, padv, reps, pw, mx * 10e-3 / rounds);
+                    fflush(stdout);
+                }
             }
     return 0;
 }

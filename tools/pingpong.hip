@@ -64,6 +64,49 @@ __global__ __launch_bounds__(256) void xchg(unsigned long long *w, int rounds, u
     if (threadIdx.x == 0) out[me] = __builtin_amdgcn_s_memrealtime() - t0;
 }
 
+// Bisect xchg (0.7 us) → hopbench (1.45 us):
+// V 0: poll only the other's word; 1: poll own + other's word (same line, adjacent)
+// 2: as 1 but the words 512 B apart; 3: as 1 with two lanes polling one word each
+template <int V>
+__global__ __launch_bounds__(256) void xchg2(unsigned long long *w, int rounds, unsigned long long *out) {
+    const int me = blockIdx.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int sp = V == 2 ? 64 : 1;
+    unsigned long long *mine = w + me * sp;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (int r = 1; r <= rounds; ++r) {
+        if (wave == 3 && lane == 0) __hip_atomic_store(mine, (unsigned long long)r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (wave == 0) {
+            if (V == 0) {
+                if (lane == 0) while (__hip_atomic_load(w + (1 - me) * sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned long long)r) {}
+            } else if (V == 3) {
+                if (lane < 2) while (__hip_atomic_load(w + lane * sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned long long)r) {}
+            } else if (lane == 0) {
+                for (;;) {
+                    unsigned long long a = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    unsigned long long b = __hip_atomic_load(w + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (a >= (unsigned long long)r && b >= (unsigned long long)r) break;
+                }
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    }
+    if (threadIdx.x == 0) out[me] = __builtin_amdgcn_s_memrealtime() - t0;
+}
+
+template <int V>
+void runx2(unsigned long long *w, unsigned long long *out) {
+    const int rounds = 2000;
+    hipMemset(w, 0, 1 << 20);
+    hipLaunchKernelGGL((xchg2<V>), dim3(2), dim3(256), 0, 0, w, rounds, out);
+    hipDeviceSynchronize();
+    unsigned long long h[2];
+    hipMemcpy(h, out, 16, hipMemcpyDeviceToHost);
+    printf("bisect V%d: %.3f us per round\n", V, (h[0] > h[1] ? h[0] : h[1]) * 10e-3 / rounds);
+    fflush(stdout);
+}
+
 template <int MODE>
 void runx(unsigned long long *w, unsigned long long *out, int threads) {
     const int rounds = 2000;
@@ -93,6 +136,10 @@ int main() {
     unsigned long long *w, *out;
     hipMalloc(&w, 1 << 20);
     hipMalloc(&out, 64);
+    runx2<0>(w, out);
+    runx2<1>(w, out);
+    runx2<2>(w, out);
+    runx2<3>(w, out);
     runx<0>(w, out, 64);
     runx<0>(w, out, 256);
     runx<1>(w, out, 256);

@@ -22,6 +22,7 @@ hipError_t launch_ci_gemm(const float *cond, int CD, int Bt, int b0, int Bc, int
 hipError_t launch_loop(const LoopArgs &a, size_t lds_bytes, hipStream_t st);
 hipError_t prepare_loop_kernel(int max_lds_bytes);
 hipError_t loop_occupancy(int *blocks_per_cu, size_t lds_bytes);
+bool loop_has_fast_path(int R, int F, int A, int NC, bool mol, int U, int UF, int UC);
 }  // namespace wrnn
 
 using namespace wrnn;
@@ -202,7 +203,10 @@ int wrnn_create(const wrnn_config *cfg, int device, wrnn_t **out) {
     h->max_rows = 0;
     for (int b = 1; b <= 64; ++b) {
         if (lds_bytes_for(*h, b) > (size_t)h->max_lds) break;
-        if ((size_t)b * h->NMAX > (size_t)kPollThreads * kGatherMax) break;
+        // one polling wave: kGatherMax slots per lane in the generic kernels, exact counts (rows ≤ 2)
+        // in the compile-time-dims ones
+        const bool fast = loop_has_fast_path(R, F, c.aux_dims, c.n_classes, mol, h->U, h->UF, h->UC);
+        if (fast ? b > 2 : (size_t)b * h->NMAX > (size_t)kPollThreads * kGatherMax) break;
         h->max_rows = b;
     }
     if (h->max_rows < 1)
@@ -281,9 +285,9 @@ int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise
     // hand-off replicas (WRNN_REPLICAS, default 8), each padded to a 64 KiB boundary
     const char *rep_env = std::getenv("WRNN_REPLICAS");
     const int reps = std::max(1, std::min(64, rep_env ? std::atoi(rep_env) : 8));
-    const char *gs_env = std::getenv("WRNN_GSTRIDE");
-    const int gstride = std::max(1, std::min(16, gs_env ? std::atoi(gs_env) : 8));
-    const long long rep_stride = (((long long)Bc_max * h->NMAX * 8 * gstride + 65535) / 65536) * 65536 / 8;
+    // replica stride ≥ 64 KiB: keeps replicas on different lines/channels and makes the
+    // pollers' fixed-count over-reads (slots ≥ n) land in allocated memory
+    const long long rep_stride = (((long long)Bc_max * h->NMAX * 8 + 65535) / 65536) * 65536 / 8;
     const size_t need_xg = (size_t)kHops * reps * rep_stride;
     if (need_xg > h->xg_cap) {
         if (h->d_xg) HIP_TRY(h, hipFree(h->d_xg));
@@ -314,7 +318,6 @@ int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise
         a.labels = labels;
         a.xg = h->d_xg;
         a.reps = reps;
-        a.gstride = gstride;
         {
             const char *dp = std::getenv("WRNN_DELAY_POLL");
             a.delay_poll = dp ? std::atoi(dp) : 1;

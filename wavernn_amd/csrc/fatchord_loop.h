@@ -6,16 +6,16 @@ namespace wrnn {
 
 // Wave roles.  vmcnt is in-order per wave, so a wave that polls hand-off granules must not
 // have slow loads (next step's conditioning) or its own publish stores outstanding:
-//   waves 0,1  poll (gather); compute only when a stage has more than 2 work items
-//   waves 2,3  compute + publish
+//   wave  0    polls (gather); computes only when a stage has more than 3 work items
+//   waves 1-3  compute + publish
 //   wave  4    loader: LDS-DMA of step t+1's record, Philox noise, output stores.  It never
 //              reads LDS while its DMA is in flight (hipcc would drain vmcnt before the read).
 constexpr int kCompute = 256;          // waves 0..3
 constexpr int kWaves = kCompute / 64;
 constexpr int kThreads = kCompute + 64;
 constexpr int kLoaderWave = 4;
-constexpr int kPollThreads = 128;
-constexpr int kGatherMax = 8;          // granules per polling thread per hand-off
+constexpr int kPollThreads = 64;
+constexpr int kGatherMax = 8;          // granules per polling lane per hand-off (generic kernels)
 constexpr int kClsPerLaneMax = 8;      // RAW softmax classes per lane (n_classes <= 512)
 constexpr int kHops = 5;               // h1, h2, f1, f2, logits(RAW)
 
@@ -43,7 +43,6 @@ struct LoopArgs {
     int U, UF, UC, G, NMAX;
     SlabLayout s;
     int delay_poll;               // pollers wait for this WG's own publish before polling
-    int gstride;                  // granule spacing (8 B units): 8 = every value on its own 64-B line
     int reps;                     // replicas of every hand-off vector (consumer w polls w % reps)
     long long rep_stride;         // granules between replicas
     // diagnostics (WRNN_DEBUG_STAMPS): per-stage s_memrealtime stamps, [G][dbg_steps][kStamps]

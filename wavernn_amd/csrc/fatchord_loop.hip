@@ -154,37 +154,40 @@ __device__ __noinline__ void record_abort(int *ctl, int code, int step, int hop,
 }
 
 // Gather n = Bc·N granules of one hop; store(b, j, v) puts each value where it belongs.
-// Called by the `npoll` polling threads only; each keeps all its polls of a pass in flight.
+// Called by the kPollThreads polling lanes only.  A pass issues NG UNCONDITIONAL loads
+// (out-of-range slots re-read a valid granule) and only then inspects them: guarding each
+// load with a runtime condition makes hipcc branch around it and wait vmcnt(0) per load,
+// i.e. NG serialized memory round trips per pass (measured: 2-4x slower hops).
 // On timeout, or when another workgroup has aborted, sets *lds_abort.
-template <typename Store>
+template <int NG, typename Store>
 __device__ __forceinline__ void gather(const unsigned long long *g, int n, int N, uint32_t tag, int *ctl,
-                                       long long timeout, int step, int hop, int *lds_abort, int gs, Store store,
+                                       long long timeout, int step, int hop, int *lds_abort, Store store,
                                        unsigned *dbg_slot = nullptr) {
-    constexpr int npoll = kPollThreads;
+    // the granule buffer is padded (replica stride >= 64 KiB) so slots >= n are readable
     const int tid = threadIdx.x;
-    const int mine = (n - tid + npoll - 1) / npoll;   // tid < npoll
-    unsigned long long v[kGatherMax];
-    const uint32_t all = (mine <= 0) ? 0u : (mine >= 32 ? 0xFFFFFFFFu : ((1u << mine) - 1u));
-    uint32_t done = 0;
+    const unsigned long long *gp = g + tid;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     unsigned spins = 0;
-    while (done != all) {
+    for (;;) {
+        unsigned long long v[NG];
 #pragma unroll
-        for (int k = 0; k < kGatherMax; ++k)
-            if (k < mine && !(done & (1u << k)))
-                v[k] = __hip_atomic_load(g + (size_t)(tid + k * npoll) * gs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int k = 0; k < NG; ++k) v[k] = __hip_atomic_load(gp + k * kPollThreads, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool ok = true;
 #pragma unroll
-        for (int k = 0; k < kGatherMax; ++k)
-            if (k < mine && !(done & (1u << k)) && (uint32_t)(v[k] >> 32) == tag) {
-                const int i = tid + k * npoll;
-                const int b = i / N;
-                store(b, i - b * N, __uint_as_float((uint32_t)v[k]));
-                done |= 1u << k;
+        for (int k = 0; k < NG; ++k) ok &= (tid + k * kPollThreads >= n) | ((uint32_t)(v[k] >> 32) == tag);
+        if (dbg_slot && spins == 0 && tid == 0) dbg_slot[1] = (unsigned)(__builtin_amdgcn_s_memrealtime() - t0);
+        if (ok) {
+#pragma unroll
+            for (int k = 0; k < NG; ++k) {
+                const int i = tid + k * kPollThreads;
+                if (i < n) {
+                    const int b = i / N;
+                    store(b, i - b * N, __uint_as_float((uint32_t)v[k]));
+                }
             }
-        if (dbg_slot && spins == 0 && threadIdx.x == 0)
-            dbg_slot[1] = (unsigned)(__builtin_amdgcn_s_memrealtime() - t0);
-        if (done == all) break;
-        if ((++spins & 31u) == 0) {
+            break;
+        }
+        if ((++spins & 63u) == 0) {
             const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - t0) > timeout;
             const bool other = __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
             if (late || other) {
@@ -193,13 +196,12 @@ __device__ __forceinline__ void gather(const unsigned long long *g, int n, int N
                 break;
             }
         }
-        __builtin_amdgcn_s_sleep(1);
     }
-    if (dbg_slot && threadIdx.x == 0) dbg_slot[0] = spins + 1;
+    if (dbg_slot && tid == 0) dbg_slot[0] = spins + 1;
 }
 
-// Stage work item `it` → wave: items 0,1 go to the non-polling waves 2,3 first.
-__device__ __forceinline__ int first_item(int wave) { return (wave + 2) & (kWaves - 1); }
+// Stage work item `it` → wave: items go to the non-polling waves 1,2,3 first, the poller last.
+__device__ __forceinline__ int first_item(int wave) { return (wave + kWaves - 1) & (kWaves - 1); }
 
 // ---- 16-lane row dots: a wave holds four DPP rows; row r (= lane >> 4) computes one dot,
 // lane li (= lane & 15) of the row takes float4 chunks li, li+16, …
@@ -302,14 +304,18 @@ __device__ __forceinline__ void bar() {
 // Template parameters fix the model dims at compile time for the shipped configurations
 // (0 = take the runtime value from LoopArgs): constant trip counts and strides free the
 // registers that let every LDS load of a dot issue before the first FMA waits on one.
-template <int kR, int kF, int kA, int kNC, bool MOL, int kU, int kUF, int kUC>
+template <int kR, int kF, int kA, int kNC, bool MOL, int kU, int kUF, int kUC, int kB>
 __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, row = lane >> 4;
     const int w = blockIdx.x;
     const int R = kR ? kR : a.R, F = kF ? kF : a.F, A = kA ? kA : a.A, NC = kNC ? kNC : a.NC;
     const int U = kU ? kU : a.U, UF = kUF ? kUF : a.UF, UC = MOL ? 0 : (kUC ? kUC : a.UC);
-    const int Bc = a.Bc, NK = MOL ? 11 : NC;
+    const int Bc = kB ? kB : a.Bc, NK = MOL ? 11 : NC;
+    // polls per lane per hop: exact when rows and dims are compile-time, else the maximum
+    constexpr int NG_R = (kB && kR) ? (kB * kR + kPollThreads - 1) / kPollThreads : kGatherMax;
+    constexpr int NG_F = (kB && kF) ? (kB * kF + kPollThreads - 1) / kPollThreads : kGatherMax;
+    constexpr int NG_C = (kB && kNC) ? (kB * kNC + kPollThreads - 1) / kPollThreads : kGatherMax;
     const LdsLayout ll = lds_layout(a.s.total, Bc, R, F, A, NC, NK, U, UF);
     const float *S = smem + ll.slab;
     float *h1 = smem + ll.h1, *h2 = smem + ll.h2, *xa = smem + ll.xa, *f1 = smem + ll.f1;
@@ -512,14 +518,14 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
                     gh[g] = p[PC_GH1 + g] + S[a.s.bhh1 + g * U + u];
                 }
                 const float hn = gru_gate_math(gi[0], gi[1], gi[2], gh[0], gh[1], gh[2], h1[b * R + j]);
-                if (pub_lane) publish(xgH1 + pub_off + (size_t)(b * R + j) * a.gstride, tag, hn);
+                if (pub_lane) publish(xgH1 + pub_off + b * R + j, tag, hn);
                 if (it == it0) STAMP_WAVE(12);
             }
         if (compute) mark_pub(HOP_H1, t);
         // hop A: h1_t; the pollers also form x = x_I + h1 (:212) and stage a3 next to it
         if (poller) {
             wait_own(HOP_H1, t, nU);
-            gather(xgH1 + poll_off, Bc * R, R, tag, a.ctl, a.timeout_ticks, t, HOP_H1, abort_flag, a.gstride,
+            gather<NG_R>(xgH1 + poll_off, Bc * R, R, tag, a.ctl, a.timeout_ticks, t, HOP_H1, abort_flag,
                    [&](int b, int j, float v) {
                        h1[b * R + j] = v;
                        xa[b * RA + j] = fmaf(wi0[j], xprev[b], cur[b * PP + j]) + v;
@@ -550,7 +556,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
                 }
                 const float hn = gru_gate_math(gi[0], gi[1], gi[2], gh[0], gh[1], gh[2], h2[b * R + j]);
                 if (it == it0) STAMP_WAVE(11);
-                if (pub_lane) publish(xgH2 + pub_off + (size_t)(b * R + j) * a.gstride, tag, hn);
+                if (pub_lane) publish(xgH2 + pub_off + b * R + j, tag, hn);
                 if (it == it0) STAMP_WAVE(13);
             }
             mark_pub(HOP_H2, t);
@@ -573,7 +579,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
         }
         if (poller) wait_own(HOP_H2, t, nU);
         if (poller)
-            gather(xgH2 + poll_off, Bc * R, R, tag, a.ctl, a.timeout_ticks, t, HOP_H2, abort_flag, a.gstride,
+            gather<NG_R>(xgH2 + poll_off, Bc * R, R, tag, a.ctl, a.timeout_ticks, t, HOP_H2, abort_flag,
                    [&](int b, int j, float v) { h2[b * R + j] = v; }, dbg_on ? stamp + 14 : nullptr);
         bar();
         STAMP(2);
@@ -584,7 +590,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
             for (int it = it0; it < nF; it += kWaves) {
                 const int b = it / UFv, r = it - b * UFv, j = w * UF + r;
                 const float v = wave_dot(S + a.s.w1 + r * RA, h2 + b * R, R / 4, lane) + PC(b, r)[PC_V1];
-                if (pub_lane) publish(xgF1 + pub_off + (size_t)(b * F + j) * a.gstride, tag, v > 0.0f ? v : 0.0f);
+                if (pub_lane) publish(xgF1 + pub_off + b * F + j, tag, v > 0.0f ? v : 0.0f);
             }
             mark_pub(HOP_F1, t);
             for (int it = it0; it < nU; it += kWaves) {     // GH2_{t+1} = W_hh2·h2_t
@@ -606,7 +612,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
         }
         if (poller) wait_own(HOP_F1, t, nF);
         if (poller)
-            gather(xgF1 + poll_off, Bc * F, F, tag, a.ctl, a.timeout_ticks, t, HOP_F1, abort_flag, a.gstride,
+            gather<NG_F>(xgF1 + poll_off, Bc * F, F, tag, a.ctl, a.timeout_ticks, t, HOP_F1, abort_flag,
                    [&](int b, int j, float v) { f1[b * F + j] = v; });
         bar();
         STAMP(3);
@@ -617,7 +623,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
             for (int it = it0; it < nF; it += kWaves) {
                 const int b = it / UFv, r = it - b * UFv, j = w * UF + r;
                 const float v = wave_dot(S + a.s.w2 + r * (F + A), f1 + b * F, F / 4, lane) + PC(b, r)[PC_V2];
-                if (pub_lane) publish(xgF2 + pub_off + (size_t)(b * F + j) * a.gstride, tag, v > 0.0f ? v : 0.0f);
+                if (pub_lane) publish(xgF2 + pub_off + b * F + j, tag, v > 0.0f ? v : 0.0f);
             }
             mark_pub(HOP_F2, t);
             if (t + 1 < a.L)
@@ -628,7 +634,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
         }
         if (poller) wait_own(HOP_F2, t, nF);
         if (poller)
-            gather(xgF2 + poll_off, Bc * F, F, tag, a.ctl, a.timeout_ticks, t, HOP_F2, abort_flag, a.gstride,
+            gather<NG_F>(xgF2 + poll_off, Bc * F, F, tag, a.ctl, a.timeout_ticks, t, HOP_F2, abort_flag,
                    [&](int b, int j, float v) { f2[b * F + j] = v; });
         bar();
         STAMP(4);
@@ -650,12 +656,12 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
                 for (int it = it0; it < nC; it += kWaves) {
                     const int b = it / UCv, r = it - b * UCv, j = w * UC + r;
                     const float v = wave_dot(S + a.s.w3 + r * F, f2 + b * F, F / 4, lane) + S[a.s.b3 + r];
-                    if (pub_lane) publish(xgLG + pub_off + (size_t)(b * NC + j) * a.gstride, tag, v);
+                    if (pub_lane) publish(xgLG + pub_off + b * NC + j, tag, v);
                 }
             if (compute) mark_pub(HOP_LOGITS, t);
             if (poller) wait_own(HOP_LOGITS, t, nC);
             if (poller)
-                gather(xgLG + poll_off, Bc * NC, NC, tag, a.ctl, a.timeout_ticks, t, HOP_LOGITS, abort_flag, a.gstride,
+                gather<NG_C>(xgLG + poll_off, Bc * NC, NC, tag, a.ctl, a.timeout_ticks, t, HOP_LOGITS, abort_flag,
                        [&](int b, int j, float v) { lg[b * ll.ncp + j] = v; });
         }
         bar();
@@ -797,15 +803,25 @@ hipError_t launch_ci_gemm(const float *cond, int CD, int Bt, int b0, int Bc, int
 
 // Shipped instantiations: the 800k-step hparams (rnn 512, fc 512, aux 32) at one workgroup
 // per CU of a 256-CU MI355X (2 units/workgroup), and a fully runtime-dimensioned fallback.
-#define WRNN_K_MOL512 fatchord_loop_kernel<512, 512, 32, 30, true, 2, 2, 0>
-#define WRNN_K_RAW512 fatchord_loop_kernel<512, 512, 32, 512, false, 2, 2, 2>
-#define WRNN_K_MOLGEN fatchord_loop_kernel<0, 0, 0, 0, true, 0, 0, 0>
-#define WRNN_K_RAWGEN fatchord_loop_kernel<0, 0, 0, 0, false, 0, 0, 0>
+#define WRNN_K_MOL512 fatchord_loop_kernel<512, 512, 32, 30, true, 2, 2, 0, 1>
+#define WRNN_K_MOL512B2 fatchord_loop_kernel<512, 512, 32, 30, true, 2, 2, 0, 2>
+#define WRNN_K_RAW512 fatchord_loop_kernel<512, 512, 32, 512, false, 2, 2, 2, 1>
+#define WRNN_K_RAW512B2 fatchord_loop_kernel<512, 512, 32, 512, false, 2, 2, 2, 2>
+#define WRNN_K_MOLGEN fatchord_loop_kernel<0, 0, 0, 0, true, 0, 0, 0, 0>
+#define WRNN_K_RAWGEN fatchord_loop_kernel<0, 0, 0, 0, false, 0, 0, 0, 0>
 
 static const void *pick_loop_kernel(const LoopArgs &a) {
-    const bool d512 = a.R == 512 && a.F == 512 && a.A == 32 && a.U == 2 && a.UF == 2;
-    if (a.mol) return d512 && a.NC == 30 ? (const void *)WRNN_K_MOL512 : (const void *)WRNN_K_MOLGEN;
-    return d512 && a.NC == 512 && a.UC == 2 ? (const void *)WRNN_K_RAW512 : (const void *)WRNN_K_RAWGEN;
+    const bool d512 = a.R == 512 && a.F == 512 && a.A == 32 && a.U == 2 && a.UF == 2 && (a.Bc == 1 || a.Bc == 2);
+    if (a.mol) {
+        if (d512 && a.NC == 30) return a.Bc == 1 ? (const void *)WRNN_K_MOL512 : (const void *)WRNN_K_MOL512B2;
+        return (const void *)WRNN_K_MOLGEN;
+    }
+    if (d512 && a.NC == 512 && a.UC == 2) return a.Bc == 1 ? (const void *)WRNN_K_RAW512 : (const void *)WRNN_K_RAW512B2;
+    return (const void *)WRNN_K_RAWGEN;
+}
+
+bool loop_has_fast_path(int R, int F, int A, int NC, bool mol, int U, int UF, int UC) {
+    return R == 512 && F == 512 && A == 32 && U == 2 && UF == 2 && (mol ? NC == 30 : (NC == 512 && UC == 2));
 }
 
 hipError_t launch_loop(const LoopArgs &a, size_t lds_bytes, hipStream_t st) {
@@ -816,8 +832,8 @@ hipError_t launch_loop(const LoopArgs &a, size_t lds_bytes, hipStream_t st) {
 }
 
 hipError_t prepare_loop_kernel(int max_lds_bytes) {
-    for (const void *k : {(const void *)WRNN_K_MOL512, (const void *)WRNN_K_RAW512, (const void *)WRNN_K_MOLGEN,
-                          (const void *)WRNN_K_RAWGEN}) {
+    for (const void *k : {(const void *)WRNN_K_MOL512, (const void *)WRNN_K_MOL512B2, (const void *)WRNN_K_RAW512,
+                          (const void *)WRNN_K_RAW512B2, (const void *)WRNN_K_MOLGEN, (const void *)WRNN_K_RAWGEN}) {
         hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds_bytes);
         if (e != hipSuccess) return e;
     }
