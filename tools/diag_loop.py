@@ -50,6 +50,7 @@ if __name__ == "__main__":
     run(syn.TINY_RAW, 2, 300)
     run(syn.DEFAULT_MOL, 1, 5000)
     run(syn.DEFAULT_MOL, 1, 5000, philox=True)
+    run(syn.DEFAULT_RAW, 1, 5000)
     for g in (64, 128):
         try:
             run(syn.DEFAULT_MOL, 1, 3000, grid=g)

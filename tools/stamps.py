@@ -10,9 +10,11 @@ import torch
 from wavernn_amd import synthetic as syn
 from wavernn_amd.loop import FatchordLoop
 
-NAMES = ["start", "gru1 + hop A (h1)", "gru2 + hop B (h2)", "fc1 + hop C (f1)", "fc2 + hop D (f2)",
+NAMES = ["start", "gru1 (all units)", "gru2 + hop B (h2)", "fc1 + hop C (f1)", "fc2 + hop D (f2)",
          "fc3 (+hop E)", "sample + end"]
 NST = len(NAMES)
+# (publish stamp, stage-done stamp, label): per-workgroup time its first item was published
+HOPS = [(13, 2, "hop B (h2)"), (7, 3, "hop C (f1)"), (8, 4, "hop D (f2)")]
 
 
 def main(mode="MOL", B=1, L=2000, grid=0):
@@ -38,31 +40,17 @@ def main(mode="MOL", B=1, L=2000, grid=0):
     for k in range(1, NST):
         dk = (st[:, :, k] - st[:, :, k - 1]) * 10e-3
         print(f"  {NAMES[k]:22s} median {np.median(dk):7.3f} us  p10 {np.percentile(dk, 10):7.3f}  p90 {np.percentile(dk, 90):7.3f}")
-    # skew: when do workgroups publish h1 (stamp 12) relative to the earliest, per step
-    pub = st[:, :, 12]
-    valid = pub > 0
-    if valid.all():
-        rel = (pub - pub.min(0, keepdims=True)) * 10e-3
-        print(f"  h1 publish skew across WGs: median of per-step max {np.median(rel.max(0)):.3f} us")
-        done = st[:, :, 1]
-        lat = (done - pub.max(0, keepdims=True)) * 10e-3
-        print(f"  last publish -> gather done: median {np.median(lat):.3f} us (p90 {np.percentile(lat, 90):.3f})")
-        pub2 = st[:, :, 13]
-        lat2 = (st[:, :, 2] - pub2.max(0, keepdims=True)) * 10e-3
-        print(f"  h2 publish skew: {np.median(((pub2 - pub2.min(0, keepdims=True)) * 10e-3).max(0)):.3f} us; "
-              f"last publish -> gather done: {np.median(lat2):.3f} us")
-        g1 = (pub - st[:, :, 0]) * 10e-3
-        g2 = (pub2 - st[:, :, 1]) * 10e-3
-        print(f"  critical compute: gru1 (start->publish) {np.median(g1):.3f} us, gru2 (hop A done->publish) {np.median(g2):.3f} us")
-        s9 = (st[:, :, 9] - st[:, :, 1]) * 10e-3
-        s10 = (st[:, :, 10] - st[:, :, 9]) * 10e-3
-        s11 = (st[:, :, 11] - st[:, :, 10]) * 10e-3
-        s13 = (st[:, :, 13] - st[:, :, 11]) * 10e-3
-        print(f"  gru2 detail: bar->start {np.median(s9):.3f}  row_dot {np.median(s10):.3f}  gates {np.median(s11):.3f}  publish {np.median(s13):.3f} us")
-        print(f"  hop B polling: passes median {np.median(st[:, :, 14]):.1f} (p90 {np.percentile(st[:, :, 14], 90):.0f}), "
-              f"first pass {np.median(st[:, :, 15]) * 10e-3:.3f} us")
-        start_skew = (st[:, :, 0] - st[:, :, 0].min(0, keepdims=True)) * 10e-3
-        print(f"  step-start skew across WGs: median of max {np.median(start_skew.max(0)):.3f} us")
+    for pk, dk_, label in HOPS:
+        pub = st[:, :, pk]
+        if not (pub > 0).all():
+            continue
+        skew = ((pub - pub.min(0, keepdims=True)) * 10e-3).max(0)
+        lat = (st[:, :, dk_] - pub.max(0, keepdims=True)) * 10e-3
+        comp = (pub - st[:, :, dk_ - 1]) * 10e-3
+        print(f"  {label}: compute->publish {np.median(comp):.3f} us, publish skew {np.median(skew):.3f} us, "
+              f"last publish -> all gathered {np.median(lat):.3f} us (p90 {np.percentile(lat, 90):.3f})")
+    t12 = (st[:, :, 12] - st[:, :, 1]) * 10e-3
+    print(f"  gru1 terms of t+1 published {np.median(t12):.3f} us after gru1 done")
 
 
 if __name__ == "__main__":

@@ -287,7 +287,9 @@ int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise
     const int reps = std::max(1, std::min(64, rep_env ? std::atoi(rep_env) : 8));
     // replica stride ≥ 64 KiB: keeps replicas on different lines/channels and makes the
     // pollers' fixed-count over-reads (slots ≥ n) land in allocated memory
-    const long long rep_stride = (((long long)Bc_max * h->NMAX * 8 + 65535) / 65536) * 65536 / 8;
+    const long long vec_max = std::max<long long>({(long long)Bc_max * h->NMAX, (long long)Bc_max * R * kTermsPerUnit,
+                                                   3LL * R});
+    const long long rep_stride = (((vec_max + kOverRead) * 8 + 65535) / 65536) * 65536 / 8;
     const size_t need_xg = (size_t)kHops * reps * rep_stride;
     if (need_xg > h->xg_cap) {
         if (h->d_xg) HIP_TRY(h, hipFree(h->d_xg));

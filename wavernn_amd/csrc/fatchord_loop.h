@@ -17,9 +17,13 @@ constexpr int kLoaderWave = 4;
 constexpr int kPollThreads = 64;
 constexpr int kGatherMax = 8;          // granules per polling lane per hand-off (generic kernels)
 constexpr int kClsPerLaneMax = 8;      // RAW softmax classes per lane (n_classes <= 512)
-constexpr int kHops = 5;               // h1, h2, f1, f2, logits(RAW)
+constexpr int kTermsPerUnit = 4;       // GRU1 terms exchanged per unit: S_r, S_z, Gi_n, Gh_n
+constexpr int kHops = 7;
+constexpr int kOverRead = 4096;        // granules a gather may read past its vector (padding)
 
-enum Hop { HOP_H1 = 0, HOP_H2 = 1, HOP_F1 = 2, HOP_F2 = 3, HOP_LOGITS = 4 };
+// Hand-off vectors.  Q1 is exchanged once (prologue); S0/S1 carry the GRU1 terms of step t in
+// buffer t & 1 (double-buffered: a workgroup can run at most one step ahead of another).
+enum Hop { HOP_Q1 = 0, HOP_H2 = 1, HOP_F1 = 2, HOP_F2 = 3, HOP_LOGITS = 4, HOP_S0 = 5, HOP_S1 = 6 };
 
 // Per-workgroup slab offsets (floats) of the resident weights.
 struct SlabLayout {
@@ -53,7 +57,7 @@ constexpr int kStamps = 16;
 
 // Dynamic-LDS layout (floats) for Bc rows; shared by host sizing and the kernel.
 struct LdsLayout {
-    int slab, h1, h2, xa, f1, f2, lg, pre, pc, q, xprev, lbl, flag, stamp, total;
+    int slab, h1, h2, xa, f1, f2, lg, pre, pc, q, sg, q1a, xprev, lbl, flag, stamp, total;
     int ncp, pp, pcu;
 };
 
@@ -61,7 +65,7 @@ __host__ __device__ inline int round4(int x) { return (x + 3) & ~3; }
 
 // Per (row, unit) precomputed terms, kept in LDS between the stage that makes them (off the
 // critical path, while a hand-off is in flight) and the stage that consumes them.
-enum PcSlot { PC_P1 = 0, PC_GH1 = 3, PC_P2 = 6, PC_GH2 = 9, PC_V1 = 12, PC_V2 = 13, PC_N = 16 };
+enum PcSlot { PC_P2 = 0, PC_GH2 = 3, PC_V1 = 6, PC_V2 = 7, PC_N = 8 };
 
 __host__ __device__ inline LdsLayout lds_layout(int slab_total, int Bc, int R, int F, int A, int NC, int NK,
                                                int U, int UF) {
@@ -79,11 +83,13 @@ __host__ __device__ inline LdsLayout lds_layout(int slab_total, int Bc, int R, i
     l.lg = o;    o += Bc * l.ncp;
     l.pre = o;   o += 3 * Bc * l.pp;           // ring of 3 step records
     l.pc = o;    o += Bc * l.pcu * PC_N;
-    l.q = o;     o += round4(6 * U);           // Q1, Q2: W_ih·W_I[:,0] per gate row
+    l.q = o;     o += round4(6 * U);           // Q1, Q2: W_ih·W_I[:,0] per gate row (own units)
+    l.sg = o;    o += Bc * R * kTermsPerUnit;  // GRU1 terms of ALL units for the coming step
+    l.q1a = o;   o += round4(3 * R);           // Q1 of all units, gate-major
     l.xprev = o; o += round4(Bc);
     l.lbl = o;   o += round4(Bc);
     l.flag = o;  o += 4 + kHops * kWaves + 4;  // abort word + per-hop, per-wave publish flags
-    l.stamp = o; o += kStamps;
+    l.stamp = o; o += 2 * kStamps;
     l.total = o;
     return l;
 }

@@ -153,33 +153,33 @@ __device__ __noinline__ void record_abort(int *ctl, int code, int step, int hop,
     __hip_atomic_store(&ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Gather n = Bc·N granules of one hop; store(b, j, v) puts each value where it belongs.
-// Called by the kPollThreads polling lanes only.  A pass issues NG UNCONDITIONAL loads
-// (out-of-range slots re-read a valid granule) and only then inspects them: guarding each
-// load with a runtime condition makes hipcc branch around it and wait vmcnt(0) per load,
-// i.e. NG serialized memory round trips per pass (measured: 2-4x slower hops).
+// Gather granules [base, base + NG·NL) ∩ [0, n) of one hand-off vector (n = rows·N values);
+// store(b, j, v) puts each value where it belongs.  Called by NL lanes (lane id `lid`).  A
+// pass issues NG UNCONDITIONAL loads (slots >= n re-read padding: the granule buffer has
+// kOverRead spare granules after every vector) and only then inspects them: guarding each load
+// with a runtime condition makes hipcc branch around it and wait vmcnt(0) per load, i.e. NG
+// serialized memory round trips per pass (measured: 2-4x slower hops).
 // On timeout, or when another workgroup has aborted, sets *lds_abort.
-template <int NG, typename Store>
-__device__ __forceinline__ void gather(const unsigned long long *g, int n, int N, uint32_t tag, int *ctl,
-                                       long long timeout, int step, int hop, int *lds_abort, Store store,
+template <int NG, int NL, typename Store>
+__device__ __forceinline__ void gather(const unsigned long long *g, int base, int n, int N, uint32_t tag, int *ctl,
+                                       long long timeout, int step, int hop, int *lds_abort, int lid, Store store,
                                        unsigned *dbg_slot = nullptr) {
-    // the granule buffer is padded (replica stride >= 64 KiB) so slots >= n are readable
-    const int tid = threadIdx.x;
-    const unsigned long long *gp = g + tid;
+    const unsigned long long *gp = g + base + lid;
+    const int i0 = base + lid;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     unsigned spins = 0;
     for (;;) {
         unsigned long long v[NG];
 #pragma unroll
-        for (int k = 0; k < NG; ++k) v[k] = __hip_atomic_load(gp + k * kPollThreads, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int k = 0; k < NG; ++k) v[k] = __hip_atomic_load(gp + k * NL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         bool ok = true;
 #pragma unroll
-        for (int k = 0; k < NG; ++k) ok &= (tid + k * kPollThreads >= n) | ((uint32_t)(v[k] >> 32) == tag);
-        if (dbg_slot && spins == 0 && tid == 0) dbg_slot[1] = (unsigned)(__builtin_amdgcn_s_memrealtime() - t0);
+        for (int k = 0; k < NG; ++k) ok &= (i0 + k * NL >= n) | ((uint32_t)(v[k] >> 32) == tag);
+        if (dbg_slot && spins == 0 && lid == 0) dbg_slot[1] = (unsigned)(__builtin_amdgcn_s_memrealtime() - t0);
         if (ok) {
 #pragma unroll
             for (int k = 0; k < NG; ++k) {
-                const int i = tid + k * kPollThreads;
+                const int i = i0 + k * NL;
                 if (i < n) {
                     const int b = i / N;
                     store(b, i - b * N, __uint_as_float((uint32_t)v[k]));
@@ -197,7 +197,18 @@ __device__ __forceinline__ void gather(const unsigned long long *g, int n, int N
             }
         }
     }
-    if (dbg_slot && tid == 0) dbg_slot[0] = spins + 1;
+    if (dbg_slot && lid == 0) dbg_slot[0] = spins + 1;
+}
+
+// A long, off-critical-path vector gathered in chunks of NG·NL granules (bounded registers).
+template <int NG, int NL, typename Store>
+__device__ __forceinline__ void gather_chunked(const unsigned long long *g, int n, int N, uint32_t tag, int *ctl,
+                                               long long timeout, int step, int hop, int *lds_abort, int lid,
+                                               Store store) {
+    for (int c0 = 0; c0 < n; c0 += NG * NL) {
+        gather<NG, NL>(g, c0, n, N, tag, ctl, timeout, step, hop, lds_abort, lid, store);
+        if (*reinterpret_cast<volatile int *>(lds_abort)) return;
+    }
 }
 
 // Stage work item `it` → wave: items go to the non-polling waves 1,2,3 first, the poller last.
@@ -273,15 +284,16 @@ __device__ __forceinline__ void bar() {
     asm volatile("" ::: "memory");
 }
 
-// Diagnostic stamp (only when a.dbg != 0): thread 0 records s_memrealtime into LDS slot k;
-// the loader wave flushes the slots of step t-1 to a.dbg at the top of step t.
+// Diagnostic stamp (only when a.dbg != 0): thread 0 records s_memrealtime into LDS slot k of
+// step t's half (double-buffered by step parity); the loader wave flushes step t-1's half to
+// a.dbg during step t.
 #define STAMP(k)                                                                               \
     do {                                                                                       \
-        if (dbg_on && tid == 0) stamp[k] = (unsigned)__builtin_amdgcn_s_memrealtime();         \
+        if (dbg_on && tid == 0) stamp[(t & 1) * kStamps + (k)] = (unsigned)__builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #define STAMP_WAVE(k)                                                                          \
     do {                                                                                       \
-        if (dbg_on && lane == 0) stamp[k] = (unsigned)__builtin_amdgcn_s_memrealtime();        \
+        if (dbg_on && lane == 0) stamp[(t & 1) * kStamps + (k)] = (unsigned)__builtin_amdgcn_s_memrealtime(); \
     } while (0)
 
 #define WRNN_GPTR(p) ((__attribute__((address_space(1))) void *)(p))
@@ -289,13 +301,20 @@ __device__ __forceinline__ void bar() {
 
 // ------------------------------------------------------------------------ the loop kernel
 //
-// Per step t the critical path is   x_{t-1} → GRU1 gates → [hop A: h1] → W_ih2[:, :R]·h1 →
-// GRU2 gates → [hop B: h2] → W1[:, :R]·h2 → [hop C: f1] → W2[:, :F]·f1 → [hop D: f2] →
-// fc3 + sample → x_t.  Everything else is linear in values known one stage earlier and is
-// computed while a hand-off is in flight (fp32 re-association of the reference sums; parity
-// is checked against the oracle/reference within the stated tolerance):
-//   P1 = W_ih1·cI_t, Q1 = W_ih1·W_I[:,0]      → gi1 = P1 + x_{t-1}·Q1 + b_ih1
-//   GH1 = W_hh1·h1_{t-1}                       → gh1 = GH1 + b_hh1
+// Per step t the critical path is
+//     x_{t-1} → GRU1 (ALL units, in every workgroup) → W_ih2[:, :R]·h1 → GRU2 gates →
+//     [hop B: h2] → W1[:, :R]·h2 → [hop C: f1] → W2[:, :F]·f1 → [hop D: f2] → fc3 + sample → x_t
+// GRU1 has no matvec on the critical path: with P1 = W_ih1·cI_t and GH1 = W_hh1·h1_{t-1}
+// known a step early, unit j needs only
+//     S_r = (GH1_r + b_hh,r) + (P1_r + b_ih,r),  S_z (likewise),  Gi_n = P1_n + b_ih,n,  Gh_n = GH1_n + b_hh,n
+//     r = σ(S_r + x·Q1_r), z = σ(S_z + x·Q1_z), n = tanh(Gi_n + x·Q1_n + Gh_n·r)   (Q1 = W_ih1·W_I[:,0])
+// so each workgroup publishes these four terms for its own units right after GRU1 of the
+// previous step, every workgroup gathers all of them while hops B-D are in flight, and GRU1
+// for all R units is then local gate math once x_{t-1} is sampled (redundantly, bit-identical
+// everywhere).  That removes the h1 all-to-all hop from the step: 3 critical hand-offs (MoL),
+// 4 with the RAW logits.  Everything else is linear in values known one stage earlier and is
+// computed while a hand-off is in flight (fp32 re-association of the reference sums; parity is
+// checked against the oracle/reference within the stated tolerance):
 //   P2 = W_ih2·[cI_t; a2_t], Q2 = W_ih2[:, :R]·W_I[:,0]
 //                                              → gi2 = W_ih2[:, :R]·h1_t + P2 + x_{t-1}·Q2 + b_ih2
 //   GH2 = W_hh2·h2_{t-1}                       → gh2 = GH2 + b_hh2
@@ -316,16 +335,17 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
     constexpr int NG_R = (kB && kR) ? (kB * kR + kPollThreads - 1) / kPollThreads : kGatherMax;
     constexpr int NG_F = (kB && kF) ? (kB * kF + kPollThreads - 1) / kPollThreads : kGatherMax;
     constexpr int NG_C = (kB && kNC) ? (kB * kNC + kPollThreads - 1) / kPollThreads : kGatherMax;
+    constexpr int kTermLanes = kCompute - kPollThreads;   // waves 1..3 gather the GRU1 terms
     const LdsLayout ll = lds_layout(a.s.total, Bc, R, F, A, NC, NK, U, UF);
     const float *S = smem + ll.slab;
     float *h1 = smem + ll.h1, *h2 = smem + ll.h2, *xa = smem + ll.xa, *f1 = smem + ll.f1;
     float *f2 = smem + ll.f2, *lg = smem + ll.lg, *pre = smem + ll.pre, *pc = smem + ll.pc;
-    float *q = smem + ll.q, *xprev = smem + ll.xprev;
+    float *q = smem + ll.q, *sg = smem + ll.sg, *q1a = smem + ll.q1a, *xprev = smem + ll.xprev;
     int *lbl = reinterpret_cast<int *>(smem + ll.lbl);
     int *abort_flag = reinterpret_cast<int *>(smem + ll.flag);
     int *pubflag = abort_flag + 4;                // [kHops][kWaves]: step+1 once a wave has published
     unsigned *stamp = reinterpret_cast<unsigned *>(smem + ll.stamp);
-    const int RA = R + A, PP = ll.pp, P = R + 3 * A + NK;
+    const int RA = R + A, PP = ll.pp, P = R + 3 * A + NK, RT = R * kTermsPerUnit;
     const int Uv = min(U, R - w * U);                 // valid units here
     const int UFv = max(0, min(UF, F - w * UF));
     const int UCv = MOL ? 0 : max(0, min(UC, NC - w * UC));
@@ -369,9 +389,25 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
             *pz = k < 10 ? logf(-logf(uu)) : (logf(uu) - logf(1.0f - uu));
         }
 
+    // every hop vector exists in a.reps replicas (spread over memory channels); a value is
+    // published to all of them by lanes 0..reps-1 at once, workgroup w polls replica w % reps
+    const size_t hop_stride = (size_t)a.reps * a.rep_stride;
+    const size_t pub_off = (size_t)(lane < a.reps ? lane : 0) * a.rep_stride;
+    const size_t poll_off = (size_t)(w % a.reps) * a.rep_stride;
+    unsigned long long *xgQ1 = a.xg + HOP_Q1 * hop_stride, *xgH2 = a.xg + HOP_H2 * hop_stride;
+    unsigned long long *xgF1 = a.xg + HOP_F1 * hop_stride, *xgF2 = a.xg + HOP_F2 * hop_stride;
+    unsigned long long *xgLG = a.xg + HOP_LOGITS * hop_stride;
+    auto xgS = [&](int t) { return a.xg + (HOP_S0 + (t & 1)) * hop_stride; };
+    const bool pub_lane = lane < a.reps;
+    // four GRU1 terms per unit: lanes [k·reps, k·reps + reps) publish term k to every replica
+    const int term_k = lane / a.reps;
+    const bool term_lane = lane < kTermsPerUnit * a.reps;
+    const size_t term_off = (size_t)(term_lane ? lane - term_k * a.reps : 0) * a.rep_stride;
+
     const float *wi0 = S + a.s.wi0;
-    // P1/P2 of step t for GRU item (b,u): six dots in two rounds of four 16-lane rows
-    auto precompute_P = [&](int t, int b, int u) {
+    // P1 (returned, wave-uniform) and P2 (→ PC) of step t for GRU item (b,u): six dots in two
+    // rounds of four 16-lane rows
+    auto precompute_P = [&](int t, int b, int u, float (&p1)[3]) {
         const float *r_ = rec(t) + b * PP;           // [cI_t (R) | a2_t (A) | …]
         float v1, v2;
         {   // rows 0..2: P1[g] = W_ih1[g]·cI ; row 3: P2[0] = W_ih2[0]·[cI; a2]
@@ -382,20 +418,29 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
             const int g = 1 + (row & 1);
             v2 = row_dot(S + a.s.wih2 + (g * U + u) * RA, r_, RA / 4, li);
         }
-        const float p10 = lane_bcast(v1, 0), p11 = lane_bcast(v1, 16), p12 = lane_bcast(v1, 32);
+        p1[0] = lane_bcast(v1, 0);
+        p1[1] = lane_bcast(v1, 16);
+        p1[2] = lane_bcast(v1, 32);
         const float p20 = lane_bcast(v1, 48), p21 = lane_bcast(v2, 0), p22 = lane_bcast(v2, 16);
         if (lane == 0) {
             float *p = PC(b, u);
-            p[PC_P1 + 0] = p10;
-            p[PC_P1 + 1] = p11;
-            p[PC_P1 + 2] = p12;
             p[PC_P2 + 0] = p20;
             p[PC_P2 + 1] = p21;
             p[PC_P2 + 2] = p22;
         }
     };
+    // publish GRU1 terms of (b, u) for step t from P1 and GH1 = W_hh1·h1_{t-1} (wave-uniform)
+    auto publish_terms = [&](int t, int b, int u, const float (&p1)[3], float g0, float g1, float g2) {
+        const int j = w * U + u;
+        const float s_r = (g0 + S[a.s.bhh1 + 0 * U + u]) + (p1[0] + S[a.s.bih1 + 0 * U + u]);
+        const float s_z = (g1 + S[a.s.bhh1 + 1 * U + u]) + (p1[1] + S[a.s.bih1 + 1 * U + u]);
+        const float gi_n = p1[2] + S[a.s.bih1 + 2 * U + u];
+        const float gh_n = g2 + S[a.s.bhh1 + 2 * U + u];
+        const float v = term_k == 0 ? s_r : term_k == 1 ? s_z : term_k == 2 ? gi_n : gh_n;
+        if (term_lane) publish(xgS(t) + term_off + (size_t)(b * R + j) * kTermsPerUnit + term_k, (uint32_t)t + 1u, v);
+    };
 
-    // constants Q1/Q2 per unit and step-0 P terms (GH = W_hh·0 = 0)
+    // constants Q1/Q2 per unit (Q1 also published for the all-unit GRU1), step-0 terms (GH = 0)
     if (compute) {
         for (int u = wave; u < Uv; u += kWaves) {
             float v1, v2;
@@ -414,27 +459,27 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
                 q[4 * U + u] = q4;
                 q[5 * U + u] = q5;
             }
+            if (term_lane && term_k < 3)
+                publish(xgQ1 + term_off + (size_t)term_k * R + w * U + u, 1u, term_k == 0 ? q0 : term_k == 1 ? q1 : q2);
         }
         for (int it = it0; it < nU; it += kWaves) {
             const int b = it / Uv, u = it - b * Uv;
-            precompute_P(0, b, u);
+            float p1[3];
+            precompute_P(0, b, u, p1);
+            publish_terms(0, b, u, p1, 0.0f, 0.0f, 0.0f);
             if (lane == 0) {
                 float *p = PC(b, u);
-                for (int g = 0; g < 3; ++g) { p[PC_GH1 + g] = 0.0f; p[PC_GH2 + g] = 0.0f; }
+                for (int g = 0; g < 3; ++g) p[PC_GH2 + g] = 0.0f;
             }
         }
+        gather_chunked<kGatherMax, kCompute>(xgQ1 + poll_off, 3 * R, 3 * R, 1u, a.ctl, a.timeout_ticks, -1, HOP_Q1,
+                                             abort_flag, tid, [&](int, int j, float v) { q1a[j] = v; });
+        gather_chunked<kGatherMax, kCompute>(xgS(0) + poll_off, Bc * RT, RT, 1u, a.ctl, a.timeout_ticks, 0, HOP_S0,
+                                             abort_flag, tid, [&](int b, int j, float v) { sg[b * RT + j] = v; });
     }
     __syncthreads();
+    if (*abort_flag) return;
 
-    // every hop vector exists in a.reps replicas (spread over memory channels); a value is
-    // published to all of them by lanes 0..reps-1 at once, workgroup w polls replica w % reps
-    const size_t hop_stride = (size_t)a.reps * a.rep_stride;
-    const size_t pub_off = (size_t)(lane < a.reps ? lane : 0) * a.rep_stride;
-    const size_t poll_off = (size_t)(w % a.reps) * a.rep_stride;
-    unsigned long long *xgH1 = a.xg + HOP_H1 * hop_stride, *xgH2 = a.xg + HOP_H2 * hop_stride;
-    unsigned long long *xgF1 = a.xg + HOP_F1 * hop_stride, *xgF2 = a.xg + HOP_F2 * hop_stride;
-    unsigned long long *xgLG = a.xg + HOP_LOGITS * hop_stride;
-    const bool pub_lane = lane < a.reps;
     // Delayed polling (a.delay_poll): the polling threads start their global polls only once
     // this workgroup's own values of the hop are out — fewer useless passes, less traffic.
     // A wave marks a hop published after its LAST item of that hop (plain LDS store).
@@ -454,9 +499,32 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
         const float *cur = rec(t);
         STAMP(0);
 
+        // ---- GRU1 (fatchord_version.py:208-210) for ALL units: gate math on the gathered
+        // terms; also x = x_I + h1 (:212) with a3 staged next to it for V1
+        if (compute) {
+            for (int i = tid; i < Bc * R; i += kCompute) {
+                const int b = i / R, j = i - b * R;
+                const float x = xprev[b];
+                const float4 st = reinterpret_cast<const float4 *>(sg)[i];
+                const float r = sigmoid_(fmaf(x, q1a[j], st.x));
+                const float z = sigmoid_(fmaf(x, q1a[R + j], st.y));
+                const float n = tanh_(fmaf(x, q1a[2 * R + j], st.z) + st.w * r);
+                const float hn = (h1[i] - n) * z + n;
+                h1[i] = hn;
+                xa[b * RA + j] = fmaf(wi0[j], x, cur[b * PP + j]) + hn;
+            }
+            for (int i = tid; i < Bc * A; i += kCompute) {
+                const int b = i / A, k = i - b * A;
+                xa[b * RA + R + k] = cur[b * PP + R + A + k];
+            }
+        }
+        bar();
+        STAMP(1);
+
+        // loader: step-top work runs behind GRU1's barrier, overlapping GRU2 + hop B
         if (loader) {
-            if (dbg_on && t > 0 && t - 1 < a.dbg_steps && lane < kStamps)
-                a.dbg[((size_t)w * a.dbg_steps + (t - 1)) * kStamps + lane] = stamp[lane];
+            if (dbg_on && t > 0 && t - 1 < a.dbg_steps && lane < kStamps)   // slots of step t-1
+                a.dbg[((size_t)w * a.dbg_steps + (t - 1)) * kStamps + lane] = stamp[((t - 1) & 1) * kStamps + lane];
             // outputs of step t-1 (LDS reads happen before any DMA is in flight)
             if (writer && t > 0) {
                 const size_t o = (size_t)(a.b0 + lane) * a.L + (t - 1);
@@ -505,41 +573,9 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
             }
         }
 
-        // ---- GRU1 (fatchord_version.py:208-210): gates only, every matvec precomputed
-        if (compute)
-            for (int it = it0; it < nU; it += kWaves) {
-                const int b = it / Uv, u = it - b * Uv, j = w * U + u;
-                const float x = xprev[b];
-                const float *p = PC(b, u);
-                float gi[3], gh[3];
-#pragma unroll
-                for (int g = 0; g < 3; ++g) {
-                    gi[g] = fmaf(x, q[g * U + u], p[PC_P1 + g]) + S[a.s.bih1 + g * U + u];
-                    gh[g] = p[PC_GH1 + g] + S[a.s.bhh1 + g * U + u];
-                }
-                const float hn = gru_gate_math(gi[0], gi[1], gi[2], gh[0], gh[1], gh[2], h1[b * R + j]);
-                if (pub_lane) publish(xgH1 + pub_off + b * R + j, tag, hn);
-                if (it == it0) STAMP_WAVE(12);
-            }
-        if (compute) mark_pub(HOP_H1, t);
-        // hop A: h1_t; the pollers also form x = x_I + h1 (:212) and stage a3 next to it
-        if (poller) {
-            wait_own(HOP_H1, t, nU);
-            gather<NG_R>(xgH1 + poll_off, Bc * R, R, tag, a.ctl, a.timeout_ticks, t, HOP_H1, abort_flag,
-                   [&](int b, int j, float v) {
-                       h1[b * R + j] = v;
-                       xa[b * RA + j] = fmaf(wi0[j], xprev[b], cur[b * PP + j]) + v;
-                   });
-            for (int i = tid; i < Bc * A; i += kPollThreads) {
-                const int b = i / A, k = i - b * A;
-                xa[b * RA + R + k] = cur[b * PP + R + A + k];
-            }
-        }
-        bar();
-        STAMP(1);
-        if (*abort_flag) return;
 
-        // ---- GRU2 (:213-214): W_ih2[:, :R]·h1 on the critical path, then GH1_{t+1} and V1
+        // ---- GRU2 (:213-214): W_ih2[:, :R]·h1 on the critical path; then the GRU1 terms of
+        // step t+1 (P1, GH1 = W_hh1·h1_t → publish), P2 of t+1, and V1
         if (compute) {
             for (int it = it0; it < nU; it += kWaves) {
                 const int b = it / Uv, u = it - b * Uv, j = w * U + u;
@@ -560,17 +596,15 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
                 if (it == it0) STAMP_WAVE(13);
             }
             mark_pub(HOP_H2, t);
-            for (int it = it0; it < nU; it += kWaves) {     // GH1_{t+1} = W_hh1·h1_t
-                const int b = it / Uv, u = it - b * Uv;
-                const float v = row_dot(S + a.s.whh1 + ((row < 3 ? row : 0) * U + u) * R, h1 + b * R, R / 4, li);
-                const float g0 = lane_bcast(v, 0), g1 = lane_bcast(v, 16), g2 = lane_bcast(v, 32);
-                if (lane == 0) {
-                    float *p = PC(b, u);
-                    p[PC_GH1 + 0] = g0;
-                    p[PC_GH1 + 1] = g1;
-                    p[PC_GH1 + 2] = g2;
+            if (t + 1 < a.L)
+                for (int it = it0; it < nU; it += kWaves) {
+                    const int b = it / Uv, u = it - b * Uv;
+                    float p1[3];
+                    precompute_P(t + 1, b, u, p1);
+                    const float v = row_dot(S + a.s.whh1 + ((row < 3 ? row : 0) * U + u) * R, h1 + b * R, R / 4, li);
+                    publish_terms(t + 1, b, u, p1, lane_bcast(v, 0), lane_bcast(v, 16), lane_bcast(v, 32));
+                    if (it == it0) STAMP_WAVE(12);
                 }
-            }
             for (int it = it0; it < nF; it += kWaves) {     // V1 = W1·[x + h1; a3] + b1
                 const int b = it / UFv, r = it - b * UFv;
                 const float v = wave_dot(S + a.s.w1 + r * RA, xa + b * RA, RA / 4, lane);
@@ -579,8 +613,9 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
         }
         if (poller) wait_own(HOP_H2, t, nU);
         if (poller)
-            gather<NG_R>(xgH2 + poll_off, Bc * R, R, tag, a.ctl, a.timeout_ticks, t, HOP_H2, abort_flag,
-                   [&](int b, int j, float v) { h2[b * R + j] = v; }, dbg_on ? stamp + 14 : nullptr);
+            gather<NG_R, kPollThreads>(xgH2 + poll_off, 0, Bc * R, R, tag, a.ctl, a.timeout_ticks, t, HOP_H2,
+                                       abort_flag, tid, [&](int b, int j, float v) { h2[b * R + j] = v; },
+                                       dbg_on ? stamp + (t & 1) * kStamps + 14 : nullptr);
         bar();
         STAMP(2);
         if (*abort_flag) return;
@@ -591,6 +626,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
                 const int b = it / UFv, r = it - b * UFv, j = w * UF + r;
                 const float v = wave_dot(S + a.s.w1 + r * RA, h2 + b * R, R / 4, lane) + PC(b, r)[PC_V1];
                 if (pub_lane) publish(xgF1 + pub_off + b * F + j, tag, v > 0.0f ? v : 0.0f);
+                if (it == it0) STAMP_WAVE(7);
             }
             mark_pub(HOP_F1, t);
             for (int it = it0; it < nU; it += kWaves) {     // GH2_{t+1} = W_hh2·h2_t
@@ -612,30 +648,31 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
         }
         if (poller) wait_own(HOP_F1, t, nF);
         if (poller)
-            gather<NG_F>(xgF1 + poll_off, Bc * F, F, tag, a.ctl, a.timeout_ticks, t, HOP_F1, abort_flag,
-                   [&](int b, int j, float v) { f1[b * F + j] = v; });
+            gather<NG_F, kPollThreads>(xgF1 + poll_off, 0, Bc * F, F, tag, a.ctl, a.timeout_ticks, t, HOP_F1,
+                                       abort_flag, tid, [&](int b, int j, float v) { f1[b * F + j] = v; });
         bar();
         STAMP(3);
         if (*abort_flag) return;
 
-        // ---- fc2 (:220-221): W2[:, :F]·f1 + V2, then P1/P2 of step t+1
+        // ---- fc2 (:220-221): W2[:, :F]·f1 + V2; then waves 1-3 gather step t+1's GRU1 terms
         if (compute) {
             for (int it = it0; it < nF; it += kWaves) {
                 const int b = it / UFv, r = it - b * UFv, j = w * UF + r;
                 const float v = wave_dot(S + a.s.w2 + r * (F + A), f1 + b * F, F / 4, lane) + PC(b, r)[PC_V2];
                 if (pub_lane) publish(xgF2 + pub_off + b * F + j, tag, v > 0.0f ? v : 0.0f);
+                if (it == it0) STAMP_WAVE(8);
             }
             mark_pub(HOP_F2, t);
-            if (t + 1 < a.L)
-                for (int it = it0; it < nU; it += kWaves) {
-                    const int b = it / Uv, u = it - b * Uv;
-                    precompute_P(t + 1, b, u);
-                }
+            if (!poller && t + 1 < a.L)
+                gather_chunked<kGatherMax, kTermLanes>(xgS(t + 1) + poll_off, Bc * RT, RT, tag + 1u, a.ctl,
+                                                       a.timeout_ticks, t + 1, HOP_S0 + ((t + 1) & 1), abort_flag,
+                                                       tid - kPollThreads,
+                                                       [&](int b, int j, float v) { sg[b * RT + j] = v; });
         }
         if (poller) wait_own(HOP_F2, t, nF);
         if (poller)
-            gather<NG_F>(xgF2 + poll_off, Bc * F, F, tag, a.ctl, a.timeout_ticks, t, HOP_F2, abort_flag,
-                   [&](int b, int j, float v) { f2[b * F + j] = v; });
+            gather<NG_F, kPollThreads>(xgF2 + poll_off, 0, Bc * F, F, tag, a.ctl, a.timeout_ticks, t, HOP_F2,
+                                       abort_flag, tid, [&](int b, int j, float v) { f2[b * F + j] = v; });
         bar();
         STAMP(4);
         if (*abort_flag) return;
@@ -661,8 +698,9 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
             if (compute) mark_pub(HOP_LOGITS, t);
             if (poller) wait_own(HOP_LOGITS, t, nC);
             if (poller)
-                gather<NG_C>(xgLG + poll_off, Bc * NC, NC, tag, a.ctl, a.timeout_ticks, t, HOP_LOGITS, abort_flag,
-                       [&](int b, int j, float v) { lg[b * ll.ncp + j] = v; });
+                gather<NG_C, kPollThreads>(xgLG + poll_off, 0, Bc * NC, NC, tag, a.ctl, a.timeout_ticks, t,
+                                           HOP_LOGITS, abort_flag, tid,
+                                           [&](int b, int j, float v) { lg[b * ll.ncp + j] = v; });
         }
         bar();
         STAMP(5);
@@ -693,7 +731,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
                     x = x > 1.0f ? 1.0f : x;
                 } else {
                     // softmax → Categorical renormalise → argmax(p / q)
-                                        float e[kClsPerLaneMax];
+                    float e[kClsPerLaneMax];
                     float m = -INFINITY;
 #pragma unroll
                     for (int k = 0; k < kClsPerLaneMax; ++k) {
