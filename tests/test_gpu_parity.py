@@ -66,13 +66,15 @@ def test_loop_vs_oracle_fresh_seeds(mode, B):
         assert np.abs(out.cpu().numpy() - ref).max() <= gf.MOL_TOL
 
 
-@pytest.mark.parametrize("grid", [128, 200])
-def test_grid_sizes_agree(grid):
-    """Other partitions (4 units per workgroup; 3 units with a ragged last workgroup) give the
-    same labels: the partition only changes fp32 reduction order, RAW labels must not move."""
-    fx = gf.load("loop_raw_b1")
+@pytest.mark.parametrize("name,grid", [("loop_raw_b1", 200), ("loop_raw_tiny_b2", 16), ("loop_raw_tiny_b2", 24)])
+def test_grid_sizes_agree(name, grid):
+    """Other partitions (3 units per workgroup with a ragged last workgroup at rnn 512; 4 and 3
+    units at the tiny dims) give the same labels: the partition only changes fp32 reduction
+    order, RAW labels must not move."""
+    fx = gf.load(name)
     d, state, mels, aux, noise = gf.loop_inputs(fx)
     loop = _loop(d, grid=grid)
+    assert loop.info["grid"] < 256
     loop.set_weights(state)
     _, lab = loop.generate(_cond(mels, aux), noise=torch.from_numpy(noise).to(DEV), want_labels=True)
     _report_raw(lab.cpu().numpy(), fx["labels"].astype(np.int32))
