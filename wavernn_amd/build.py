@@ -9,8 +9,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "_lib", "libwavernn_amd.so")
-SOURCES = [os.path.join(CSRC, f) for f in ("fatchord_loop.hip", "capi.cpp")]
-HEADERS = [os.path.join(CSRC, "fatchord_loop.h"), os.path.join(REPO, "include", "wavernn_amd.h")]
+SOURCES = [os.path.join(CSRC, f) for f in ("fatchord_loop.hip", "fatchord_rows.hip", "capi.cpp")]
+HEADERS = [os.path.join(CSRC, f) for f in ("fatchord_loop.h", "fatchord_rows.h", "wrnn_device.h")] + \
+    [os.path.join(REPO, "include", "wavernn_amd.h")]
 ARCH = os.environ.get("WRNN_OFFLOAD_ARCH", "gfx950")
 
 
@@ -33,7 +34,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-I" + os.path.join(REPO, "include"), *SOURCES, "-o", OUT + ".tmp"]
+           "-I" + os.path.join(REPO, "include"), *SOURCES, "-lrocblas", "-o", OUT + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

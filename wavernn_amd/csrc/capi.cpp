@@ -4,6 +4,7 @@
 // reference state_dict tensors), the I-layer weights for the conditioning GEMM, the
 // conditioning-projection workspace, the hand-off granules and the control words.
 #include <hip/hip_runtime.h>
+#include <rocblas/rocblas.h>
 
 #include <algorithm>
 #include <cstdlib>
@@ -15,10 +16,16 @@
 
 #include "../../include/wavernn_amd.h"
 #include "fatchord_loop.h"
+#include "fatchord_rows.h"
 
 namespace wrnn {
-hipError_t launch_ci_gemm(const float *cond, int CD, int Bt, int b0, int Bc, int L, const float *W, int ldw,
-                          const float *bias, int N, int K, float *cI, hipStream_t st);
+hipError_t launch_ci_gemm(const float *cond, int CD, int Bt, int b0, int Bc, int t0, int L, const float *W, int ldw,
+                          const float *bias, int N, int K, float *cI, int ldc, hipStream_t st);
+hipError_t launch_pack_terms_input(const float *cond, int CD, int Bt, int b0, int B, int t0, int Lc, int feat, int A,
+                                   int R, int KX, float *X, hipStream_t st);
+hipError_t launch_rows(const RowsArgs &a, size_t lds_bytes, hipStream_t st);
+hipError_t prepare_rows_kernel(int max_lds_bytes);
+hipError_t rows_occupancy(int *blocks_per_cu, size_t lds_bytes);
 hipError_t launch_loop(const LoopArgs &a, size_t lds_bytes, hipStream_t st);
 hipError_t prepare_loop_kernel(int max_lds_bytes);
 hipError_t loop_occupancy(int *blocks_per_cu, size_t lds_bytes);
@@ -47,6 +54,17 @@ struct wrnn_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     std::string err;
+    // multi-row (fold-batched) path: fatchord_rows.hip
+    RowsSlab rs{};
+    int NT = 0, KX = 0, KA = 0;
+    bool rows_ok = false;                           // weights fit LDS with at least one row
+    float *d_rslab = nullptr, *d_Wt = nullptr;      // per-workgroup slabs, terms-GEMM weights [G·NT][KX]
+    float *d_X = nullptr, *d_T = nullptr, *d_act = nullptr, *d_state = nullptr;
+    size_t X_cap = 0, T_cap = 0, act_cap = 0, state_cap = 0;   // floats
+    unsigned *d_flags = nullptr;
+    unsigned long long *d_xr = nullptr;             // x granules
+    rocblas_handle blas = nullptr;
+    int last_path = 0;                              // 1 = latency kernel, 2 = rows kernel
 };
 
 namespace {
@@ -154,10 +172,325 @@ void pack_slab(const wrnn_ctx &h, int w, float *out) {
     for (int j = 0; j < R; ++j) out[s.wi0 + j] = IW[(size_t)j * nin];
 }
 
+RowsSlab make_rows_slab(const wrnn_ctx &h) {
+    const int R = h.cfg.rnn_dims, F = h.cfg.fc_dims, NC = h.cfg.n_classes;
+    const bool mol = h.cfg.mode == WRNN_MODE_MOL;
+    RowsSlab s{};
+    int o = 0;
+    auto take = [&](int n) { int at = o; o += round4(n); return at; };
+    s.wih2 = take(3 * h.U * R);
+    s.whh1 = take(3 * h.U * R);
+    s.whh2 = take(3 * h.U * R);
+    s.w1 = take(h.UF * R);
+    s.w2 = take(h.UF * F);
+    s.w3 = take((mol ? NC : h.UC) * F);
+    s.b3 = take(mol ? NC : h.UC);
+    s.bih1 = take(3 * h.U);
+    s.bhh1 = take(3 * h.U);
+    s.bih2 = take(3 * h.U);
+    s.bhh2 = take(3 * h.U);
+    s.q1 = take(3 * h.U);
+    s.q2 = take(3 * h.U);
+    s.q3 = take(h.UF);
+    s.total = o;
+    return s;
+}
+
+// x-column constants Q = W[:, :R]·W_I[:, 0] (fp32, sequential)
+float xcol_dot(const float *wrow, const float *IW, int nin, int R) {
+    float acc = 0.0f;
+    for (int k = 0; k < R; ++k) acc = std::fma(wrow[k], IW[(size_t)k * nin], acc);
+    return acc;
+}
+
+void pack_rows_slab(const wrnn_ctx &h, int w, float *out) {
+    const int R = h.cfg.rnn_dims, F = h.cfg.fc_dims, A = h.cfg.aux_dims, NC = h.cfg.n_classes;
+    const bool mol = h.cfg.mode == WRNN_MODE_MOL;
+    const RowsSlab &s = h.rs;
+    std::fill(out, out + s.total, 0.0f);
+    auto W = [&](const char *n) { return h.w.at(n).data(); };
+    const float *IW = W("I.weight");
+    const int nin = 1 + h.cfg.feat_dims + A;
+    for (int u = 0; u < h.U; ++u) {
+        const int j = w * h.U + u;
+        if (j >= R) continue;
+        for (int g = 0; g < 3; ++g) {
+            const int src = g * R + j, dst = g * h.U + u;
+            const float *ih1 = W("rnn1.weight_ih_l0") + (size_t)src * R;
+            const float *ih2 = W("rnn2.weight_ih_l0") + (size_t)src * (R + A);
+            std::memcpy(out + s.wih2 + (size_t)dst * R, ih2, R * 4);
+            std::memcpy(out + s.whh1 + (size_t)dst * R, W("rnn1.weight_hh_l0") + (size_t)src * R, R * 4);
+            std::memcpy(out + s.whh2 + (size_t)dst * R, W("rnn2.weight_hh_l0") + (size_t)src * R, R * 4);
+            out[s.bih1 + dst] = W("rnn1.bias_ih_l0")[src];
+            out[s.bhh1 + dst] = W("rnn1.bias_hh_l0")[src];
+            out[s.bih2 + dst] = W("rnn2.bias_ih_l0")[src];
+            out[s.bhh2 + dst] = W("rnn2.bias_hh_l0")[src];
+            out[s.q1 + dst] = xcol_dot(ih1, IW, nin, R);
+            out[s.q2 + dst] = xcol_dot(ih2, IW, nin, R);
+        }
+    }
+    for (int r = 0; r < h.UF; ++r) {
+        const int j = w * h.UF + r;
+        if (j >= F) continue;
+        const float *w1 = W("fc1.weight") + (size_t)j * (R + A);
+        std::memcpy(out + s.w1 + (size_t)r * R, w1, R * 4);
+        std::memcpy(out + s.w2 + (size_t)r * F, W("fc2.weight") + (size_t)j * (F + A), F * 4);
+        out[s.q3 + r] = xcol_dot(w1, IW, nin, R);
+    }
+    if (mol) {
+        std::memcpy(out + s.w3, W("fc3.weight"), (size_t)NC * F * 4);
+        std::memcpy(out + s.b3, W("fc3.bias"), (size_t)NC * 4);
+    } else {
+        for (int r = 0; r < h.UC; ++r) {
+            const int j = w * h.UC + r;
+            if (j >= NC) continue;
+            std::memcpy(out + s.w3 + (size_t)r * F, W("fc3.weight") + (size_t)j * F, F * 4);
+            out[s.b3 + r] = W("fc3.bias")[j];
+        }
+    }
+}
+
+// Weights of the conditioning-terms GEMM: row w·NT + k of [G·NT][KX] against X = [cI | a2 a3 a4 | 1 0 0 0]
+void pack_terms_weights(const wrnn_ctx &h, float *Wt) {
+    const int R = h.cfg.rnn_dims, F = h.cfg.fc_dims, A = h.cfg.aux_dims, U = h.U, UF = h.UF, KX = h.KX;
+    auto W = [&](const char *n) { return h.w.at(n).data(); };
+    std::fill(Wt, Wt + (size_t)h.G * h.NT * KX, 0.0f);
+    for (int w = 0; w < h.G; ++w)
+        for (int k = 0; k < 6 * U + 2 * UF; ++k) {
+            float *row = Wt + ((size_t)w * h.NT + k) * KX;
+            if (k < 6 * U) {
+                const int kk = k % (3 * U), g = kk / U, j = w * U + kk % U;
+                if (j >= R) continue;
+                if (k < 3 * U) {
+                    std::memcpy(row, W("rnn1.weight_ih_l0") + (size_t)(g * R + j) * R, R * 4);
+                } else {
+                    const float *ih2 = W("rnn2.weight_ih_l0") + (size_t)(g * R + j) * (R + A);
+                    std::memcpy(row, ih2, R * 4);
+                    std::memcpy(row + R, ih2 + R, A * 4);                       // a2
+                }
+            } else if (k < 6 * U + UF) {
+                const int r = w * UF + (k - 6 * U);
+                if (r >= F) continue;
+                const float *w1 = W("fc1.weight") + (size_t)r * (R + A);
+                std::memcpy(row, w1, R * 4);
+                std::memcpy(row + R + A, w1 + R, A * 4);                        // a3
+                row[R + 3 * A] = W("fc1.bias")[r];
+            } else {
+                const int r = w * UF + (k - 6 * U - UF);
+                if (r >= F) continue;
+                std::memcpy(row + R + 2 * A, W("fc2.weight") + (size_t)r * (F + A) + F, A * 4);   // a4
+                row[R + 3 * A] = W("fc2.bias")[r];
+            }
+        }
+}
+
+size_t rows_lds_bytes(const wrnn_ctx &h, int B, int TB) {
+    return (size_t)rows_lds_layout(h.rs.total, B, TB, h.cfg.rnn_dims, h.cfg.fc_dims, h.cfg.n_classes, h.NK, h.U, h.UF,
+                                   h.G)
+               .total * sizeof(float);
+}
+
+// Largest tile (<= 16 rows) that fits next to B rows of state; 0 if none does
+int rows_tile_for(const wrnn_ctx &h, int B) {
+    for (int tb = std::min(B, 16); tb >= 1; --tb)
+        if (rows_lds_bytes(h, B, tb) <= (size_t)h.max_lds) return tb;
+    return 0;
+}
+
 size_t lds_bytes_for(const wrnn_ctx &h, int Bc) {
     return (size_t)lds_layout(h.s.total, Bc, h.cfg.rnn_dims, h.cfg.fc_dims, h.cfg.aux_dims, h.cfg.n_classes, h.NK,
                               h.U, h.UF)
                .total * sizeof(float);
+}
+
+}  // namespace
+
+namespace {
+
+// grow-only device buffer
+template <typename T>
+hipError_t ensure(T *&p, size_t &cap, size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) {
+        hipError_t e = hipFree(p);
+        if (e != hipSuccess) return e;
+    }
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(&p, n * sizeof(T));
+    if (e == hipSuccess) cap = n;
+    return e;
+}
+
+int grow(wrnn_t *h, float *&p, size_t &cap, size_t n) {
+    HIP_TRY(h, ensure(p, cap, n));
+    return WRNN_OK;
+}
+
+// B rows through the multi-row kernel: row groups of <= kRowsMax, time chunks sized so the
+// precomputed terms stay within WRNN_TERMS_MB (default 2048 MiB).
+int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed, int64_t row_offset,
+                  float *out, int32_t *labels, hipStream_t st) {
+    const wrnn_config &c = h->cfg;
+    const int R = c.rnn_dims, A = c.aux_dims, N = h->G * h->NT;
+    if (!h->d_flags) {
+        HIP_TRY(h, hipMalloc(&h->d_flags, (size_t)kRowsHops * kFlagSlots * kFlagStride * 4));
+        HIP_TRY(h, hipMalloc(&h->d_xr, (size_t)kXReps * kXRepStride * 8));
+    }
+    if (!h->blas && rocblas_create_handle(&h->blas) != rocblas_status_success)
+        return fail(h, WRNN_EHIP, "rocblas_create_handle failed");
+    if (rocblas_set_stream(h->blas, st) != rocblas_status_success) return fail(h, WRNN_EHIP, "rocblas_set_stream failed");
+    const char *mb_env = std::getenv("WRNN_TERMS_MB");
+    const double budget = (mb_env ? std::atof(mb_env) : 2048.0) * (1 << 20) / 4.0;   // floats
+    const float one = 1.0f, zero = 0.0f;
+    for (int b0 = 0; b0 < B;) {
+        int Bl = std::min(B - b0, kRowsMax);
+        while (Bl > 1 && rows_tile_for(*h, Bl) == 0) --Bl;
+        const int TB = rows_tile_for(*h, Bl);
+        if (TB == 0) return fail(h, WRNN_EUNSUPPORTED, "rows kernel: one row of state does not fit LDS");
+        const int SW = rows_state_width(h->U, h->UF);
+        const int Lc_max = (int)std::max(1.0, std::min((double)L, budget / ((double)Bl * (N + h->KX))));
+        if (grow(h, h->d_X, h->X_cap, (size_t)Lc_max * Bl * h->KX) ||
+            grow(h, h->d_T, h->T_cap, (size_t)Lc_max * Bl * N) ||
+            grow(h, h->d_act, h->act_cap, (size_t)kRowsHops * 2 * Bl * h->KA) ||
+            grow(h, h->d_state, h->state_cap, (size_t)h->G * Bl * SW + Bl))
+            return WRNN_EHIP;
+        HIP_TRY(h, hipMemsetAsync(h->d_flags, 0, (size_t)kRowsHops * kFlagSlots * kFlagStride * 4, st));
+        HIP_TRY(h, hipMemsetAsync(h->d_xr, 0, (size_t)kXReps * kXRepStride * 8, st));
+        for (int t0 = 0; t0 < L; t0 += Lc_max) {
+            const int Lc = std::min(Lc_max, L - t0);
+            // conditioning terms of steps [t0, t0 + Lc): cI, then one fp32 GEMM for every workgroup's terms
+            HIP_TRY(h, launch_ci_gemm(cond, h->CD, B, b0, Bl, t0, Lc, h->d_IW, 1 + c.feat_dims + A, h->d_Ib, R,
+                                      c.feat_dims + A, h->d_X, h->KX, st));
+            HIP_TRY(h, launch_pack_terms_input(cond, h->CD, B, b0, Bl, t0, Lc, c.feat_dims, A, R, h->KX, h->d_X, st));
+            if (rocblas_sgemm(h->blas, rocblas_operation_transpose, rocblas_operation_none, N, Lc * Bl, h->KX, &one,
+                              h->d_Wt, h->KX, h->d_X, h->KX, &zero, h->d_T, N) != rocblas_status_success)
+                return fail(h, WRNN_EHIP, "rocblas_sgemm (conditioning terms) failed");
+            RowsArgs a{};
+            a.slab = h->d_rslab;
+            a.terms = h->d_T;
+            a.noise = noise;
+            a.out = out;
+            a.labels = labels;
+            a.act = h->d_act;
+            a.flags = h->d_flags;
+            a.xg = h->d_xr;
+            a.state = h->d_state;
+            a.ctl = h->d_ctl;
+            a.seed = seed;
+            a.row0 = row_offset + b0;
+            a.timeout_ticks = h->timeout_ticks;
+            a.L = L;
+            a.t0 = t0;
+            a.Lc = Lc;
+            a.B = Bl;
+            a.Bt = B;
+            a.b0 = b0;
+            a.R = R;
+            a.F = c.fc_dims;
+            a.A = A;
+            a.NC = c.n_classes;
+            a.NK = h->NK;
+            a.mol = c.mode == WRNN_MODE_MOL;
+            a.U = h->U;
+            a.UF = h->UF;
+            a.UC = h->UC;
+            a.G = h->G;
+            a.NT = h->NT;
+            a.TB = TB;
+            a.KA = h->KA;
+            a.s = h->rs;
+            HIP_TRY(h, launch_rows(a, rows_lds_bytes(*h, Bl, TB), st));
+        }
+        b0 += Bl;
+    }
+    return WRNN_OK;
+}
+
+int generate_latency(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed,
+                     int64_t row_offset, float *out, int32_t *labels, hipStream_t st) {
+    const wrnn_config &c = h->cfg;
+    const int R = c.rnn_dims;
+    const int Bc_max = std::min(B, h->max_rows);
+    // workspaces (grow-only)
+    if (grow(h, h->d_cI, h->cI_cap, (size_t)L * Bc_max * R)) return WRNN_EHIP;
+    // hand-off replicas (WRNN_REPLICAS, default 8), each padded to a 64 KiB boundary
+    const char *rep_env = std::getenv("WRNN_REPLICAS");
+    const int reps = std::max(1, std::min(64, rep_env ? std::atoi(rep_env) : 8));
+    // replica stride ≥ 64 KiB: keeps replicas on different lines/channels and makes the
+    // pollers' fixed-count over-reads (slots ≥ n) land in allocated memory
+    const long long vec_max = std::max<long long>({(long long)Bc_max * h->NMAX, (long long)Bc_max * R * kTermsPerUnit,
+                                                   3LL * R});
+    const long long rep_stride = (((vec_max + kOverRead) * 8 + 65535) / 65536) * 65536 / 8;
+    const size_t need_xg = (size_t)kHops * reps * rep_stride;
+    HIP_TRY(h, ensure(h->d_xg, h->xg_cap, need_xg));
+    // diagnostics: WRNN_DEBUG_STAMPS=<steps> WRNN_DEBUG_FILE=<path> dumps per-stage stamps
+    const char *dbg_env = std::getenv("WRNN_DEBUG_STAMPS");
+    const int dbg_steps = dbg_env ? std::min(L, std::atoi(dbg_env)) : 0;
+    unsigned *d_dbg = nullptr;
+    if (dbg_steps > 0) {
+        HIP_TRY(h, hipMalloc(&d_dbg, (size_t)h->G * dbg_steps * kStamps * 4));
+        HIP_TRY(h, hipMemsetAsync(d_dbg, 0, (size_t)h->G * dbg_steps * kStamps * 4, st));
+    }
+    for (int b0 = 0; b0 < B; b0 += h->max_rows) {
+        const int Bc = std::min(h->max_rows, B - b0);
+        HIP_TRY(h, launch_ci_gemm(cond, h->CD, B, b0, Bc, 0, L, h->d_IW, 1 + c.feat_dims + c.aux_dims, h->d_Ib, R,
+                                  c.feat_dims + c.aux_dims, h->d_cI, R, st));
+        HIP_TRY(h, hipMemsetAsync(h->d_xg, 0, need_xg * 8, st));
+        LoopArgs a{};
+        a.slab = h->d_slab;
+        a.cI = h->d_cI;
+        a.cond = cond;
+        a.noise = noise;
+        a.out = out;
+        a.labels = labels;
+        a.xg = h->d_xg;
+        a.reps = reps;
+        {
+            const char *dp = std::getenv("WRNN_DELAY_POLL");
+            a.delay_poll = dp ? std::atoi(dp) : 1;
+        }
+        a.rep_stride = rep_stride;
+        a.ctl = h->d_ctl;
+        a.seed = seed;
+        a.row0 = row_offset + b0;
+        a.timeout_ticks = h->timeout_ticks;
+        a.L = L;
+        a.Bc = Bc;
+        a.Bt = B;
+        a.b0 = b0;
+        a.R = R;
+        a.F = c.fc_dims;
+        a.A = c.aux_dims;
+        a.CD = h->CD;
+        a.feat = c.feat_dims;
+        a.NC = c.n_classes;
+        a.NK = h->NK;
+        a.mol = c.mode == WRNN_MODE_MOL;
+        a.U = h->U;
+        a.UF = h->UF;
+        a.UC = h->UC;
+        a.G = h->G;
+        a.NMAX = h->NMAX;
+        a.s = h->s;
+        a.dbg = (b0 == 0) ? d_dbg : nullptr;
+        a.dbg_steps = dbg_steps;
+        HIP_TRY(h, launch_loop(a, lds_bytes_for(*h, Bc), st));
+    }
+    if (d_dbg) {
+        std::vector<unsigned> host((size_t)h->G * dbg_steps * kStamps);
+        HIP_TRY(h, hipStreamSynchronize(st));
+        HIP_TRY(h, hipMemcpy(host.data(), d_dbg, host.size() * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(h, hipFree(d_dbg));
+        const char *path = std::getenv("WRNN_DEBUG_FILE");
+        if (FILE *f = std::fopen(path ? path : "wrnn_stamps.bin", "wb")) {
+            int hdr[3] = {h->G, dbg_steps, kStamps};
+            std::fwrite(hdr, sizeof(hdr), 1, f);
+            std::fwrite(host.data(), 4, host.size(), f);
+            std::fclose(f);
+        }
+    }
+    return WRNN_OK;
 }
 
 }  // namespace
@@ -200,6 +533,11 @@ int wrnn_create(const wrnn_config *cfg, int device, wrnn_t **out) {
     h->CD = c.feat_dims + 4 * c.aux_dims;
     h->s = make_slab_layout(*h);
     // rows per launch: LDS, and the per-thread gather register budget
+    h->rs = make_rows_slab(*h);
+    h->NT = rows_terms(h->U, h->UF);
+    h->KX = R + 3 * c.aux_dims + 4;
+    h->KA = round4(std::max(R, std::max(F, c.n_classes)));
+    h->rows_ok = rows_tile_for(*h, 1) > 0;
     h->max_rows = 0;
     for (int b = 1; b <= 64; ++b) {
         if (lds_bytes_for(*h, b) > (size_t)h->max_lds) break;
@@ -209,16 +547,23 @@ int wrnn_create(const wrnn_config *cfg, int device, wrnn_t **out) {
         if (fast ? b > 2 : (size_t)b * h->NMAX > (size_t)kPollThreads * kGatherMax) break;
         h->max_rows = b;
     }
-    if (h->max_rows < 1)
+    if (h->max_rows < 1 && !h->rows_ok)
         return fail(h, WRNN_EUNSUPPORTED, "weight slab + one row of state exceeds LDS (" +
                                               std::to_string(lds_bytes_for(*h, 1)) + " B)");
     HIP_TRY(h, prepare_loop_kernel(h->max_lds));
+    HIP_TRY(h, prepare_rows_kernel(h->max_lds));
     int per_cu = 0;
-    HIP_TRY(h, loop_occupancy(&per_cu, lds_bytes_for(*h, h->max_rows)));
-    if (per_cu * h->num_cus < h->G)
-        return fail(h, WRNN_EUNSUPPORTED, "persistent grid of " + std::to_string(h->G) +
-                                              " workgroups is not co-resident (" + std::to_string(per_cu) +
-                                              "/CU × " + std::to_string(h->num_cus) + " CUs)");
+    if (h->max_rows >= 1) {
+        HIP_TRY(h, loop_occupancy(&per_cu, lds_bytes_for(*h, h->max_rows)));
+        if (per_cu * h->num_cus < h->G)
+            return fail(h, WRNN_EUNSUPPORTED, "persistent grid of " + std::to_string(h->G) +
+                                                  " workgroups is not co-resident (" + std::to_string(per_cu) +
+                                                  "/CU × " + std::to_string(h->num_cus) + " CUs)");
+    }
+    if (h->rows_ok) {
+        HIP_TRY(h, rows_occupancy(&per_cu, rows_lds_bytes(*h, 1, 1)));
+        if (per_cu * h->num_cus < h->G) h->rows_ok = false;
+    }
     h->timeout_ticks = (long long)(c.timeout_ms > 0 ? c.timeout_ms : 2000) * 100000LL;   // 100 MHz
     HIP_TRY(h, hipMalloc(&h->d_ctl, kCtlWords * sizeof(int)));
     HIP_TRY(h, hipMemset(h->d_ctl, 0, kCtlWords * sizeof(int)));
@@ -259,6 +604,16 @@ int wrnn_set_weights(wrnn_t *h, const wrnn_tensor *tensors, int n) {
     if (!h->d_Ib) HIP_TRY(h, hipMalloc(&h->d_Ib, Ib.size() * 4));
     HIP_TRY(h, hipMemcpy(h->d_IW, IW.data(), IW.size() * 4, hipMemcpyHostToDevice));
     HIP_TRY(h, hipMemcpy(h->d_Ib, Ib.data(), Ib.size() * 4, hipMemcpyHostToDevice));
+    if (h->rows_ok) {
+        std::vector<float> rslab((size_t)h->G * h->rs.total);
+        for (int w = 0; w < h->G; ++w) pack_rows_slab(*h, w, rslab.data() + (size_t)w * h->rs.total);
+        if (!h->d_rslab) HIP_TRY(h, hipMalloc(&h->d_rslab, rslab.size() * 4));
+        HIP_TRY(h, hipMemcpy(h->d_rslab, rslab.data(), rslab.size() * 4, hipMemcpyHostToDevice));
+        std::vector<float> Wt((size_t)h->G * h->NT * h->KX);
+        pack_terms_weights(*h, Wt.data());
+        if (!h->d_Wt) HIP_TRY(h, hipMalloc(&h->d_Wt, Wt.size() * 4));
+        HIP_TRY(h, hipMemcpy(h->d_Wt, Wt.data(), Wt.size() * 4, hipMemcpyHostToDevice));
+    }
     h->ready = true;
     return WRNN_OK;
 }
@@ -271,102 +626,21 @@ int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise
     if (labels && h->cfg.mode != WRNN_MODE_RAW) return fail(h, WRNN_EINVAL, "labels are a RAW-mode output");
     HIP_TRY(h, hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
-    const wrnn_config &c = h->cfg;
-    const int R = c.rnn_dims;
-    const int Bc_max = std::min(B, h->max_rows);
-    // workspaces (grow-only)
-    const size_t need_cI = (size_t)L * Bc_max * R;
-    if (need_cI > h->cI_cap) {
-        if (h->d_cI) HIP_TRY(h, hipFree(h->d_cI));
-        h->d_cI = nullptr;
-        HIP_TRY(h, hipMalloc(&h->d_cI, need_cI * 4));
-        h->cI_cap = need_cI;
-    }
-    // hand-off replicas (WRNN_REPLICAS, default 8), each padded to a 64 KiB boundary
-    const char *rep_env = std::getenv("WRNN_REPLICAS");
-    const int reps = std::max(1, std::min(64, rep_env ? std::atoi(rep_env) : 8));
-    // replica stride ≥ 64 KiB: keeps replicas on different lines/channels and makes the
-    // pollers' fixed-count over-reads (slots ≥ n) land in allocated memory
-    const long long vec_max = std::max<long long>({(long long)Bc_max * h->NMAX, (long long)Bc_max * R * kTermsPerUnit,
-                                                   3LL * R});
-    const long long rep_stride = (((vec_max + kOverRead) * 8 + 65535) / 65536) * 65536 / 8;
-    const size_t need_xg = (size_t)kHops * reps * rep_stride;
-    if (need_xg > h->xg_cap) {
-        if (h->d_xg) HIP_TRY(h, hipFree(h->d_xg));
-        h->d_xg = nullptr;
-        HIP_TRY(h, hipMalloc(&h->d_xg, need_xg * 8));
-        h->xg_cap = need_xg;
-    }
+    // path: the latency kernel while the rows fit its LDS layout in one launch, else the
+    // multi-row kernel; WRNN_PATH=latency|rows forces one (tests, benchmarks)
+    const char *path_env = std::getenv("WRNN_PATH");
+    bool rows = h->max_rows < 1 || B > h->max_rows;
+    if (path_env && std::string(path_env) == "rows") rows = true;
+    if (path_env && std::string(path_env) == "latency" && h->max_rows >= 1) rows = false;
+    if (rows && !h->rows_ok) rows = false;
     HIP_TRY(h, hipMemsetAsync(h->d_ctl, 0, kCtlWords * sizeof(int), st));
-    // diagnostics: WRNN_DEBUG_STAMPS=<steps> WRNN_DEBUG_FILE=<path> dumps per-stage stamps
-    const char *dbg_env = std::getenv("WRNN_DEBUG_STAMPS");
-    const int dbg_steps = dbg_env ? std::min(L, std::atoi(dbg_env)) : 0;
-    unsigned *d_dbg = nullptr;
-    if (dbg_steps > 0) {
-        HIP_TRY(h, hipMalloc(&d_dbg, (size_t)h->G * dbg_steps * kStamps * 4));
-        HIP_TRY(h, hipMemsetAsync(d_dbg, 0, (size_t)h->G * dbg_steps * kStamps * 4, st));
-    }
-    for (int b0 = 0; b0 < B; b0 += h->max_rows) {
-        const int Bc = std::min(h->max_rows, B - b0);
-        HIP_TRY(h, launch_ci_gemm(cond, h->CD, B, b0, Bc, L, h->d_IW, 1 + c.feat_dims + c.aux_dims, h->d_Ib, R,
-                                  c.feat_dims + c.aux_dims, h->d_cI, st));
-        HIP_TRY(h, hipMemsetAsync(h->d_xg, 0, need_xg * 8, st));
-        LoopArgs a{};
-        a.slab = h->d_slab;
-        a.cI = h->d_cI;
-        a.cond = cond;
-        a.noise = noise;
-        a.out = out;
-        a.labels = labels;
-        a.xg = h->d_xg;
-        a.reps = reps;
-        {
-            const char *dp = std::getenv("WRNN_DELAY_POLL");
-            a.delay_poll = dp ? std::atoi(dp) : 1;
-        }
-        a.rep_stride = rep_stride;
-        a.ctl = h->d_ctl;
-        a.seed = seed;
-        a.row0 = row_offset + b0;
-        a.timeout_ticks = h->timeout_ticks;
-        a.L = L;
-        a.Bc = Bc;
-        a.Bt = B;
-        a.b0 = b0;
-        a.R = R;
-        a.F = c.fc_dims;
-        a.A = c.aux_dims;
-        a.CD = h->CD;
-        a.feat = c.feat_dims;
-        a.NC = c.n_classes;
-        a.NK = h->NK;
-        a.mol = c.mode == WRNN_MODE_MOL;
-        a.U = h->U;
-        a.UF = h->UF;
-        a.UC = h->UC;
-        a.G = h->G;
-        a.NMAX = h->NMAX;
-        a.s = h->s;
-        a.dbg = (b0 == 0) ? d_dbg : nullptr;
-        a.dbg_steps = dbg_steps;
-        if (b0 == 0) HIP_TRY(h, hipEventRecord(h->ev0, st));
-        HIP_TRY(h, launch_loop(a, lds_bytes_for(*h, Bc), st));
-    }
+    HIP_TRY(h, hipEventRecord(h->ev0, st));
+    h->last_path = rows ? 2 : 1;
+    const int rc = rows ? generate_rows(h, cond, B, L, noise, seed, row_offset, out, labels, st)
+                        : generate_latency(h, cond, B, L, noise, seed, row_offset, out, labels, st);
+    if (rc != WRNN_OK) return rc;
     HIP_TRY(h, hipEventRecord(h->ev1, st));
     h->timed = true;
-    if (d_dbg) {
-        std::vector<unsigned> host((size_t)h->G * dbg_steps * kStamps);
-        HIP_TRY(h, hipStreamSynchronize(st));
-        HIP_TRY(h, hipMemcpy(host.data(), d_dbg, host.size() * 4, hipMemcpyDeviceToHost));
-        HIP_TRY(h, hipFree(d_dbg));
-        const char *path = std::getenv("WRNN_DEBUG_FILE");
-        if (FILE *f = std::fopen(path ? path : "wrnn_stamps.bin", "wb")) {
-            int hdr[3] = {h->G, dbg_steps, kStamps};
-            std::fwrite(hdr, sizeof(hdr), 1, f);
-            std::fwrite(host.data(), 4, host.size(), f);
-            std::fclose(f);
-        }
-    }
     return WRNN_OK;
 }
 
@@ -377,10 +651,13 @@ int wrnn_check(wrnn_t *h, void *stream) {
     int ctl[kCtlWords];
     HIP_TRY(h, hipMemcpy(ctl, h->d_ctl, sizeof(ctl), hipMemcpyDeviceToHost));
     if (ctl[1] != 0) {
-        static const char *hops[] = {"h1", "h2", "f1", "f2", "logits"};
+        static const char *lat_hops[] = {"q1", "h2", "f1", "f2", "logits", "gru1-terms", "gru1-terms"};
+        static const char *row_hops[] = {"h1", "h2", "f1", "f2", "logits", "x"};
         const int hop = ctl[3];
+        const char *name = h->last_path == 2 ? (hop >= 0 && hop < 6 ? row_hops[hop] : "?")
+                                             : (hop >= 0 && hop < 7 ? lat_hops[hop] : "?");
         return fail(h, WRNN_ETIMEOUT,
-                    "persistent kernel aborted: wait on hand-off '" + std::string(hop >= 0 && hop < 5 ? hops[hop] : "?") +
+                    "persistent kernel aborted: wait on hand-off '" + std::string(name) +
                         "' at step " + std::to_string(ctl[2]) + " in workgroup " + std::to_string(ctl[4]) +
                         " exceeded the timeout (grid not co-resident, or a fault)");
     }
@@ -416,8 +693,10 @@ void wrnn_destroy(wrnn_t *h) {
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     for (void *p : {(void *)h->d_slab, (void *)h->d_IW, (void *)h->d_Ib, (void *)h->d_cI, (void *)h->d_xg,
-                    (void *)h->d_ctl})
+                    (void *)h->d_ctl, (void *)h->d_rslab, (void *)h->d_Wt, (void *)h->d_X, (void *)h->d_T,
+                    (void *)h->d_act, (void *)h->d_state, (void *)h->d_flags, (void *)h->d_xr})
         if (p) (void)hipFree(p);
+    if (h->blas) (void)rocblas_destroy_handle(h->blas);
     delete h;
 }
 

@@ -21,268 +21,12 @@
 #include <stdint.h>
 
 #include "fatchord_loop.h"
+#include "wrnn_device.h"
 
 namespace wrnn {
 
-// ------------------------------------------------------------------ wave-level helpers
-#define WRNN_DPP(v, ctrl) \
-    __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, (v)), (ctrl), 0xF, 0xF, false))
-
-// Full-wave sum; every lane returns the same bits.  Row stages via DPP (xor1, xor2,
-// half-mirror, mirror), then the four row sums combined in a fixed order.
-__device__ __forceinline__ float wave_sum(float v) {
-    v += WRNN_DPP(v, 0xB1);    // quad_perm [1,0,3,2]
-    v += WRNN_DPP(v, 0x4E);    // quad_perm [2,3,0,1]
-    v += WRNN_DPP(v, 0x141);   // row_half_mirror
-    v += WRNN_DPP(v, 0x140);   // row_mirror
-    float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
-    float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16));
-    float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
-    float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
-    return (r0 + r1) + (r2 + r3);
-}
-
-__device__ __forceinline__ float wave_max(float v) {
-    v = fmaxf(v, WRNN_DPP(v, 0xB1));
-    v = fmaxf(v, WRNN_DPP(v, 0x4E));
-    v = fmaxf(v, WRNN_DPP(v, 0x141));
-    v = fmaxf(v, WRNN_DPP(v, 0x140));
-    float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
-    float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16));
-    float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
-    float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
-    return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
-}
-
-// (value, index) argmax: larger value wins, ties go to the smaller index (torch: first max).
-__device__ __forceinline__ void am_merge(float &v, int &i, float ov, int oi) {
-    if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }
-}
-
-__device__ __forceinline__ int wave_argmax(float v, int i) {
-#define WRNN_AM_STAGE(ctrl)                                                           \
-    {                                                                                 \
-        float ov = WRNN_DPP(v, ctrl);                                                 \
-        int oi = __builtin_amdgcn_mov_dpp(i, (ctrl), 0xF, 0xF, false);                \
-        am_merge(v, i, ov, oi);                                                       \
-    }
-    WRNN_AM_STAGE(0xB1) WRNN_AM_STAGE(0x4E) WRNN_AM_STAGE(0x141) WRNN_AM_STAGE(0x140)
-#undef WRNN_AM_STAGE
-    float bv = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
-    int bi = __builtin_amdgcn_readlane(i, 0);
-#pragma unroll
-    for (int r = 16; r < 64; r += 16) {
-        float ov = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), r));
-        int oi = __builtin_amdgcn_readlane(i, r);
-        am_merge(bv, bi, ov, oi);
-    }
-    return bi;
-}
-
-// NR dot products against one shared vector: acc[r] += W[r]·x over K4 float4 chunks,
-// row r at w0 + r·wstride.  Lane l takes chunks l, l+64, … (contiguous 16 B per lane:
-// conflict-free ds_read_b128).
-template <int NR>
-__device__ __forceinline__ void dots(const float *__restrict__ w0, int wstride, const float *__restrict__ x,
-                                     int K4, int lane, float (&acc)[NR]) {
-    const float4 *x4 = reinterpret_cast<const float4 *>(x);
-#pragma unroll 4
-    for (int c = lane; c < K4; c += 64) {
-        const float4 xv = x4[c];
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            const float4 wv = reinterpret_cast<const float4 *>(w0 + r * wstride)[c];
-            float a = acc[r];
-            a = fmaf(wv.x, xv.x, a);
-            a = fmaf(wv.y, xv.y, a);
-            a = fmaf(wv.z, xv.z, a);
-            a = fmaf(wv.w, xv.w, a);
-            acc[r] = a;
-        }
-    }
-}
-
-// Gate nonlinearities on the critical path use the hardware exp2 (v_exp_f32) and reciprocal:
-// ≈1e-7 absolute error, inside the parity tolerance (the reference's SLEEF/MKL paths are not
-// correctly rounded either).  Samplers keep the accurate libm functions.
-__device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
-__device__ __forceinline__ float sigmoid_(float x) { return __builtin_amdgcn_rcpf(1.0f + fast_exp(-x)); }
-__device__ __forceinline__ float tanh_(float x) {
-    const float e = fast_exp(-2.0f * fabsf(x));            // in (0, 1]: no overflow
-    const float t = (1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e);
-    return copysignf(t, x);
-}
-
-// ------------------------------------------------------------------------------ Philox
-__device__ __forceinline__ uint32_t philox_word(unsigned long long seed, unsigned long long row,
-                                                uint32_t step, uint32_t k) {
-    uint32_t c0 = k >> 2, c1 = step, c2 = (uint32_t)row, c3 = (uint32_t)(row >> 32);
-    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-#pragma unroll
-    for (int i = 0; i < 10; ++i) {
-        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
-        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
-        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
-        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
-        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
-    }
-    const uint32_t w = k & 3;
-    return w == 0 ? c0 : w == 1 ? c1 : w == 2 ? c2 : c3;
-}
-
-// Draw k of row/step in the reference distribution (MOL: U(1e-5, 1-1e-5); RAW: Exp(1)).
-__device__ __forceinline__ float philox_noise(unsigned long long seed, unsigned long long row,
-                                              uint32_t step, uint32_t k, int mol) {
-    const uint32_t w = philox_word(seed, row, step, k);
-    if (mol) return 1e-5f + (1.0f - 2e-5f) * ((float)(w >> 8) * 0x1p-24f);
-    return -logf((float)((w >> 8) + 1u) * 0x1p-24f);
-}
-
-// ---------------------------------------------------------------------------- hand-off
-__device__ __forceinline__ void publish(unsigned long long *g, uint32_t tag, float v) {
-    const unsigned long long x = ((unsigned long long)tag << 32) | __float_as_uint(v);
-    __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __noinline__ void record_abort(int *ctl, int code, int step, int hop, int wg) {
-    if (atomicCAS(&ctl[1], 0, code) == 0) {
-        ctl[2] = step;
-        ctl[3] = hop;
-        ctl[4] = wg;
-    }
-    __hip_atomic_store(&ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Gather granules [base, base + NG·NL) ∩ [0, n) of one hand-off vector (n = rows·N values);
-// store(b, j, v) puts each value where it belongs.  Called by NL lanes (lane id `lid`).  A
-// pass issues NG UNCONDITIONAL loads (slots >= n re-read padding: the granule buffer has
-// kOverRead spare granules after every vector) and only then inspects them: guarding each load
-// with a runtime condition makes hipcc branch around it and wait vmcnt(0) per load, i.e. NG
-// serialized memory round trips per pass (measured: 2-4x slower hops).
-// On timeout, or when another workgroup has aborted, sets *lds_abort.
-template <int NG, int NL, typename Store>
-__device__ __forceinline__ void gather(const unsigned long long *g, int base, int n, int N, uint32_t tag, int *ctl,
-                                       long long timeout, int step, int hop, int *lds_abort, int lid, Store store,
-                                       unsigned *dbg_slot = nullptr) {
-    const unsigned long long *gp = g + base + lid;
-    const int i0 = base + lid;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    unsigned spins = 0;
-    for (;;) {
-        unsigned long long v[NG];
-#pragma unroll
-        for (int k = 0; k < NG; ++k) v[k] = __hip_atomic_load(gp + k * NL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        bool ok = true;
-#pragma unroll
-        for (int k = 0; k < NG; ++k) ok &= (i0 + k * NL >= n) | ((uint32_t)(v[k] >> 32) == tag);
-        if (dbg_slot && spins == 0 && lid == 0) dbg_slot[1] = (unsigned)(__builtin_amdgcn_s_memrealtime() - t0);
-        if (ok) {
-#pragma unroll
-            for (int k = 0; k < NG; ++k) {
-                const int i = i0 + k * NL;
-                if (i < n) {
-                    const int b = i / N;
-                    store(b, i - b * N, __uint_as_float((uint32_t)v[k]));
-                }
-            }
-            break;
-        }
-        if ((++spins & 63u) == 0) {
-            const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - t0) > timeout;
-            const bool other = __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-            if (late || other) {
-                if (late) record_abort(ctl, -4, step, hop, blockIdx.x);
-                *lds_abort = 1;
-                break;
-            }
-        }
-    }
-    if (dbg_slot && lid == 0) dbg_slot[0] = spins + 1;
-}
-
-// A long, off-critical-path vector gathered in chunks of NG·NL granules (bounded registers).
-template <int NG, int NL, typename Store>
-__device__ __forceinline__ void gather_chunked(const unsigned long long *g, int n, int N, uint32_t tag, int *ctl,
-                                               long long timeout, int step, int hop, int *lds_abort, int lid,
-                                               Store store) {
-    for (int c0 = 0; c0 < n; c0 += NG * NL) {
-        gather<NG, NL>(g, c0, n, N, tag, ctl, timeout, step, hop, lds_abort, lid, store);
-        if (*reinterpret_cast<volatile int *>(lds_abort)) return;
-    }
-}
-
 // Stage work item `it` → wave: items go to the non-polling waves 1,2,3 first, the poller last.
 __device__ __forceinline__ int first_item(int wave) { return (wave + kWaves - 1) & (kWaves - 1); }
-
-// ---- 16-lane row dots: a wave holds four DPP rows; row r (= lane >> 4) computes one dot,
-// lane li (= lane & 15) of the row takes float4 chunks li, li+16, …
-__device__ __forceinline__ float row_sum16(float v) {
-    v += WRNN_DPP(v, 0xB1);    // quad_perm [1,0,3,2]
-    v += WRNN_DPP(v, 0x4E);    // quad_perm [2,3,0,1]
-    v += WRNN_DPP(v, 0x141);   // row_half_mirror
-    v += WRNN_DPP(v, 0x140);   // row_mirror
-    return v;                  // the row's sum, identical bits in all 16 lanes
-}
-
-__device__ __forceinline__ float row_dot(const float *__restrict__ w, const float *__restrict__ x, int K4, int li) {
-    const float4 *w4 = reinterpret_cast<const float4 *>(w);
-    const float4 *x4 = reinterpret_cast<const float4 *>(x);
-    float acc = 0.0f;
-#pragma unroll 8
-    for (int c = li; c < K4; c += 16) {
-        const float4 a = w4[c], b = x4[c];
-        acc = fmaf(a.x, b.x, acc);
-        acc = fmaf(a.y, b.y, acc);
-        acc = fmaf(a.z, b.z, acc);
-        acc = fmaf(a.w, b.w, acc);
-    }
-    return row_sum16(acc);
-}
-
-// Two rows against one x in a single pass (ILP for the 30-row MoL head).
-__device__ __forceinline__ float2 row_dot2(const float *__restrict__ w0, const float *__restrict__ w1,
-                                          const float *__restrict__ x, int K4, int li) {
-    const float4 *a4 = reinterpret_cast<const float4 *>(w0);
-    const float4 *b4 = reinterpret_cast<const float4 *>(w1);
-    const float4 *x4 = reinterpret_cast<const float4 *>(x);
-    float s0 = 0.0f, s1 = 0.0f;
-#pragma unroll 8
-    for (int c = li; c < K4; c += 16) {
-        const float4 a = a4[c], b = b4[c], v = x4[c];
-        s0 = fmaf(a.x, v.x, s0); s0 = fmaf(a.y, v.y, s0); s0 = fmaf(a.z, v.z, s0); s0 = fmaf(a.w, v.w, s0);
-        s1 = fmaf(b.x, v.x, s1); s1 = fmaf(b.y, v.y, s1); s1 = fmaf(b.z, v.z, s1); s1 = fmaf(b.w, v.w, s1);
-    }
-    return make_float2(row_sum16(s0), row_sum16(s1));
-}
-
-__device__ __forceinline__ float lane_bcast(float v, int src) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src));
-}
-
-// Whole-wave dot (one dot, 64 lanes): lane l takes chunks l, l+64, …
-__device__ __forceinline__ float wave_dot(const float *__restrict__ w, const float *__restrict__ x, int K4, int lane) {
-    float acc[1] = {0.f};
-    dots<1>(w, 0, x, K4, lane, acc);
-    return wave_sum(acc[0]);
-}
-
-__device__ __forceinline__ float gru_gate_math(float gi_r, float gi_z, float gi_n, float gh_r, float gh_z,
-                                               float gh_n, float h_old) {
-    // ATen gru_cell order (bit-exact vs torch.nn.GRUCell on CPU in the oracle):
-    // r = σ(hr + ir), z = σ(hz + iz), n = tanh(in + hn·r), h' = (h − n)·z + n
-    const float r = sigmoid_(gh_r + gi_r);
-    const float z = sigmoid_(gh_z + gi_z);
-    const float n = tanh_(gi_n + gh_n * r);
-    return (h_old - n) * z + n;
-}
-
-// LDS-only workgroup barrier.  Unlike __syncthreads() it does not drain vmcnt, so the loader
-// wave's LDS-DMA and the publishers' granule stores stay in flight across it.
-__device__ __forceinline__ void bar() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-}
 
 // Diagnostic stamp (only when a.dbg != 0): thread 0 records s_memrealtime into LDS slot k of
 // step t's half (double-buffered by step parity); the loader wave flushes step t-1's half to
@@ -296,8 +40,6 @@ __device__ __forceinline__ void bar() {
         if (dbg_on && lane == 0) stamp[(t & 1) * kStamps + (k)] = (unsigned)__builtin_amdgcn_s_memrealtime(); \
     } while (0)
 
-#define WRNN_GPTR(p) ((__attribute__((address_space(1))) void *)(p))
-#define WRNN_LPTR(p) ((__attribute__((address_space(3))) void *)(p))
 
 // ------------------------------------------------------------------------ the loop kernel
 //
@@ -386,7 +128,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
             const int b = i / 11, k = i - b * 11;
             float *pz = rec(0) + b * PP + R + 3 * A + k;
             const float uu = *pz;
-            *pz = k < 10 ? logf(-logf(uu)) : (logf(uu) - logf(1.0f - uu));
+            *pz = mol_noise_term(uu, k);
         }
 
     // every hop vector exists in a.reps replicas (spread over memory channels); a value is
@@ -540,7 +282,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
                     const int b = i / 11, k = i - b * 11;
                     float *pz = nz1 + b * PP + R + 3 * A + k;
                     const float uu = *pz;
-                    *pz = k < 10 ? logf(-logf(uu)) : (logf(uu) - logf(1.0f - uu));
+                    *pz = mol_noise_term(uu, k);
                 }
             }
             // record of step t+2 → ring (lands while this step's hand-offs are in flight)
@@ -714,56 +456,10 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
                 float x;
                 int label = 0;
                 if (MOL) {
-                    // utils/distribution.py:87-123
-                    float v = -INFINITY;
-                    if (lane < 10) v = l[lane] - u[lane];          // u[k] = log(-log(u1_k)), prepared by the loader
-                    int k = 0;
-                    float best = lane_bcast(v, 0);
-#pragma unroll
-                    for (int j = 1; j < 10; ++j) {
-                        const float vj = lane_bcast(v, j);
-                        if (vj > best) { best = vj; k = j; }
-                    }
-                    const float mean = l[10 + k];
-                    const float ls = fmaxf(l[20 + k], -32.23619130191664f);
-                    x = mean + expf(ls) * u[10];                      // u[10] = log(u2) − log(1 − u2)
-                    x = x < -1.0f ? -1.0f : x;
-                    x = x > 1.0f ? 1.0f : x;
+                    x = mol_sample(l, u, lane);
                 } else {
-                    // softmax → Categorical renormalise → argmax(p / q)
-                    float e[kClsPerLaneMax];
-                    float m = -INFINITY;
-#pragma unroll
-                    for (int k = 0; k < kClsPerLaneMax; ++k) {
-                        const int c = lane + 64 * k;
-                        e[k] = (c < NC) ? l[c] : -INFINITY;
-                        m = fmaxf(m, e[k]);
-                    }
-                    m = wave_max(m);
-                    float s1 = 0.0f;
-#pragma unroll
-                    for (int k = 0; k < kClsPerLaneMax; ++k) {
-                        const int c = lane + 64 * k;
-                        e[k] = (c < NC) ? expf(e[k] - m) : 0.0f;
-                        s1 += e[k];
-                    }
-                    s1 = wave_sum(s1);
-                    float s2 = 0.0f;
-#pragma unroll
-                    for (int k = 0; k < kClsPerLaneMax; ++k) {
-                        e[k] = e[k] / s1;
-                        s2 += e[k];
-                    }
-                    s2 = wave_sum(s2);
-                    float bv = -INFINITY;
-                    int bi = 0x7FFFFFFF;
-#pragma unroll
-                    for (int k = 0; k < kClsPerLaneMax; ++k) {
-                        const int c = lane + 64 * k;
-                        if (c < NC) am_merge(bv, bi, (e[k] / s2) / u[c], c);
-                    }
-                    label = wave_argmax(bv, bi);
-                    x = (2.0f * (float)label) / ((float)NC - 1.0f) - 1.0f;
+                    label = raw_sample<kClsPerLaneMax>(l, u, NC, lane);
+                    x = label_to_x(label, NC);
                 }
                 if (lane == 0) { xprev[b] = x; lbl[b] = label; }
             }
@@ -781,13 +477,13 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
 }
 
 // --------------------------------------------------------- I-layer conditioning GEMM
-// cI[t][b][r] = I.bias[r] + Σ_k I.weight[r][1+k] · cond[t][b0+b][k],  k < feat + aux
+// cI[t][b][r] = I.bias[r] + Σ_k I.weight[r][1+k] · cond[t0+t][b0+b][k],  k < feat + aux  (row stride ldc)
 // (the conditioning columns of fatchord_version.py:208-209; the x_{t-1} column is applied
 // inside the loop).  64×64 output tile per 256-thread block, K staged by 32.
 __global__ __launch_bounds__(256) void ci_gemm_kernel(const float *__restrict__ cond, int CD, int Bt, int b0,
-                                                      int Bc, int M, const float *__restrict__ W, int ldw,
+                                                      int Bc, int t0, int M, const float *__restrict__ W, int ldw,
                                                       const float *__restrict__ bias, int N, int K,
-                                                      float *__restrict__ cI) {
+                                                      float *__restrict__ cI, int ldc) {
     __shared__ float As[32][64 + 1];
     __shared__ float Ws[32][64 + 1];
     const int m0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
@@ -799,7 +495,7 @@ __global__ __launch_bounds__(256) void ci_gemm_kernel(const float *__restrict__ 
             float v = 0.0f;
             if (m < M && k < K) {
                 const int t = m / Bc, b = m - t * Bc;
-                v = cond[((size_t)t * Bt + b0 + b) * CD + k];
+                v = cond[((size_t)(t0 + t) * Bt + b0 + b) * CD + k];
             }
             As[kk][mm] = v;
             const int n = n0 + mm;
@@ -825,17 +521,18 @@ __global__ __launch_bounds__(256) void ci_gemm_kernel(const float *__restrict__ 
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int n = n0 + tx * 4 + j;
-            if (n < N) cI[(size_t)m * N + n] = acc[i][j] + bias[n];
+            if (n < N) cI[(size_t)m * ldc + n] = acc[i][j] + bias[n];
         }
     }
 }
 
 // ------------------------------------------------------------------------ host launchers
-hipError_t launch_ci_gemm(const float *cond, int CD, int Bt, int b0, int Bc, int L, const float *W, int ldw,
-                          const float *bias, int N, int K, float *cI, hipStream_t st) {
+hipError_t launch_ci_gemm(const float *cond, int CD, int Bt, int b0, int Bc, int t0, int L, const float *W, int ldw,
+                          const float *bias, int N, int K, float *cI, int ldc, hipStream_t st) {
     const int M = L * Bc;
     dim3 grid((M + 63) / 64, (N + 63) / 64);
-    hipLaunchKernelGGL(ci_gemm_kernel, grid, dim3(256), 0, st, cond, CD, Bt, b0, Bc, M, W, ldw, bias, N, K, cI);
+    hipLaunchKernelGGL(ci_gemm_kernel, grid, dim3(256), 0, st, cond, CD, Bt, b0, Bc, t0, M, W, ldw, bias, N, K, cI,
+                       ldc);
     return hipGetLastError();
 }
 

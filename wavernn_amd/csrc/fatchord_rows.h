@@ -1,0 +1,87 @@
+// Shared between the host launcher (capi.cpp) and fatchord_rows.hip: the multi-row
+// (fold-batched) variant of the sample loop.
+#pragma once
+#include <stdint.h>
+
+#include "fatchord_loop.h"
+
+namespace wrnn {
+
+// Activations of all rows move through HBM as bulk hand-offs: producers store their slice with
+// sc1 stores, drain them (s_waitcnt vmcnt(0) per storing wave), pass a workgroup barrier, and one
+// lane stores the step into the workgroup's flag; consumers poll every producer's flag, then
+// load the rows with sc1 LDS-DMA (MI355X_MICROARCH.md "Valid forms", first table row).
+constexpr int kRowsHops = 5;        // h1, h2, f1, f2, logits (RAW)
+constexpr int kFlagStride = 16;     // uints between two producers' flags (64 B)
+constexpr int kFlagSlots = 256;     // producer slots per hop: >= G, fixed so polls may over-read
+constexpr int kRowsMax = 256;       // rows per launch (x hand-off: <= 4 granules per polling lane)
+constexpr int kXReps = 8;           // replicas of the x granules
+constexpr int kXRepStride = 8192;   // granules between x replicas (64 KiB)
+constexpr int kDotEngines = 16;     // 16-lane dot engines: 4 compute waves x 4 DPP rows
+
+enum RowsHop { RH_H1 = 0, RH_H2 = 1, RH_F1 = 2, RH_F2 = 3, RH_LG = 4 };
+
+// Per-workgroup resident weights (floats).  Only the parts that multiply per-step state are
+// here; everything linear in the conditioning is in the precomputed terms.
+struct RowsSlab {
+    int wih2, whh1, whh2, w1, w2, w3, b3, bih1, bhh1, bih2, bhh2, q1, q2, q3, total;
+};
+
+// Precomputed per (step, row, workgroup) terms, NT floats: [P1 3U | P2 3U | V1c UF | V2 UF | pad]
+//   P1  = W_ih1[g·R+j]·cI             P2 = W_ih2[g·R+j]·[cI; a2]
+//   V1c = W1[r]·[cI; a3] + b1[r]      V2 = W2[r, F:]·a4 + b2[r]
+__host__ __device__ inline int rows_terms(int U, int UF) { return round4(6 * U + 2 * UF); }
+
+// Carried per-row state of a workgroup's own units (floats within a row's SW block)
+enum RowsState { RS_H1 = 0 };   // h1o U | h2o U | GH1 3U | GH2 3U | V1h UF
+__host__ __device__ inline int rows_state_width(int U, int UF) { return round4(8 * U + UF); }
+
+struct RowsArgs {
+    const float *slab;            // [G][s.total]
+    const float *terms;           // [Lc][B][G·NT] precomputed terms of this launch's steps
+    const float *noise;           // [L][Bt][NK] or nullptr (Philox)
+    float *out;                   // [Bt][L]
+    int32_t *labels;              // [Bt][L] or nullptr
+    float *act;                   // [kRowsHops][2][B][KA] activations, parity = step & 1
+    unsigned *flags;              // [kRowsHops][kFlagSlots][kFlagStride]
+    unsigned long long *xg;       // [kXReps][kXRepStride] x granules {tag | value}
+    float *state;                 // [G][B][SW] carried state, then x [B]
+    int *ctl;                     // as LoopArgs::ctl
+    unsigned long long seed;
+    long long row0;
+    long long timeout_ticks;
+    int L, t0, Lc;                // total steps, first step of this launch, steps in this launch
+    int B, Bt, b0;                // rows in this launch, rows in out/noise, first row
+    int R, F, A, NC, NK, mol, U, UF, UC, G, NT, TB, KA;
+    RowsSlab s;
+};
+
+struct RowsLds {
+    int slab, tile, st, x, ring, lg, nz, flag, total;
+    int SW, KT, NS, ncp, nkp;
+};
+
+__host__ __device__ inline RowsLds rows_lds_layout(int slab_total, int B, int TB, int R, int F, int NC, int NK,
+                                                   int U, int UF, int G) {
+    RowsLds l;
+    l.SW = rows_state_width(U, UF);
+    l.KT = round4(R > F ? (R > NC ? R : NC) : (F > NC ? F : NC));
+    l.NS = (B + G - 1) / G;                    // rows this workgroup samples (b = w, w + G, ...)
+    l.ncp = round4(NC);
+    l.nkp = round4(NK);
+    const int NT = rows_terms(U, UF);
+    const int tr = TB > l.NS ? TB : l.NS;
+    int o = 0;
+    l.slab = o;  o += round4(slab_total);
+    l.tile = o;  o += tr * l.KT;               // one tile of activation rows
+    l.st = o;    o += B * l.SW;
+    l.x = o;     o += round4(B);
+    l.ring = o;  o += 2 * B * NT;              // terms of steps t, t+1
+    l.lg = o;    o += l.NS * l.ncp;
+    l.nz = o;    o += 2 * l.NS * l.nkp;        // sampler draws of steps t, t+1
+    l.flag = o;  o += 8;
+    l.total = o;
+    return l;
+}
+
+}  // namespace wrnn

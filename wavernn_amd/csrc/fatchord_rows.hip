@@ -1,0 +1,455 @@
+// fatchord_rows.hip — persistent CDNA4 kernel for MANY rows of the WaveRNN sample loop.
+//
+// The fold-batched generate() (models/fatchord_version.py:186-188, fold_with_overlap :293-340)
+// runs B independent rows (folds, or utterances) through the same loop (:201-241).  The latency
+// kernel (fatchord_loop.hip) keeps every row's activations in LDS and exchanges them as tagged
+// granules, which fits ~1 row next to the weights.  This kernel keeps only the weights and a
+// few floats of per-row state in LDS and moves whole activation matrices [B][512] through HBM:
+//
+//   * grid = G workgroups (one per CU); workgroup w owns GRU units [w·U, w·U+U), fc1/fc2 rows
+//     [w·UF, …) and (RAW) fc3 rows [w·UC, …), as in the latency kernel;
+//   * every term that depends only on the conditioning (P1, P2, the conditioning part of fc1,
+//     V2) was computed for all steps by one fp32 GEMM before the launch (capi.cpp: rocBLAS),
+//     so a workgroup streams NT = 16 floats per row-step of its own terms;
+//   * each stage ends in a bulk hand-off (fatchord_rows.h): sc1 stores → vmcnt(0) → barrier →
+//     flag; consumers poll all G flags and LDS-DMA the rows (sc1) tile by tile;
+//   * sampling is distributed by row: workgroup w samples rows w, w+G, … (MoL: fc3 + sampler;
+//     RAW: sampler over the gathered logits) and hands x to everyone as tagged granules.
+//
+// Per step:  GRU1 own units (all rows) → [h1] → GRU2 (W_ih2[:, :R]·h1) → [h2] → fc1 → [f1] →
+//            fc2 → [f2] → (RAW: fc3 → [logits]) → sample (row-distributed) → [x] → next step.
+// Off the critical path (after a stage's flag, overlapping the next hand-off):
+//   GH1_{t+1} = W_hh1·h1_t and V1h = W1[:, :R]·h1_t (on the h1 tiles), GH2_{t+1} = W_hh2·h2_t.
+// Arithmetic is fp32 throughout, in the same re-associated forms as the latency kernel.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fatchord_rows.h"
+#include "wrnn_device.h"
+
+namespace wrnn {
+
+// Wave 0 waits until every producer flag of a hop holds >= want (flags are monotonic).
+// kFlagSlots = 256 slots are always allocated, so the four unconditional loads stay in bounds.
+__device__ __forceinline__ void wait_flags(const unsigned *f, int n, unsigned want, int *ctl, long long timeout,
+                                           int step, int hop, int *lds_abort) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned spins = 0;
+    for (;;) {
+        unsigned v[kFlagSlots / 64];
+#pragma unroll
+        for (int k = 0; k < kFlagSlots / 64; ++k)
+            v[k] = __hip_atomic_load(f + (lane + 64 * k) * kFlagStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool ok = true;
+#pragma unroll
+        for (int k = 0; k < kFlagSlots / 64; ++k) ok &= (lane + 64 * k >= n) | (v[k] >= want);
+        if (ok) break;
+        if ((++spins & 63u) == 0) {
+            const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - t0) > timeout;
+            const bool other = __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+            if (late || other) {
+                if (late) record_abort(ctl, -4, step, hop, blockIdx.x);
+                *lds_abort = 1;
+                break;
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void store_sc1(float *p, float v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <bool MOL>
+__global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, row = lane >> 4;
+    const int w = blockIdx.x;
+    const int R = a.R, F = a.F, NC = a.NC, NK = a.NK, U = a.U, UF = a.UF, UC = a.UC, G = a.G, B = a.B;
+    const int NT = a.NT, TB = a.TB, KA = a.KA;
+    const RowsLds ll = rows_lds_layout(a.s.total, B, TB, R, F, NC, NK, U, UF, G);
+    const RowsSlab &s = a.s;
+    const float *S = smem + ll.slab;
+    float *tile = smem + ll.tile, *st = smem + ll.st, *xs = smem + ll.x, *ring = smem + ll.ring;
+    float *lgs = smem + ll.lg, *nzs = smem + ll.nz;
+    int *abort_flag = reinterpret_cast<int *>(smem + ll.flag);
+    const int SW = ll.SW, NS = ll.NS;
+    const int O_H2 = U, O_GH1 = 2 * U, O_GH2 = 5 * U, O_V1 = 8 * U;   // offsets in a row's state
+    const int Uv = max(0, min(U, R - w * U));
+    const int UFv = max(0, min(UF, F - w * UF));
+    const int UCv = MOL ? 0 : max(0, min(UC, NC - w * UC));
+    const bool loader = wave == kLoaderWave;
+    const bool compute = !loader;
+    const int eng = wave * 4 + row;                    // dot engine of this lane (compute waves)
+    const size_t hop_sz = (size_t)2 * B * KA;
+    auto actp = [&](int hop, int t) { return a.act + hop * hop_sz + (size_t)(t & 1) * B * KA; };
+    auto flagp = [&](int hop) { return a.flags + (size_t)hop * kFlagSlots * kFlagStride; };
+    auto signal = [&](int hop, int t) {                // after every storing wave's vmcnt(0) + a barrier
+        if (tid == 0) __hip_atomic_store(flagp(hop) + w * kFlagStride, (unsigned)t + 1u, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    };
+    // LDS-DMA (sc1) of n floats (contiguous rows) from src into dst by the compute waves
+    auto dma = [&](float *dst, const float *src, int n) {
+        for (int c = wave * 256; c < n; c += kCompute * 4)
+            if (c + lane * 4 < n)
+                __builtin_amdgcn_global_load_lds(WRNN_GPTR(src + c + lane * 4), WRNN_LPTR(dst + c), 16, 0, 16);
+    };
+    // draws of step t for this workgroup's sampled rows → nz slot (t & 1); MoL turned into sampler terms
+    auto load_noise = [&](int t, int id, int nl) {
+        float *slot = nzs + (t & 1) * NS * ll.nkp;
+        for (int i = id; i < NS * NK; i += nl) {
+            const int sr = i / NK, k = i - sr * NK, b = w + sr * G;
+            if (b >= B) continue;
+            float v = a.noise ? a.noise[((size_t)t * a.Bt + a.b0 + b) * NK + k]
+                              : philox_noise(a.seed, (unsigned long long)(a.row0 + b), (uint32_t)t, (uint32_t)k, MOL);
+            if (MOL) v = mol_noise_term(v, k);
+            slot[sr * ll.nkp + k] = v;
+        }
+    };
+    auto load_terms = [&](int tl, int id, int nl) {
+        float4 *dst = reinterpret_cast<float4 *>(ring + (tl & 1) * B * NT);
+        const int q = NT / 4;
+        for (int i = id; i < B * q; i += nl) {
+            const int b = i / q, k = i - b * q;
+            dst[i] = reinterpret_cast<const float4 *>(a.terms + ((size_t)tl * B + b) * G * NT + (size_t)w * NT)[k];
+        }
+    };
+
+    // ---- prologue: weights, carried state, terms + draws of the first step
+    {
+        const float4 *src = reinterpret_cast<const float4 *>(a.slab + (size_t)w * s.total);
+        float4 *dst = reinterpret_cast<float4 *>(smem + ll.slab);
+        for (int i = tid; i < s.total / 4; i += kThreads) dst[i] = src[i];
+        const float *cs = a.state + (size_t)w * B * SW;
+        for (int i = tid; i < B * SW; i += kThreads) st[i] = a.t0 > 0 ? cs[i] : 0.0f;
+        const float *cx = a.state + (size_t)G * B * SW;
+        for (int i = tid; i < B; i += kThreads) xs[i] = a.t0 > 0 ? cx[i] : 0.0f;   // x = 0 (:196)
+        if (tid == 0) *abort_flag = 0;
+        load_terms(0, tid, kThreads);
+        load_noise(a.t0, tid, kThreads);
+    }
+    __syncthreads();
+
+    for (int tl = 0; tl < a.Lc; ++tl) {
+        const int t = a.t0 + tl;
+        const unsigned want = (unsigned)t + 1u;
+        const float *T = ring + (tl & 1) * B * NT;
+
+        // ---- GRU1 (:208-210), own units, every row
+        if (compute) {
+            float *h1o = actp(RH_H1, t);
+            for (int i = tid; i < B * Uv; i += kCompute) {
+                const int b = i / Uv, u = i - b * Uv, j = w * U + u;
+                const float x = xs[b];
+                const float *Tb = T + b * NT;
+                float *sb = st + b * SW;
+                float gi[3], gh[3];
+#pragma unroll
+                for (int g = 0; g < 3; ++g) {
+                    gi[g] = fmaf(x, S[s.q1 + g * U + u], Tb[g * U + u]) + S[s.bih1 + g * U + u];
+                    gh[g] = sb[O_GH1 + g * U + u] + S[s.bhh1 + g * U + u];
+                }
+                const float hn = gru_gate_math(gi[0], gi[1], gi[2], gh[0], gh[1], gh[2], sb[u]);
+                sb[u] = hn;
+                store_sc1(h1o + (size_t)b * R + j, hn);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        bar();
+        signal(RH_H1, t);
+        // loader: terms and draws of the next step, overlapping the hand-offs
+        if (loader && tl + 1 < a.Lc) {
+            load_terms(tl + 1, lane, 64);
+            load_noise(t + 1, lane, 64);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+
+        // ---- GRU2 (:212-214): W_ih2[:, :R]·h1 + P2 + x·Q2 on the critical path
+        if (wave == 0) wait_flags(flagp(RH_H1), G, want, a.ctl, a.timeout_ticks, t, RH_H1, abort_flag);
+        bar();
+        if (*abort_flag) return;
+        {
+            const float *src = actp(RH_H1, t);
+            float *h2o = actp(RH_H2, t);
+            for (int tb0 = 0; tb0 < B; tb0 += TB) {
+                const int nb = min(TB, B - tb0);
+                if (compute) {
+                    dma(tile, src + (size_t)tb0 * R, nb * R);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                bar();
+                if (compute)
+                    for (int it = eng; it < nb * Uv; it += kDotEngines) {
+                        const int bl = it / Uv, u = it - bl * Uv, b = tb0 + bl, j = w * U + u;
+                        const float3 d = row_dot3(S + s.wih2 + (0 * U + u) * R, S + s.wih2 + (1 * U + u) * R,
+                                                  S + s.wih2 + (2 * U + u) * R, tile + bl * R, R / 4, li);
+                        if (li == 0) {
+                            const float x = xs[b];
+                            const float *Tb = T + b * NT + 3 * U;
+                            float *sb = st + b * SW;
+                            const float dd[3] = {d.x, d.y, d.z};
+                            float gi[3], gh[3];
+#pragma unroll
+                            for (int g = 0; g < 3; ++g) {
+                                gi[g] = (dd[g] + fmaf(x, S[s.q2 + g * U + u], Tb[g * U + u])) + S[s.bih2 + g * U + u];
+                                gh[g] = sb[O_GH2 + g * U + u] + S[s.bhh2 + g * U + u];
+                            }
+                            const float hn = gru_gate_math(gi[0], gi[1], gi[2], gh[0], gh[1], gh[2], sb[O_H2 + u]);
+                            sb[O_H2 + u] = hn;
+                            store_sc1(h2o + (size_t)b * R + j, hn);
+                        }
+                    }
+                if (compute && tb0 + TB >= B) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                bar();
+            }
+            signal(RH_H2, t);
+            // off the critical path, on the h1 tiles: GH1_{t+1} = W_hh1·h1, V1h = W1[:, :R]·h1
+            for (int tb0 = 0; tb0 < B; tb0 += TB) {
+                const int nb = min(TB, B - tb0);
+                if (B > TB) {
+                    if (compute) {
+                        dma(tile, src + (size_t)tb0 * R, nb * R);
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    }
+                    bar();
+                }
+                if (compute) {
+                    for (int it = eng; it < nb * Uv; it += kDotEngines) {
+                        const int bl = it / Uv, u = it - bl * Uv, b = tb0 + bl;
+                        const float3 d = row_dot3(S + s.whh1 + (0 * U + u) * R, S + s.whh1 + (1 * U + u) * R,
+                                                  S + s.whh1 + (2 * U + u) * R, tile + bl * R, R / 4, li);
+                        if (li == 0) {
+                            float *sb = st + b * SW + O_GH1;
+                            sb[0 * U + u] = d.x;
+                            sb[1 * U + u] = d.y;
+                            sb[2 * U + u] = d.z;
+                        }
+                    }
+                    for (int it = eng; it < nb * UFv; it += kDotEngines) {
+                        const int bl = it / UFv, r = it - bl * UFv, b = tb0 + bl;
+                        const float v = row_dot(S + s.w1 + r * R, tile + bl * R, R / 4, li);
+                        if (li == 0) st[b * SW + O_V1 + r] = v;
+                    }
+                }
+                if (B > TB) bar();
+            }
+        }
+
+        // ---- fc1 (:216-218): W1[:, :R]·h2 + V1h + V1c + x·Q3, then GH2_{t+1} = W_hh2·h2
+        if (wave == 0) wait_flags(flagp(RH_H2), G, want, a.ctl, a.timeout_ticks, t, RH_H2, abort_flag);
+        bar();
+        if (*abort_flag) return;
+        {
+            const float *src = actp(RH_H2, t);
+            float *f1o = actp(RH_F1, t);
+            for (int tb0 = 0; tb0 < B; tb0 += TB) {
+                const int nb = min(TB, B - tb0);
+                if (compute) {
+                    dma(tile, src + (size_t)tb0 * R, nb * R);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                bar();
+                if (compute)
+                    for (int it = eng; it < nb * UFv; it += kDotEngines) {
+                        const int bl = it / UFv, r = it - bl * UFv, b = tb0 + bl, j = w * UF + r;
+                        const float d = row_dot(S + s.w1 + r * R, tile + bl * R, R / 4, li);
+                        if (li == 0) {
+                            const float v = d + (st[b * SW + O_V1 + r] +
+                                                 fmaf(xs[b], S[s.q3 + r], T[b * NT + 6 * U + r]));
+                            store_sc1(f1o + (size_t)b * F + j, v > 0.0f ? v : 0.0f);
+                        }
+                    }
+                if (compute && tb0 + TB >= B) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                bar();
+            }
+            signal(RH_F1, t);
+            for (int tb0 = 0; tb0 < B; tb0 += TB) {
+                const int nb = min(TB, B - tb0);
+                if (B > TB) {
+                    if (compute) {
+                        dma(tile, src + (size_t)tb0 * R, nb * R);
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    }
+                    bar();
+                }
+                if (compute)
+                    for (int it = eng; it < nb * Uv; it += kDotEngines) {
+                        const int bl = it / Uv, u = it - bl * Uv, b = tb0 + bl;
+                        const float3 d = row_dot3(S + s.whh2 + (0 * U + u) * R, S + s.whh2 + (1 * U + u) * R,
+                                                  S + s.whh2 + (2 * U + u) * R, tile + bl * R, R / 4, li);
+                        if (li == 0) {
+                            float *sb = st + b * SW + O_GH2;
+                            sb[0 * U + u] = d.x;
+                            sb[1 * U + u] = d.y;
+                            sb[2 * U + u] = d.z;
+                        }
+                    }
+                if (B > TB) bar();
+            }
+        }
+
+        // ---- fc2 (:220-221): W2[:, :F]·f1 + V2
+        if (wave == 0) wait_flags(flagp(RH_F1), G, want, a.ctl, a.timeout_ticks, t, RH_F1, abort_flag);
+        bar();
+        if (*abort_flag) return;
+        {
+            const float *src = actp(RH_F1, t);
+            float *f2o = actp(RH_F2, t);
+            for (int tb0 = 0; tb0 < B; tb0 += TB) {
+                const int nb = min(TB, B - tb0);
+                if (compute) {
+                    dma(tile, src + (size_t)tb0 * F, nb * F);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                bar();
+                if (compute)
+                    for (int it = eng; it < nb * UFv; it += kDotEngines) {
+                        const int bl = it / UFv, r = it - bl * UFv, b = tb0 + bl, j = w * UF + r;
+                        const float d = row_dot(S + s.w2 + r * F, tile + bl * F, F / 4, li);
+                        if (li == 0) {
+                            const float v = d + T[b * NT + 6 * U + UF + r];
+                            store_sc1(f2o + (size_t)b * F + j, v > 0.0f ? v : 0.0f);
+                        }
+                    }
+                if (compute && tb0 + TB >= B) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                bar();
+            }
+            signal(RH_F2, t);
+        }
+
+        // ---- fc3 (:223) + sampling (:225-237), distributed by row
+        const bool sampler = w < B;
+        if (!MOL) {   // fc3 rows are distributed: logits hand-off first
+            if (wave == 0) wait_flags(flagp(RH_F2), G, want, a.ctl, a.timeout_ticks, t, RH_F2, abort_flag);
+            bar();
+            if (*abort_flag) return;
+            const float *src = actp(RH_F2, t);
+            float *lgo = actp(RH_LG, t);
+            for (int tb0 = 0; tb0 < B; tb0 += TB) {
+                const int nb = min(TB, B - tb0);
+                if (compute) {
+                    dma(tile, src + (size_t)tb0 * F, nb * F);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                bar();
+                if (compute)
+                    for (int it = eng; it < nb * UCv; it += kDotEngines) {
+                        const int bl = it / UCv, r = it - bl * UCv, b = tb0 + bl, j = w * UC + r;
+                        const float d = row_dot(S + s.w3 + r * F, tile + bl * F, F / 4, li);
+                        if (li == 0) store_sc1(lgo + (size_t)b * NC + j, d + S[s.b3 + r]);
+                    }
+                if (compute && tb0 + TB >= B) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                bar();
+            }
+            signal(RH_LG, t);
+        }
+        if (sampler) {
+            const int hop = MOL ? RH_F2 : RH_LG;
+            const int K = MOL ? F : NC;
+            if (wave == 0) wait_flags(flagp(hop), G, want, a.ctl, a.timeout_ticks, t, hop, abort_flag);
+            bar();
+            if (*abort_flag) return;
+            const float *src = actp(hop, t);
+            if (compute) {
+                for (int sr = 0; sr < NS && w + sr * G < B; ++sr) dma(tile + sr * ll.KT, src + (size_t)(w + sr * G) * K, K);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            bar();
+            if (MOL) {   // the 30 head rows (replicated in every workgroup) against f2 of each sampled row
+                if (compute)
+                    for (int sr = 0; sr < NS && w + sr * G < B; ++sr)
+                        for (int c0 = eng; c0 < NC; c0 += 2 * kDotEngines) {
+                            const int ca = c0, cb = min(c0 + kDotEngines, NC - 1);
+                            const float2 v = row_dot2(S + s.w3 + ca * F, S + s.w3 + cb * F, tile + sr * ll.KT, F / 4, li);
+                            if (li == 0) lgs[sr * ll.ncp + ca] = v.x + S[s.b3 + ca];
+                            if (li == 0 && c0 + kDotEngines < NC) lgs[sr * ll.ncp + cb] = v.y + S[s.b3 + cb];
+                        }
+                bar();
+            }
+            if (compute)
+                for (int sr = wave; sr < NS; sr += kWaves) {
+                    const int b = w + sr * G;
+                    if (b >= B) break;
+                    const float *u = nzs + (t & 1) * NS * ll.nkp + sr * ll.nkp;
+                    float x;
+                    int label = 0;
+                    if (MOL) {
+                        x = mol_sample(lgs + sr * ll.ncp, u, lane);
+                    } else {
+                        label = raw_sample<kClsPerLaneMax>(tile + sr * ll.KT, u, NC, lane);
+                        x = label_to_x(label, NC);
+                    }
+                    if (lane < kXReps) publish(a.xg + (size_t)lane * kXRepStride + b, want, x);
+                    if (lane == 0) {
+                        const size_t o = (size_t)(a.b0 + b) * a.L + t;
+                        a.out[o] = x;
+                        if (a.labels) a.labels[o] = label;
+                    }
+                }
+        }
+
+        // ---- x of every row → next step's GRU1
+        if (wave == 0)
+            gather<kRowsMax / 64, 64>(a.xg + (size_t)(w % kXReps) * kXRepStride, 0, B, B, want, a.ctl,
+                                      a.timeout_ticks, t, kRowsHops, abort_flag, lane,
+                                      [&](int, int j, float v) { xs[j] = v; });
+        bar();
+        if (*abort_flag) return;
+    }
+
+    // carried state for the next launch of this generate()
+    {
+        float *cs = a.state + (size_t)w * B * SW;
+        for (int i = tid; i < B * SW; i += kThreads) cs[i] = st[i];
+        if (w == 0)
+            for (int i = tid; i < B; i += kThreads) a.state[(size_t)G * B * SW + i] = xs[i];
+    }
+}
+
+// --------------------------------------------------------------- conditioning terms input
+// X[m][0..KX) for m = tl·B + b:  [cI (R, written by ci_gemm) | a2 a3 a4 (3A) | 1 | 0 0 0]
+__global__ void pack_terms_input_kernel(const float *__restrict__ cond, int CD, int Bt, int b0, int B, int t0,
+                                        int M, int feat, int A, int R, int KX, float *__restrict__ X) {
+    const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (m >= M) return;
+    const int tl = m / B, b = m - tl * B;
+    const float *src = cond + ((size_t)(t0 + tl) * Bt + b0 + b) * CD + feat + A;
+    float *dst = X + (size_t)m * KX + R;
+    for (int k = threadIdx.x & 63; k < KX - R; k += 64) dst[k] = k < 3 * A ? src[k] : (k == 3 * A ? 1.0f : 0.0f);
+}
+
+hipError_t launch_pack_terms_input(const float *cond, int CD, int Bt, int b0, int B, int t0, int Lc, int feat, int A,
+                                   int R, int KX, float *X, hipStream_t st) {
+    const int M = Lc * B;
+    hipLaunchKernelGGL(pack_terms_input_kernel, dim3((M + 3) / 4), dim3(256), 0, st, cond, CD, Bt, b0, B, t0, M, feat,
+                       A, R, KX, X);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------ host launchers
+hipError_t launch_rows(const RowsArgs &a, size_t lds_bytes, hipStream_t st) {
+    const void *k = a.mol ? (const void *)fatchord_rows_kernel<true> : (const void *)fatchord_rows_kernel<false>;
+    RowsArgs args = a;
+    void *params[] = {&args};
+    return hipLaunchKernel(k, dim3(a.G), dim3(kThreads), params, lds_bytes, st);
+}
+
+hipError_t prepare_rows_kernel(int max_lds_bytes) {
+    for (const void *k : {(const void *)fatchord_rows_kernel<true>, (const void *)fatchord_rows_kernel<false>}) {
+        hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds_bytes);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t rows_occupancy(int *blocks_per_cu, size_t lds_bytes) {
+    int a = 0, b = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, fatchord_rows_kernel<true>, kThreads, lds_bytes);
+    if (e != hipSuccess) return e;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, fatchord_rows_kernel<false>, kThreads, lds_bytes);
+    *blocks_per_cu = a < b ? a : b;
+    return e;
+}
+
+}  // namespace wrnn
