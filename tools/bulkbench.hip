@@ -18,7 +18,7 @@ __global__ __launch_bounds__(kThreads) void bulk(float *buf, unsigned *ctr, unsi
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     float acc = 0.0f;
     for (int r = 0; r < rounds; ++r) {
-        float *cur = buf + (size_t)(r & 1) * B * R;
+        float *cur = buf + (size_t)(LD == 2 ? r : (r & 1)) * B * R;
         // publish: B rows × U values of this workgroup (wave 1)
         if (wave == 1)
             for (int i = lane; i < B * U; i += 64) {
@@ -69,10 +69,15 @@ __global__ __launch_bounds__(kThreads) void bulk(float *buf, unsigned *ctr, unsi
                     if (i < B * R / 4) reinterpret_cast<float4 *>(act)[i] = v[k];
                 }
             }
-        } else {
+        } else if (LD == 1) {
             for (int c = wave * 256; c < B * R; c += kThreads * 4)
                 __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(cur + c + lane * 4),
                                                  (__attribute__((address_space(3))) void *)(act + c), 16, 0, 16);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {   // fresh address every round: plain (L2-cached) DMA
+            for (int c = wave * 256; c < B * R; c += kThreads * 4)
+                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(cur + c + lane * 4),
+                                                 (__attribute__((address_space(3))) void *)(act + c), 16, 0, 0);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         __syncthreads();
@@ -95,7 +100,8 @@ void run(int G, int B) {
     float *buf, *sink;
     unsigned *ctr, *flags;
     unsigned long long *out;
-    hipMalloc(&buf, 2ull * B * R * 4);
+    const size_t nbuf = (LD == 2 ? 2000ull : 2ull) * B * R;
+    hipMalloc(&buf, nbuf * 4);
     hipMalloc(&ctr, kReps * kRepStride * 4);
     hipMalloc(&flags, G * 64);
     hipMalloc(&out, G * 8);
@@ -103,7 +109,7 @@ void run(int G, int B) {
     hipMemset(ctr, 0, kReps * kRepStride * 4);
     hipMemset(flags, 0, G * 64);
     hipMemset(sink, 0, (G + 1) * 4);
-    hipMemset(buf, 0xFF, 2ull * B * R * 4);
+    hipMemset(buf, 0xFF, nbuf * 4);
     const int rounds = 2000;
     hipFuncSetAttribute((const void *)bulk<SIG, LD, V>, hipFuncAttributeMaxDynamicSharedMemorySize, B * R * 4);
     hipLaunchKernelGGL((bulk<SIG, LD, V>), dim3(G), dim3(kThreads), B * R * 4, 0, buf, ctr, flags, B, rounds, out, sink);
@@ -114,18 +120,17 @@ void run(int G, int B) {
     hipMemcpy(&bad, sink, 4, hipMemcpyDeviceToHost);
     unsigned long long mx = 0;
     for (int i = 0; i < G; ++i) mx = h[i] > mx ? h[i] : mx;
-    printf("%s %s%s G=%3d B=%3d: %.3f us/round  stale=%u  %s\n", SIG == 0 ? "counter" : "flags  ", LD == 0 ? "regs" : "dma ", V ? " verify" : "", G, B,
+    printf("%s %s%s G=%3d B=%3d: %.3f us/round  stale=%u  %s\n", SIG == 0 ? "counter" : "flags  ", LD == 0 ? "regs" : LD == 1 ? "dma " : "fresh", V ? " verify" : "", G, B,
            mx * 10e-3 / rounds, bad, hipGetErrorString(e));
     fflush(stdout);
     hipFree(buf); hipFree(ctr); hipFree(flags); hipFree(out); hipFree(sink);
 }
 
 int main() {
-    for (int B : {1, 4, 16, 32, 64, 128}) {
-        run<0, 1, 0>(256, B);
-        run<1, 0, 0>(256, B);
+    for (int B : {1, 4, 16, 32, 64}) {
         run<1, 1, 0>(256, B);
-        run<1, 1, 1>(256, B);
+        run<1, 2, 0>(256, B);
+        run<1, 2, 1>(256, B);
     }
     return 0;
 }

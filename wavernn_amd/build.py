@@ -29,12 +29,28 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(s) <= t for s in SOURCES + HEADERS)
 
 
+# per-source extra flags: the multi-row kernel's register-blocked dots are plain fp32 FMAs; the
+# SLP vectorizer packs them into v_pk_fma_f32 with operand-shuffling moves and mid-loop LDS
+# waits (measured 4x slower jobs on gfx950)
+EXTRA_FLAGS = {"fatchord_rows.hip": ["-fno-slp-vectorize"]}
+
+
 def build(force: bool = False, verbose: bool = True) -> str:
     if not force and up_to_date():
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-I" + os.path.join(REPO, "include"), *SOURCES, "-lrocblas", "-o", OUT + ".tmp"]
+    objdir = os.path.join(os.path.dirname(OUT), "obj")
+    os.makedirs(objdir, exist_ok=True)
+    common = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-I" + os.path.join(REPO, "include")]
+    objs = []
+    for src in SOURCES:
+        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        cmd = common + EXTRA_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        objs.append(obj)
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-lrocblas", "-o", OUT + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -322,6 +322,22 @@ hipError_t ensure(T *&p, size_t &cap, size_t n) {
     return e;
 }
 
+// WRNN_DEBUG_FILE (default wrnn_stamps.bin): int32 header {G, steps, kStamps}, then the stamps
+int dump_stamps(wrnn_t *h, unsigned *d_dbg, int dbg_steps, hipStream_t st) {
+    std::vector<unsigned> host((size_t)h->G * dbg_steps * kStamps);
+    HIP_TRY(h, hipStreamSynchronize(st));
+    HIP_TRY(h, hipMemcpy(host.data(), d_dbg, host.size() * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(h, hipFree(d_dbg));
+    const char *path = std::getenv("WRNN_DEBUG_FILE");
+    if (FILE *f = std::fopen(path ? path : "wrnn_stamps.bin", "wb")) {
+        int hdr[3] = {h->G, dbg_steps, kStamps};
+        std::fwrite(hdr, sizeof(hdr), 1, f);
+        std::fwrite(host.data(), 4, host.size(), f);
+        std::fclose(f);
+    }
+    return WRNN_OK;
+}
+
 int grow(wrnn_t *h, float *&p, size_t &cap, size_t n) {
     HIP_TRY(h, ensure(p, cap, n));
     return WRNN_OK;
@@ -343,6 +359,13 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
     const char *mb_env = std::getenv("WRNN_TERMS_MB");
     const double budget = (mb_env ? std::atof(mb_env) : 2048.0) * (1 << 20) / 4.0;   // floats
     const float one = 1.0f, zero = 0.0f;
+    const char *dbg_env = std::getenv("WRNN_DEBUG_STAMPS");
+    const int dbg_steps = dbg_env ? std::min(L, std::atoi(dbg_env)) : 0;
+    unsigned *d_dbg = nullptr;
+    if (dbg_steps > 0) {
+        HIP_TRY(h, hipMalloc(&d_dbg, (size_t)h->G * dbg_steps * kStamps * 4));
+        HIP_TRY(h, hipMemsetAsync(d_dbg, 0, (size_t)h->G * dbg_steps * kStamps * 4, st));
+    }
     for (int b0 = 0; b0 < B;) {
         int Bl = std::min(B - b0, kRowsMax);
         while (Bl > 1 && rows_tile_for(*h, Bl) == 0) --Bl;
@@ -400,10 +423,13 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
             a.TB = TB;
             a.KA = h->KA;
             a.s = h->rs;
+            a.dbg = (b0 == 0 && t0 == 0) ? d_dbg : nullptr;
+            a.dbg_steps = std::min(dbg_steps, Lc);
             HIP_TRY(h, launch_rows(a, rows_lds_bytes(*h, Bl, TB), st));
         }
         b0 += Bl;
     }
+    if (d_dbg) return dump_stamps(h, d_dbg, dbg_steps, st);
     return WRNN_OK;
 }
 
@@ -477,19 +503,7 @@ int generate_latency(wrnn_t *h, const float *cond, int B, int L, const float *no
         a.dbg_steps = dbg_steps;
         HIP_TRY(h, launch_loop(a, lds_bytes_for(*h, Bc), st));
     }
-    if (d_dbg) {
-        std::vector<unsigned> host((size_t)h->G * dbg_steps * kStamps);
-        HIP_TRY(h, hipStreamSynchronize(st));
-        HIP_TRY(h, hipMemcpy(host.data(), d_dbg, host.size() * 4, hipMemcpyDeviceToHost));
-        HIP_TRY(h, hipFree(d_dbg));
-        const char *path = std::getenv("WRNN_DEBUG_FILE");
-        if (FILE *f = std::fopen(path ? path : "wrnn_stamps.bin", "wb")) {
-            int hdr[3] = {h->G, dbg_steps, kStamps};
-            std::fwrite(hdr, sizeof(hdr), 1, f);
-            std::fwrite(host.data(), 4, host.size(), f);
-            std::fclose(f);
-        }
-    }
+    if (d_dbg) return dump_stamps(h, d_dbg, dbg_steps, st);
     return WRNN_OK;
 }
 

@@ -54,6 +54,8 @@ struct RowsArgs {
     int B, Bt, b0;                // rows in this launch, rows in out/noise, first row
     int R, F, A, NC, NK, mol, U, UF, UC, G, NT, TB, KA;
     RowsSlab s;
+    unsigned *dbg;                // WRNN_DEBUG_STAMPS: [G][dbg_steps][kStamps] s_memrealtime per stage
+    int dbg_steps;
 };
 
 struct RowsLds {
@@ -70,10 +72,10 @@ __host__ __device__ inline RowsLds rows_lds_layout(int slab_total, int B, int TB
     l.ncp = round4(NC);
     l.nkp = round4(NK);
     const int NT = rows_terms(U, UF);
-    const int tr = TB > l.NS ? TB : l.NS;
+    const int tr = 2 * TB > l.NS ? 2 * TB : l.NS;   // two tiles (double-buffered DMA)
     int o = 0;
     l.slab = o;  o += round4(slab_total);
-    l.tile = o;  o += tr * l.KT;               // one tile of activation rows
+    l.tile = o;  o += tr * l.KT;
     l.st = o;    o += B * l.SW;
     l.x = o;     o += round4(B);
     l.ring = o;  o += 2 * B * NT;              // terms of steps t, t+1

@@ -61,12 +61,14 @@ __device__ __forceinline__ void store_sc1(float *p, float v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <bool MOL>
+// kRF = 512 instantiates the shipped dims (rnn_dims = fc_dims = 512) with compile-time dot
+// lengths; 0 = runtime dims.
+template <bool MOL, int kRF>
 __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, row = lane >> 4;
     const int w = blockIdx.x;
-    const int R = a.R, F = a.F, NC = a.NC, NK = a.NK, U = a.U, UF = a.UF, UC = a.UC, G = a.G, B = a.B;
+    const int R = kRF ? kRF : a.R, F = kRF ? kRF : a.F, NC = a.NC, NK = a.NK, U = a.U, UF = a.UF, UC = a.UC, G = a.G, B = a.B;
     const int NT = a.NT, TB = a.TB, KA = a.KA;
     const RowsLds ll = rows_lds_layout(a.s.total, B, TB, R, F, NC, NK, U, UF, G);
     const RowsSlab &s = a.s;
@@ -83,15 +85,21 @@ __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
     const bool compute = !loader;
     const int eng = wave * 4 + row;                    // dot engine of this lane (compute waves)
     const size_t hop_sz = (size_t)2 * B * KA;
+    unsigned *dbgw = a.dbg ? a.dbg + (size_t)w * a.dbg_steps * kStamps : nullptr;
+#define RSTAMP(k)                                                                                   \
+    do {                                                                                            \
+        if (dbgw && tid == 0 && tl < a.dbg_steps)                                                  \
+            dbgw[(size_t)tl * kStamps + (k)] = (unsigned)__builtin_amdgcn_s_memrealtime();          \
+    } while (0)
     auto actp = [&](int hop, int t) { return a.act + hop * hop_sz + (size_t)(t & 1) * B * KA; };
     auto flagp = [&](int hop) { return a.flags + (size_t)hop * kFlagSlots * kFlagStride; };
     auto signal = [&](int hop, int t) {                // after every storing wave's vmcnt(0) + a barrier
         if (tid == 0) __hip_atomic_store(flagp(hop) + w * kFlagStride, (unsigned)t + 1u, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT);
     };
-    // LDS-DMA (sc1) of n floats (contiguous rows) from src into dst by the compute waves
+    // LDS-DMA (sc1) of n floats (contiguous rows) from src into dst, issued by the loader wave
     auto dma = [&](float *dst, const float *src, int n) {
-        for (int c = wave * 256; c < n; c += kCompute * 4)
+        for (int c = 0; c < n; c += 256)
             if (c + lane * 4 < n)
                 __builtin_amdgcn_global_load_lds(WRNN_GPTR(src + c + lane * 4), WRNN_LPTR(dst + c), 16, 0, 16);
     };
@@ -131,10 +139,66 @@ __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
     }
     __syncthreads();
 
+    // ---- matvec stages.  A stage reads one activation matrix [B][K] tile by tile (LDS-DMA,
+    // double-buffered: tile k+1 lands while tile k is computed) and runs a job list on each
+    // tile: a job is one 16-lane engine's block of weight rows × up to kNX activation rows.
+    // Critical and off-critical jobs of a stage share the list (critical ones first), so the
+    // 16 engines stay busy and each activation row is read from HBM once per stage.
+    constexpr int kNX = 4;
+    auto tbuf = [&](int k) { return tile + (k & 1) * TB * ll.KT; };
+    int t_cur = a.t0;                                  // step the stage driver works on
+#define RSTAMP_T(k)                                                                                 \
+    do {                                                                                            \
+        if (dbgw && tid == 0 && t_cur - a.t0 < a.dbg_steps)                                        \
+            dbgw[(size_t)(t_cur - a.t0) * kStamps + (k)] = (unsigned)__builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+    // Stage driver.  The loader wave polls the hop's flags and issues every tile DMA, waiting
+    // only for its own loads; the compute waves run the jobs and store their outputs (sc1), and
+    // drain those stores once, before the stage's signal.  Returns false on abort.
+    auto run_stage = [&](int hop, int K, auto &&jobs) -> bool {
+        const float *src = actp(hop, t_cur);
+        const int ntiles = (B + TB - 1) / TB;
+        if (loader) {
+            wait_flags(flagp(hop), G, (unsigned)t_cur + 1u, a.ctl, a.timeout_ticks, t_cur, hop, abort_flag);
+            if (!*abort_flag) dma(tbuf(0), src, min(TB, B) * K);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        bar();
+        if (hop == RH_H2) RSTAMP_T(13);
+        if (*abort_flag) return false;
+        for (int k = 0; k < ntiles; ++k) {
+            const int tb0 = k * TB, nb = min(TB, B - tb0);
+            if (loader && k + 1 < ntiles) {
+                dma(tbuf(k + 1), src + (size_t)(tb0 + TB) * K, min(TB, B - tb0 - TB) * K);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            if (compute) jobs(tbuf(k), tb0, nb);
+            bar();
+        }
+        if (hop == RH_H2) RSTAMP_T(14);
+        if (compute) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bar();
+        if (hop == RH_H2) RSTAMP_T(15);
+        return true;
+    };
+    // job helpers: unit blocks (3 gate rows of unit u) and fc blocks (2 rows r0, r0+1)
+    // (lane li of the engine ends up with activation row li & 3 of the block)
+    constexpr int KI = kRF / 64;                       // chunks per lane when R = F = kRF
+    auto unit_block = [&](int wbase, const float *x, int K, int nx, int u, float (&acc)[3]) {
+        bdot4<3, KI>(S + wbase + u * K, U * K, x, K, nx, K / 4, li, acc);
+    };
+    auto fc_block = [&](int wbase, int nrows, const float *x, int K, int nx, int r0, float (&acc)[2]) {
+        const int r1 = r0 + 1 < nrows ? r0 + 1 : r0;
+        bdot4<2, KI>(S + wbase + r0 * K, (r1 - r0) * K, x, K, nx, K / 4, li, acc);
+    };
+    const int nUF2 = (UFv + 1) / 2, nUC2 = (UCv + 1) / 2;
+
     for (int tl = 0; tl < a.Lc; ++tl) {
         const int t = a.t0 + tl;
+        t_cur = t;
         const unsigned want = (unsigned)t + 1u;
         const float *T = ring + (tl & 1) * B * NT;
+        RSTAMP(0);
 
         // ---- GRU1 (:208-210), own units, every row
         if (compute) {
@@ -158,204 +222,162 @@ __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
         }
         bar();
         signal(RH_H1, t);
-        // loader: terms and draws of the next step, overlapping the hand-offs
-        if (loader && tl + 1 < a.Lc) {
-            load_terms(tl + 1, lane, 64);
-            load_noise(t + 1, lane, 64);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+        RSTAMP(1);
 
-        // ---- GRU2 (:212-214): W_ih2[:, :R]·h1 + P2 + x·Q2 on the critical path
-        if (wave == 0) wait_flags(flagp(RH_H1), G, want, a.ctl, a.timeout_ticks, t, RH_H1, abort_flag);
-        bar();
-        if (*abort_flag) return;
+        // ---- GRU2 (:212-214): W_ih2[:, :R]·h1 + P2 + x·Q2 → h2; with GH1_{t+1} = W_hh1·h1 and
+        // V1h = W1[:, :R]·h1 (the h1 part of fc1's input x = x_I + h1 + h2)
+        RSTAMP(2);
         {
-            const float *src = actp(RH_H1, t);
             float *h2o = actp(RH_H2, t);
-            for (int tb0 = 0; tb0 < B; tb0 += TB) {
-                const int nb = min(TB, B - tb0);
-                if (compute) {
-                    dma(tile, src + (size_t)tb0 * R, nb * R);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                }
-                bar();
-                if (compute)
-                    for (int it = eng; it < nb * Uv; it += kDotEngines) {
-                        const int bl = it / Uv, u = it - bl * Uv, b = tb0 + bl, j = w * U + u;
-                        const float3 d = row_dot3(S + s.wih2 + (0 * U + u) * R, S + s.wih2 + (1 * U + u) * R,
-                                                  S + s.wih2 + (2 * U + u) * R, tile + bl * R, R / 4, li);
-                        if (li == 0) {
-                            const float x = xs[b];
-                            const float *Tb = T + b * NT + 3 * U;
+            const bool ok = run_stage(RH_H1, R, [&](const float *tl_, int tb0, int nb) {
+                // job types padded to multiples of 4 so the 4 engines of a wave never diverge
+                const int nbb = (nb + kNX - 1) / kNX, n1 = Uv * nbb, nj1 = round4(n1), nj2 = 2 * nj1;
+                const int nj3 = nj2 + nUF2 * nbb;
+                for (int jb = eng; jb < nj3; jb += kDotEngines) {
+                    if (jb < nj2) {
+                        const int jj = jb < nj1 ? jb : jb - nj1, u = jj % Uv, bb = jj / Uv;
+                        if (jj >= n1) continue;
+                        const int nx = min(kNX, nb - bb * kNX), b = tb0 + bb * kNX + li;
+                        float acc[3];
+                        unit_block(jb < nj1 ? s.wih2 : s.whh1, tl_ + bb * kNX * R, R, nx, u, acc);
+                        if (li < nx) {
                             float *sb = st + b * SW;
-                            const float dd[3] = {d.x, d.y, d.z};
-                            float gi[3], gh[3];
+                            if (jb < nj1) {   // GRU2 gates of (b, u)
+                                const float x = xs[b];
+                                const float *Tb = T + b * NT + 3 * U;
+                                float gi[3], gh[3];
 #pragma unroll
-                            for (int g = 0; g < 3; ++g) {
-                                gi[g] = (dd[g] + fmaf(x, S[s.q2 + g * U + u], Tb[g * U + u])) + S[s.bih2 + g * U + u];
-                                gh[g] = sb[O_GH2 + g * U + u] + S[s.bhh2 + g * U + u];
+                                for (int g = 0; g < 3; ++g) {
+                                    gi[g] = (acc[g] + fmaf(x, S[s.q2 + g * U + u], Tb[g * U + u])) +
+                                            S[s.bih2 + g * U + u];
+                                    gh[g] = sb[O_GH2 + g * U + u] + S[s.bhh2 + g * U + u];
+                                }
+                                const float hn = gru_gate_math(gi[0], gi[1], gi[2], gh[0], gh[1], gh[2], sb[O_H2 + u]);
+                                sb[O_H2 + u] = hn;
+                                store_sc1(h2o + (size_t)b * R + w * U + u, hn);
+                            } else {          // GH1 of the next step
+#pragma unroll
+                                for (int g = 0; g < 3; ++g) sb[O_GH1 + g * U + u] = acc[g];
                             }
-                            const float hn = gru_gate_math(gi[0], gi[1], gi[2], gh[0], gh[1], gh[2], sb[O_H2 + u]);
-                            sb[O_H2 + u] = hn;
-                            store_sc1(h2o + (size_t)b * R + j, hn);
+                        }
+                    } else {                  // V1h rows r0, r0+1
+                        const int jj = jb - nj2, r0 = 2 * (jj % nUF2), bb = jj / nUF2;
+                        const int nx = min(kNX, nb - bb * kNX), b = tb0 + bb * kNX + li;
+                        float acc[2];
+                        fc_block(s.w1, UFv, tl_ + bb * kNX * R, R, nx, r0, acc);
+                        if (li < nx) {
+                            st[b * SW + O_V1 + r0] = acc[0];
+                            if (r0 + 1 < UFv) st[b * SW + O_V1 + r0 + 1] = acc[1];
                         }
                     }
-                if (compute && tb0 + TB >= B) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                bar();
-            }
+                }
+            });
+            if (!ok) return;
             signal(RH_H2, t);
-            // off the critical path, on the h1 tiles: GH1_{t+1} = W_hh1·h1, V1h = W1[:, :R]·h1
-            for (int tb0 = 0; tb0 < B; tb0 += TB) {
-                const int nb = min(TB, B - tb0);
-                if (B > TB) {
-                    if (compute) {
-                        dma(tile, src + (size_t)tb0 * R, nb * R);
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    }
-                    bar();
-                }
-                if (compute) {
-                    for (int it = eng; it < nb * Uv; it += kDotEngines) {
-                        const int bl = it / Uv, u = it - bl * Uv, b = tb0 + bl;
-                        const float3 d = row_dot3(S + s.whh1 + (0 * U + u) * R, S + s.whh1 + (1 * U + u) * R,
-                                                  S + s.whh1 + (2 * U + u) * R, tile + bl * R, R / 4, li);
-                        if (li == 0) {
-                            float *sb = st + b * SW + O_GH1;
-                            sb[0 * U + u] = d.x;
-                            sb[1 * U + u] = d.y;
-                            sb[2 * U + u] = d.z;
-                        }
-                    }
-                    for (int it = eng; it < nb * UFv; it += kDotEngines) {
-                        const int bl = it / UFv, r = it - bl * UFv, b = tb0 + bl;
-                        const float v = row_dot(S + s.w1 + r * R, tile + bl * R, R / 4, li);
-                        if (li == 0) st[b * SW + O_V1 + r] = v;
-                    }
-                }
-                if (B > TB) bar();
-            }
+            RSTAMP(3);
         }
 
-        // ---- fc1 (:216-218): W1[:, :R]·h2 + V1h + V1c + x·Q3, then GH2_{t+1} = W_hh2·h2
-        if (wave == 0) wait_flags(flagp(RH_H2), G, want, a.ctl, a.timeout_ticks, t, RH_H2, abort_flag);
-        bar();
-        if (*abort_flag) return;
+        // ---- fc1 (:216-218): W1[:, :R]·h2 + V1h + V1c + x·Q3 → f1; with GH2_{t+1} = W_hh2·h2
+        RSTAMP(4);
         {
-            const float *src = actp(RH_H2, t);
             float *f1o = actp(RH_F1, t);
-            for (int tb0 = 0; tb0 < B; tb0 += TB) {
-                const int nb = min(TB, B - tb0);
-                if (compute) {
-                    dma(tile, src + (size_t)tb0 * R, nb * R);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                }
-                bar();
-                if (compute)
-                    for (int it = eng; it < nb * UFv; it += kDotEngines) {
-                        const int bl = it / UFv, r = it - bl * UFv, b = tb0 + bl, j = w * UF + r;
-                        const float d = row_dot(S + s.w1 + r * R, tile + bl * R, R / 4, li);
-                        if (li == 0) {
-                            const float v = d + (st[b * SW + O_V1 + r] +
-                                                 fmaf(xs[b], S[s.q3 + r], T[b * NT + 6 * U + r]));
-                            store_sc1(f1o + (size_t)b * F + j, v > 0.0f ? v : 0.0f);
-                        }
+            const bool ok = run_stage(RH_H2, R, [&](const float *tl_, int tb0, int nb) {
+                const int nbb = (nb + kNX - 1) / kNX, n1 = nUF2 * nbb, nj1 = round4(n1), nj2 = nj1 + Uv * nbb;
+                for (int jb = eng; jb < nj2; jb += kDotEngines) {
+                    if (jb < nj1) {
+                        if (jb >= n1) continue;
+                        const int r0 = 2 * (jb % nUF2), bb = jb / nUF2;
+                        const int nx = min(kNX, nb - bb * kNX), b = tb0 + bb * kNX + li;
+                        float acc[2];
+                        fc_block(s.w1, UFv, tl_ + bb * kNX * R, R, nx, r0, acc);
+                        if (li < nx)
+#pragma unroll
+                            for (int q = 0; q < 2; ++q) {
+                                const int r = r0 + q;
+                                if (r >= UFv) break;
+                                const float v = acc[q] +
+                                                (st[b * SW + O_V1 + r] + fmaf(xs[b], S[s.q3 + r], T[b * NT + 6 * U + r]));
+                                store_sc1(f1o + (size_t)b * F + w * UF + r, v > 0.0f ? v : 0.0f);
+                            }
+                    } else {
+                        const int jj = jb - nj1, u = jj % Uv, bb = jj / Uv;
+                        const int nx = min(kNX, nb - bb * kNX), b = tb0 + bb * kNX + li;
+                        float acc[3];
+                        unit_block(s.whh2, tl_ + bb * kNX * R, R, nx, u, acc);
+                        if (li < nx)
+#pragma unroll
+                            for (int g = 0; g < 3; ++g) st[b * SW + O_GH2 + g * U + u] = acc[g];
                     }
-                if (compute && tb0 + TB >= B) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                bar();
-            }
+                }
+            });
+            if (!ok) return;
             signal(RH_F1, t);
-            for (int tb0 = 0; tb0 < B; tb0 += TB) {
-                const int nb = min(TB, B - tb0);
-                if (B > TB) {
-                    if (compute) {
-                        dma(tile, src + (size_t)tb0 * R, nb * R);
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    }
-                    bar();
-                }
-                if (compute)
-                    for (int it = eng; it < nb * Uv; it += kDotEngines) {
-                        const int bl = it / Uv, u = it - bl * Uv, b = tb0 + bl;
-                        const float3 d = row_dot3(S + s.whh2 + (0 * U + u) * R, S + s.whh2 + (1 * U + u) * R,
-                                                  S + s.whh2 + (2 * U + u) * R, tile + bl * R, R / 4, li);
-                        if (li == 0) {
-                            float *sb = st + b * SW + O_GH2;
-                            sb[0 * U + u] = d.x;
-                            sb[1 * U + u] = d.y;
-                            sb[2 * U + u] = d.z;
-                        }
-                    }
-                if (B > TB) bar();
-            }
+            RSTAMP(6);
         }
 
-        // ---- fc2 (:220-221): W2[:, :F]·f1 + V2
-        if (wave == 0) wait_flags(flagp(RH_F1), G, want, a.ctl, a.timeout_ticks, t, RH_F1, abort_flag);
-        bar();
-        if (*abort_flag) return;
+        // ---- fc2 (:220-221): W2[:, :F]·f1 + V2 → f2
+        RSTAMP(7);
         {
-            const float *src = actp(RH_F1, t);
             float *f2o = actp(RH_F2, t);
-            for (int tb0 = 0; tb0 < B; tb0 += TB) {
-                const int nb = min(TB, B - tb0);
-                if (compute) {
-                    dma(tile, src + (size_t)tb0 * F, nb * F);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                }
-                bar();
-                if (compute)
-                    for (int it = eng; it < nb * UFv; it += kDotEngines) {
-                        const int bl = it / UFv, r = it - bl * UFv, b = tb0 + bl, j = w * UF + r;
-                        const float d = row_dot(S + s.w2 + r * F, tile + bl * F, F / 4, li);
-                        if (li == 0) {
-                            const float v = d + T[b * NT + 6 * U + UF + r];
-                            store_sc1(f2o + (size_t)b * F + j, v > 0.0f ? v : 0.0f);
+            const bool ok = run_stage(RH_F1, F, [&](const float *tl_, int tb0, int nb) {
+                const int nbb = (nb + kNX - 1) / kNX, nj = nUF2 * nbb;
+                for (int jb = eng; jb < nj; jb += kDotEngines) {
+                    const int r0 = 2 * (jb % nUF2), bb = jb / nUF2;
+                    const int nx = min(kNX, nb - bb * kNX), b = tb0 + bb * kNX + li;
+                    float acc[2];
+                    fc_block(s.w2, UFv, tl_ + bb * kNX * F, F, nx, r0, acc);
+                    if (li < nx)
+#pragma unroll
+                        for (int q = 0; q < 2; ++q) {
+                            const int r = r0 + q;
+                            if (r >= UFv) break;
+                            const float v = acc[q] + T[b * NT + 6 * U + UF + r];
+                            store_sc1(f2o + (size_t)b * F + w * UF + r, v > 0.0f ? v : 0.0f);
                         }
-                    }
-                if (compute && tb0 + TB >= B) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                bar();
-            }
+                }
+            });
+            if (!ok) return;
             signal(RH_F2, t);
+            RSTAMP(9);
         }
 
         // ---- fc3 (:223) + sampling (:225-237), distributed by row
         const bool sampler = w < B;
         if (!MOL) {   // fc3 rows are distributed: logits hand-off first
-            if (wave == 0) wait_flags(flagp(RH_F2), G, want, a.ctl, a.timeout_ticks, t, RH_F2, abort_flag);
-            bar();
-            if (*abort_flag) return;
-            const float *src = actp(RH_F2, t);
             float *lgo = actp(RH_LG, t);
-            for (int tb0 = 0; tb0 < B; tb0 += TB) {
-                const int nb = min(TB, B - tb0);
-                if (compute) {
-                    dma(tile, src + (size_t)tb0 * F, nb * F);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const bool ok = run_stage(RH_F2, F, [&](const float *tl_, int tb0, int nb) {
+                const int nbb = (nb + kNX - 1) / kNX, nj = nUC2 * nbb;
+                for (int jb = eng; jb < nj; jb += kDotEngines) {
+                    const int r0 = 2 * (jb % nUC2), bb = jb / nUC2;
+                    const int nx = min(kNX, nb - bb * kNX), b = tb0 + bb * kNX + li;
+                    float acc[2];
+                    fc_block(s.w3, UCv, tl_ + bb * kNX * F, F, nx, r0, acc);
+                    if (li < nx)
+#pragma unroll
+                        for (int q = 0; q < 2; ++q) {
+                            const int r = r0 + q;
+                            if (r >= UCv) break;
+                            store_sc1(lgo + (size_t)b * NC + w * UC + r, acc[q] + S[s.b3 + r]);
+                        }
                 }
-                bar();
-                if (compute)
-                    for (int it = eng; it < nb * UCv; it += kDotEngines) {
-                        const int bl = it / UCv, r = it - bl * UCv, b = tb0 + bl, j = w * UC + r;
-                        const float d = row_dot(S + s.w3 + r * F, tile + bl * F, F / 4, li);
-                        if (li == 0) store_sc1(lgo + (size_t)b * NC + j, d + S[s.b3 + r]);
-                    }
-                if (compute && tb0 + TB >= B) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                bar();
-            }
+            });
+            if (!ok) return;
             signal(RH_LG, t);
         }
         if (sampler) {
             const int hop = MOL ? RH_F2 : RH_LG;
             const int K = MOL ? F : NC;
-            if (wave == 0) wait_flags(flagp(hop), G, want, a.ctl, a.timeout_ticks, t, hop, abort_flag);
-            bar();
-            if (*abort_flag) return;
             const float *src = actp(hop, t);
-            if (compute) {
-                for (int sr = 0; sr < NS && w + sr * G < B; ++sr) dma(tile + sr * ll.KT, src + (size_t)(w + sr * G) * K, K);
+            if (loader) {
+                wait_flags(flagp(hop), G, want, a.ctl, a.timeout_ticks, t, hop, abort_flag);
+                if (!*abort_flag)
+                    for (int sr = 0; sr < NS && w + sr * G < B; ++sr)
+                        dma(tile + sr * ll.KT, src + (size_t)(w + sr * G) * K, K);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
             bar();
+            RSTAMP(10);
+            if (*abort_flag) return;
             if (MOL) {   // the 30 head rows (replicated in every workgroup) against f2 of each sampled row
                 if (compute)
                     for (int sr = 0; sr < NS && w + sr * G < B; ++sr)
@@ -387,17 +409,27 @@ __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
                         if (a.labels) a.labels[o] = label;
                     }
                 }
+            RSTAMP(11);
         }
 
+        // loader: terms and draws of the next step, while wave 0 collects x
+        if (loader && tl + 1 < a.Lc) {
+            load_terms(tl + 1, lane, 64);
+            load_noise(t + 1, lane, 64);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         // ---- x of every row → next step's GRU1
         if (wave == 0)
             gather<kRowsMax / 64, 64>(a.xg + (size_t)(w % kXReps) * kXRepStride, 0, B, B, want, a.ctl,
                                       a.timeout_ticks, t, kRowsHops, abort_flag, lane,
                                       [&](int, int j, float v) { xs[j] = v; });
         bar();
+        RSTAMP(12);
         if (*abort_flag) return;
     }
 
+#undef RSTAMP
+#undef RSTAMP_T
     // carried state for the next launch of this generate()
     {
         float *cs = a.state + (size_t)w * B * SW;
@@ -428,15 +460,21 @@ hipError_t launch_pack_terms_input(const float *cond, int CD, int Bt, int b0, in
 }
 
 // ------------------------------------------------------------------------ host launchers
+static const void *pick_rows_kernel(const RowsArgs &a) {
+    const bool d512 = a.R == 512 && a.F == 512;
+    if (a.mol) return d512 ? (const void *)fatchord_rows_kernel<true, 512> : (const void *)fatchord_rows_kernel<true, 0>;
+    return d512 ? (const void *)fatchord_rows_kernel<false, 512> : (const void *)fatchord_rows_kernel<false, 0>;
+}
+
 hipError_t launch_rows(const RowsArgs &a, size_t lds_bytes, hipStream_t st) {
-    const void *k = a.mol ? (const void *)fatchord_rows_kernel<true> : (const void *)fatchord_rows_kernel<false>;
     RowsArgs args = a;
     void *params[] = {&args};
-    return hipLaunchKernel(k, dim3(a.G), dim3(kThreads), params, lds_bytes, st);
+    return hipLaunchKernel(pick_rows_kernel(a), dim3(a.G), dim3(kThreads), params, lds_bytes, st);
 }
 
 hipError_t prepare_rows_kernel(int max_lds_bytes) {
-    for (const void *k : {(const void *)fatchord_rows_kernel<true>, (const void *)fatchord_rows_kernel<false>}) {
+    for (const void *k : {(const void *)fatchord_rows_kernel<true, 512>, (const void *)fatchord_rows_kernel<true, 0>,
+                          (const void *)fatchord_rows_kernel<false, 512>, (const void *)fatchord_rows_kernel<false, 0>}) {
         hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds_bytes);
         if (e != hipSuccess) return e;
     }
@@ -444,12 +482,16 @@ hipError_t prepare_rows_kernel(int max_lds_bytes) {
 }
 
 hipError_t rows_occupancy(int *blocks_per_cu, size_t lds_bytes) {
-    int a = 0, b = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, fatchord_rows_kernel<true>, kThreads, lds_bytes);
-    if (e != hipSuccess) return e;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, fatchord_rows_kernel<false>, kThreads, lds_bytes);
-    *blocks_per_cu = a < b ? a : b;
-    return e;
+    int best = 1 << 30;
+    for (const void *k : {(const void *)fatchord_rows_kernel<true, 512>, (const void *)fatchord_rows_kernel<true, 0>,
+                          (const void *)fatchord_rows_kernel<false, 512>, (const void *)fatchord_rows_kernel<false, 0>}) {
+        int n = 0;
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kThreads, lds_bytes);
+        if (e != hipSuccess) return e;
+        best = n < best ? n : best;
+    }
+    *blocks_per_cu = best;
+    return hipSuccess;
 }
 
 }  // namespace wrnn

@@ -264,6 +264,72 @@ __device__ __forceinline__ float3 row_dot3(const float *__restrict__ w0, const f
     return make_float3(row_sum16(s0), row_sum16(s1), row_sum16(s2));
 }
 
+// Reduce-scatter of 4 values over a 16-lane DPP row: lane l returns Σ_row p[l & 3].
+// Two in-quad exchange stages (each lane keeps half of what it holds, adds its partner's
+// other half), then the four quads summed by row rotations of 4 and 8 lanes.
+__device__ __forceinline__ float row_reduce_scatter4(const float (&p)[4], int lane) {
+    const bool o1 = lane & 1, o2 = lane & 2;
+    float k0 = o1 ? p[1] : p[0], g0 = o1 ? p[0] : p[1];
+    float k1 = o1 ? p[3] : p[2], g1 = o1 ? p[2] : p[3];
+    k0 += WRNN_DPP(g0, 0xB1);            // quad_perm [1,0,3,2]: partner l^1
+    k1 += WRNN_DPP(g1, 0xB1);
+    float k = o2 ? k1 : k0, g = o2 ? k0 : k1;
+    k += WRNN_DPP(g, 0x4E);              // quad_perm [2,3,0,1]: partner l^2
+    k += WRNN_DPP(k, 0x124);             // row_ror:4
+    k += WRNN_DPP(k, 0x128);             // row_ror:8
+    return k;
+}
+
+// Register-blocked 16-lane dot engine: out[i] = W_i · X_{li & 3} for NW weight rows (W + i·ws)
+// and 4 activation rows (X + j·xs; rows j >= nx re-read row 0: lanes with (li & 3) >= nx hold
+// garbage), K4 float4 chunks split over the 16 lanes of a DPP row (lane li takes chunks li,
+// li+16, …).  Each chunk load feeds 4·NW·4 FMAs, so LDS traffic per FMA is (NW + 4) / (4·NW) of
+// a plain dot's.  KI > 0 fixes the per-lane chunk count (K4 = 16·KI) at compile time: the loop
+// unrolls fully and the loads of later chunks are issued ahead of the FMAs of earlier ones
+// (with a runtime count hipcc keeps load → lgkmcnt(0) → FMA per chunk).
+template <int NW, int KI = 0>
+__device__ __forceinline__ void bdot4(const float *__restrict__ W, int ws, const float *__restrict__ X, int xs, int nx,
+                                      int K4, int li, float (&out)[NW]) {
+    constexpr int NX = 4;
+    const float4 *w4[NW];
+    const float4 *x4[NX];
+#pragma unroll
+    for (int i = 0; i < NW; ++i) w4[i] = reinterpret_cast<const float4 *>(W + i * ws) + li;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) x4[j] = reinterpret_cast<const float4 *>(X + (j < nx ? j : 0) * xs) + li;
+    float acc[NW][NX];
+#pragma unroll
+    for (int i = 0; i < NW; ++i)
+#pragma unroll
+        for (int j = 0; j < NX; ++j) acc[i][j] = 0.0f;
+    auto step = [&](int k) {
+        float4 wv[NW], xv[NX];
+#pragma unroll
+        for (int i = 0; i < NW; ++i) wv[i] = w4[i][16 * k];
+#pragma unroll
+        for (int j = 0; j < NX; ++j) xv[j] = x4[j][16 * k];
+#pragma unroll
+        for (int i = 0; i < NW; ++i)
+#pragma unroll
+            for (int j = 0; j < NX; ++j) {
+                float a = acc[i][j];
+                a = fmaf(wv[i].x, xv[j].x, a);
+                a = fmaf(wv[i].y, xv[j].y, a);
+                a = fmaf(wv[i].z, xv[j].z, a);
+                a = fmaf(wv[i].w, xv[j].w, a);
+                acc[i][j] = a;
+            }
+    };
+    if (KI > 0) {
+#pragma unroll
+        for (int k = 0; k < KI; ++k) step(k);
+    } else {
+        for (int k = 0; 16 * k + li < K4; ++k) step(k);
+    }
+#pragma unroll
+    for (int i = 0; i < NW; ++i) out[i] = row_reduce_scatter4(acc[i], li);
+}
+
 // ----------------------------------------------------------------------------- samplers
 // One wave samples one row; the result is wave-uniform.
 //
