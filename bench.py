@@ -29,7 +29,7 @@ sys.path.insert(0, REPO)
 from wavernn_amd import synthetic as syn  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
-PMC_PROFILE = os.path.join(REPO, "profiles", "r01_v4_pmc_traffic.json")
+PMC_PROFILE = os.path.join(REPO, "profiles", "r01_v5_pmc_traffic.json")
 
 
 def pmc_traffic_bytes(mode: str, batched: bool, seconds: float):
@@ -151,10 +151,28 @@ def main():
                 "traffic": pmc_traffic_bytes(args.mode, args.batched, args.seconds),
                 "note": "achieved = algorithmic bytes (all loop weights fp32 per step + 836 B/row-step) per launch "
                         "/ launch time (HIP events); weights are LDS-resident, the kernel is hand-off-latency bound. "
-                        "traffic = FETCH_SIZE+WRITE_SIZE bytes per launch from profiles/r01_v4_pmc_traffic.json: "
+                        "traffic = FETCH_SIZE+WRITE_SIZE bytes per launch from profiles/r01_v5_pmc_traffic.json: "
                         "granule polling/publishing, not weight streaming",
             },
         }
+        if not args.batched and args.mode == "MOL":
+            # the same utterance through the reference's default generate() mode
+            # (hparams voc_gen_batched = True: 11000/550 folds, one multi-row launch)
+            model.generate(mel, None, True, target, overlap, True, seed=7, verbose=False)
+            torch.cuda.synchronize()
+            tb = time.perf_counter()
+            outb = model.generate(mel, None, True, target, overlap, True, seed=8, verbose=False)
+            torch.cuda.synchronize()
+            dtb = time.perf_counter() - tb
+            kb = model.loop_handle().elapsed_ms()
+            condb, _ = model.conditioning(mel, True, target, overlap)
+            rec["fold_batched"] = {
+                "samples_per_s": outb.shape[0] / dtb, "rtf": outb.shape[0] / dtb / d.sample_rate,
+                "rows": int(condb.shape[1]), "loop_steps": int(condb.shape[0]), "device_ms": kb,
+                "us_per_loop_step": kb * 1e3 / condb.shape[0],
+                "note": "same 5 s utterance, generate(batched=True) as gen_wavernn.py runs it with the 800k "
+                        "hparams; one multi-row persistent launch (fatchord_rows.hip) + conditioning-terms GEMM",
+            }
         if args.cpu_steps > 0 and world == 1:
             from oracle import oracle
             cpu = cond.transpose(0, 1).cpu().numpy()
