@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define WRNN_ABI_VERSION 1
+#define WRNN_ABI_VERSION 2
 
 enum wrnn_status {
     WRNN_OK = 0,
@@ -65,16 +65,21 @@ typedef struct {
     int32_t on_device;       /* 1: `data` is a device pointer, 0: host pointer */
 } wrnn_tensor;
 
-/* Launch geometry chosen for the handle (read-only). */
+/* Launch geometry chosen for the handle (read-only).  Two kernels: the per-row latency kernel
+ * (rows in LDS, used while B <= max_rows) and the multi-row kernel (rows through HBM). */
 typedef struct {
     int32_t grid;            /* workgroups (all co-resident, one persistent launch) */
     int32_t units_rnn;       /* hidden units per workgroup (GRU rows ×3)            */
     int32_t units_fc;        /* fc1/fc2 rows per workgroup                          */
     int32_t units_cls;       /* fc3 rows per workgroup (RAW; MOL computes all 30)   */
-    int32_t max_rows;        /* batch rows one launch holds; more are chunked       */
+    int32_t max_rows;        /* rows one latency-kernel launch holds (0: multi-row kernel only) */
     int32_t lds_bytes;       /* dynamic LDS per workgroup at max_rows                */
     int32_t slab_floats;     /* resident weight floats per workgroup                 */
     int32_t num_cus;
+    int32_t rows_grid;       /* multi-row kernel: workgroups (0: unavailable)        */
+    int32_t rows_units_rnn;  /*                   hidden units per workgroup         */
+    int32_t sparse_blocks;   /*                   max nonzero 4x4 blocks per gate block-row when
+                                                  the GRU weights are block-sparse, else 0 */
 } wrnn_info;
 
 /* Create a handle on `device` (replaces WaveRNN.__init__ for the loop's dims,

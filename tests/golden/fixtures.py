@@ -12,6 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LOOP_CASES = ["loop_raw_tiny_b2", "loop_mol_tiny_b2", "loop_raw_b1", "loop_mol_b1",
               "loop_raw_b3", "loop_mol_b4"]
 LONG_LOOP_CASES = ["loop_raw_1s", "loop_mol_1s"]
+SPARSE_LOOP_CASES = ["loop_mol_sparse896_b2", "loop_raw_sparse_b2"]
 GEN_CASES = ["gen_mol_unbatched", "gen_raw_batched_mulaw", "gen_mol_batched", "gen_raw_tiny_unbatched"]
 
 # MoL parity tolerance per sample under noise injection: ~50-100x the
@@ -34,6 +35,9 @@ def loop_inputs(fx: dict):
     d = dims_of(fx)
     B, L = int(fx["B"]), int(fx["L"])
     state = syn.make_fatchord_state(d, int(fx["wseed"]))
+    if float(fx.get("prune", 0.0)) > 0:
+        from wavernn_amd.pruning import prune_state
+        state = prune_state(state, float(fx["prune"]))
     mels, aux = syn.make_conditioning(B, L, d.feat_dims, d.res_out_dims, int(fx["cseed"]))
     noise = syn.make_noise(d.mode, B, L, d.n_classes, int(fx["nseed"]))
     assert syn.state_digest(state) == str(fx["state_sha"]), "synthetic weight generator drifted"

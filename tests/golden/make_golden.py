@@ -150,9 +150,13 @@ def fold_count(L: int, target: int, overlap: int) -> int:
 
 
 # ----------------------------------------------------------------------------- loop cases
-def loop_case(fv, name, d: syn.FatchordDims, B: int, L: int, wseed=0, cseed=2, nseed=3):
-    """Drive the reference loop (fatchord_version.py:201-241) on given folded conditioning."""
+def loop_case(fv, name, d: syn.FatchordDims, B: int, L: int, wseed=0, cseed=2, nseed=3, prune=0.0):
+    """Drive the reference loop (fatchord_version.py:201-241) on given folded conditioning.
+    prune > 0: GRU weights block-pruned to that sparsity first (wavernn_amd/pruning.py)."""
     state = syn.make_fatchord_state(d, wseed)
+    if prune > 0:
+        from wavernn_amd.pruning import prune_state
+        state = prune_state(state, prune)
     mels, aux = syn.make_conditioning(B, L, d.feat_dims, d.res_out_dims, cseed)
     noise = syn.make_noise(d.mode, B, L, d.n_classes, nseed)
     model = build_ref_model(fv, d, state)
@@ -177,7 +181,7 @@ def loop_case(fv, name, d: syn.FatchordDims, B: int, L: int, wseed=0, cseed=2, n
     dt = time.time() - t0
     assert inj.t == L, (inj.t, L)
     outs = np.stack(inj.samples)  # [L][B]
-    rec = dict(kind="loop", mode=d.mode, B=B, L=L, wseed=wseed, cseed=cseed, nseed=nseed,
+    rec = dict(kind="loop", mode=d.mode, B=B, L=L, wseed=wseed, cseed=cseed, nseed=nseed, prune=prune,
                dims=np.array(repr(d)), ref_seconds=dt,
                state_sha=syn.state_digest(state), cond_sha=syn.digest(mels, aux),
                noise_sha=syn.digest(noise))
@@ -243,6 +247,9 @@ def cases():
         # config 1 (RAW 9-bit, rnn 512, 1 s) and its MoL twin, full length
         "loop_raw_1s": ("loop", dict(d=R, B=1, L=22275)),
         "loop_mol_1s": ("loop", dict(d=M, B=1, L=22275)),
+        # config 4: rnn 896 with 95 % 4x4 block-sparse GRU weights; and a RAW twin at rnn 512
+        "loop_mol_sparse896_b2": ("loop", dict(d=syn.SPARSE896_MOL, B=2, L=1100, prune=0.95)),
+        "loop_raw_sparse_b2": ("loop", dict(d=R, B=2, L=1500, prune=0.95)),
         # end-to-end generate() fixtures
         "gen_mol_unbatched": ("gen", dict(d=M, T=22, batched=False, target=11000, overlap=550, mu_law=True)),
         "gen_raw_batched_mulaw": ("gen", dict(d=R, T=30, batched=True, target=2000, overlap=200, mu_law=True)),

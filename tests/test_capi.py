@@ -32,9 +32,22 @@ def test_library_exports_every_declared_symbol(lib):
         assert hasattr(lib, name), name
 
 
+def _header_fields(struct_name):
+    """(type, name) of the fields of `typedef struct {...} struct_name;` in include/wavernn_amd.h"""
+    import re
+    text = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
+                             "wavernn_amd.h")).read()
+    body = re.search(r"typedef struct \{([^{}]*)\}\s*" + struct_name + ";", text).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    return re.findall(r"(\w+)\s*\*?\s*(\w+);", body)
+
+
 def test_struct_layouts_match_header():
-    assert ctypes.sizeof(nat.Config) == 9 * 4
-    assert ctypes.sizeof(nat.Info) == 8 * 4
+    for struct, ct in (("wrnn_config", nat.Config), ("wrnn_info", nat.Info)):
+        fields = _header_fields(struct)
+        assert [n for _, n in fields] == [n for n, _ in ct._fields_], struct
+        assert all(t == "int32_t" for t, _ in fields)
+        assert ctypes.sizeof(ct) == 4 * len(fields)
     assert ctypes.sizeof(nat.Tensor) == 8 + 8 + 8 + 8
 
 

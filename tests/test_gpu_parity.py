@@ -147,6 +147,44 @@ def test_paths_agree_under_philox(mode, monkeypatch):
         assert (res["latency"][0] - res["rows"][0]).abs().max().item() <= 2 * gf.MOL_TOL
 
 
+@pytest.mark.parametrize("name", gf.SPARSE_LOOP_CASES)
+def test_sparse_loop_vs_reference_fixture(name, monkeypatch):
+    """Config 4: 4x4 block-sparse GRU weights (pruning.py) run in the multi-row kernel with only
+    the nonzero blocks resident (rnn 896 → G = 224 workgroups of one block-row each)."""
+    monkeypatch.setenv("WRNN_PATH", "rows")
+    fx = gf.load(name)
+    d, state, mels, aux, noise = gf.loop_inputs(fx)
+    loop = _loop(d)
+    loop.set_weights(state)
+    assert loop.info["sparse_blocks"] > 0 and loop.info["rows_units_rnn"] == 4
+    out, lab = loop.generate(_cond(mels, aux), noise=torch.from_numpy(noise).to(DEV), want_labels=True)
+    if d.mode == "RAW":
+        _report_raw(lab.cpu().numpy(), fx["labels"].astype(np.int32))
+    else:
+        err = np.abs(out.cpu().numpy() - fx["samples"])
+        assert err.max() <= gf.MOL_TOL, f"max |Δ| {err.max()}"
+
+
+@pytest.mark.parametrize("sparse", ["1", "0"])
+def test_pruned_weights_sparse_and_dense_rows_kernel(sparse, monkeypatch):
+    """The same pruned weights through the sparse (nonzero blocks) and dense rows kernels, and
+    a tiny-dims RAW model (G = 16 block-rows): oracle parity, labels exact."""
+    from oracle import oracle
+    from wavernn_amd.pruning import prune_state
+    monkeypatch.setenv("WRNN_PATH", "rows")
+    monkeypatch.setenv("WRNN_SPARSE", sparse)
+    for d, B, L in ((syn.DEFAULT_RAW, 3, 500), (syn.TINY_RAW, 5, 300)):
+        state = prune_state(syn.make_fatchord_state(d, 51), 0.9)
+        mels, aux = syn.make_conditioning(B, L, d.feat_dims, d.res_out_dims, 52)
+        noise = syn.make_noise(d.mode, B, L, d.n_classes, 53)
+        _, ref_lab = oracle.fatchord_loop(state, d.mode, mels, aux, noise)
+        loop = _loop(d)
+        loop.set_weights(state)
+        assert (loop.info["sparse_blocks"] > 0) == (sparse == "1")
+        _, lab = loop.generate(_cond(mels, aux), noise=torch.from_numpy(noise).to(DEV), want_labels=True)
+        _report_raw(lab.cpu().numpy(), ref_lab)
+
+
 def test_philox_deterministic_and_shard_invariant(path):
     """Philox draws are keyed by (seed, global row, step, k): a row generated alone with its
     global row offset reproduces that row of a batch.  Bit-exact in the latency kernel; within

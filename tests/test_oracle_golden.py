@@ -8,7 +8,7 @@ from oracle import oracle as orc
 from tests.golden import fixtures as gf
 
 
-@pytest.mark.parametrize("name", gf.LOOP_CASES)
+@pytest.mark.parametrize("name", gf.LOOP_CASES + gf.SPARSE_LOOP_CASES)
 def test_loop_matches_reference(name):
     fx = gf.load(name)
     d, state, mels, aux, noise = gf.loop_inputs(fx)

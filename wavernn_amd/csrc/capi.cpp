@@ -56,6 +56,8 @@ struct wrnn_ctx {
     std::string err;
     // multi-row (fold-batched) path: fatchord_rows.hip
     RowsSlab rs{};
+    int rU = 0, rG = 0, rUF = 0, rUC = 0;           // rows-kernel partition (U = 4 when sparse)
+    bool sparse = false;                            // GRU weights stored as nonzero 4x4 blocks
     int NT = 0, KX = 0, KA = 0;
     bool rows_ok = false;                           // weights fit LDS with at least one row
     float *d_rslab = nullptr, *d_Wt = nullptr;      // per-workgroup slabs, terms-GEMM weights [G·NT][KX]
@@ -172,28 +174,73 @@ void pack_slab(const wrnn_ctx &h, int w, float *out) {
     for (int j = 0; j < R; ++j) out[s.wi0 + j] = IW[(size_t)j * nin];
 }
 
-RowsSlab make_rows_slab(const wrnn_ctx &h) {
+RowsSlab make_rows_slab(const wrnn_ctx &h, int nbmax) {
     const int R = h.cfg.rnn_dims, F = h.cfg.fc_dims, NC = h.cfg.n_classes;
     const bool mol = h.cfg.mode == WRNN_MODE_MOL;
+    const int dense = nbmax > 0 ? 0 : 1;
     RowsSlab s{};
     int o = 0;
     auto take = [&](int n) { int at = o; o += round4(n); return at; };
-    s.wih2 = take(3 * h.U * R);
-    s.whh1 = take(3 * h.U * R);
-    s.whh2 = take(3 * h.U * R);
-    s.w1 = take(h.UF * R);
-    s.w2 = take(h.UF * F);
-    s.w3 = take((mol ? NC : h.UC) * F);
-    s.b3 = take(mol ? NC : h.UC);
-    s.bih1 = take(3 * h.U);
-    s.bhh1 = take(3 * h.U);
-    s.bih2 = take(3 * h.U);
-    s.bhh2 = take(3 * h.U);
-    s.q1 = take(3 * h.U);
-    s.q2 = take(3 * h.U);
-    s.q3 = take(h.UF);
+    s.wih2 = take(dense * 3 * h.rU * R);
+    s.whh1 = take(dense * 3 * h.rU * R);
+    s.whh2 = take(dense * 3 * h.rU * R);
+    s.sp = take(9 * nbmax * 16);
+    s.spc = take(9 * nbmax);
+    s.spn = take(nbmax > 0 ? 9 : 0);
+    s.nbmax = nbmax;
+    s.w1 = take(h.rUF * R);
+    s.w2 = take(h.rUF * F);
+    s.w3 = take((mol ? NC : h.rUC) * F);
+    s.b3 = take(mol ? NC : h.rUC);
+    s.bih1 = take(3 * h.rU);
+    s.bhh1 = take(3 * h.rU);
+    s.bih2 = take(3 * h.rU);
+    s.bhh2 = take(3 * h.rU);
+    s.q1 = take(3 * h.rU);
+    s.q2 = take(3 * h.rU);
+    s.q3 = take(h.rUF);
     s.total = o;
     return s;
+}
+
+// The three GRU matrices the rows kernel multiplies in the loop, as (tensor, row stride):
+// W_ih2[:, :R] (stride R + A), W_hh1, W_hh2 (SparseMat order).
+struct LoopMat {
+    const float *w;
+    int ld;
+};
+void loop_mats(const wrnn_ctx &h, LoopMat (&m)[3]) {
+    const int R = h.cfg.rnn_dims, A = h.cfg.aux_dims;
+    m[SP_WIH2] = {h.w.at("rnn2.weight_ih_l0").data(), R + A};
+    m[SP_WHH1] = {h.w.at("rnn1.weight_hh_l0").data(), R};
+    m[SP_WHH2] = {h.w.at("rnn2.weight_hh_l0").data(), R};
+}
+
+bool block_nonzero(const float *w, int ld, int r0, int c0) {
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c)
+            if (w[(size_t)(r0 + r) * ld + c0 + c] != 0.0f) return true;
+    return false;
+}
+
+// Largest nonzero-block count of any gate block-row (4 rows) of the three loop matrices, and the
+// overall block density; the rows kernel goes sparse when density <= 1/2.
+void block_stats(const wrnn_ctx &h, int *nbmax, double *density) {
+    const int R = h.cfg.rnn_dims;
+    LoopMat m[3];
+    loop_mats(h, m);
+    long long nz = 0, tot = 0;
+    int mx = 0;
+    for (int k = 0; k < 3; ++k)
+        for (int rb = 0; rb < 3 * R; rb += 4) {
+            int n = 0;
+            for (int cb = 0; cb < R; cb += 4) n += block_nonzero(m[k].w, m[k].ld, rb, cb);
+            nz += n;
+            tot += R / 4;
+            mx = std::max(mx, n);
+        }
+    *nbmax = mx;
+    *density = tot ? (double)nz / tot : 1.0;
 }
 
 // x-column constants Q = W[:, :R]·W_I[:, 0] (fp32, sequential)
@@ -207,20 +254,23 @@ void pack_rows_slab(const wrnn_ctx &h, int w, float *out) {
     const int R = h.cfg.rnn_dims, F = h.cfg.fc_dims, A = h.cfg.aux_dims, NC = h.cfg.n_classes;
     const bool mol = h.cfg.mode == WRNN_MODE_MOL;
     const RowsSlab &s = h.rs;
+    const int U = h.rU, UF = h.rUF, UC = h.rUC;
     std::fill(out, out + s.total, 0.0f);
     auto W = [&](const char *n) { return h.w.at(n).data(); };
     const float *IW = W("I.weight");
     const int nin = 1 + h.cfg.feat_dims + A;
-    for (int u = 0; u < h.U; ++u) {
-        const int j = w * h.U + u;
+    for (int u = 0; u < U; ++u) {
+        const int j = w * U + u;
         if (j >= R) continue;
         for (int g = 0; g < 3; ++g) {
-            const int src = g * R + j, dst = g * h.U + u;
+            const int src = g * R + j, dst = g * U + u;
             const float *ih1 = W("rnn1.weight_ih_l0") + (size_t)src * R;
             const float *ih2 = W("rnn2.weight_ih_l0") + (size_t)src * (R + A);
-            std::memcpy(out + s.wih2 + (size_t)dst * R, ih2, R * 4);
-            std::memcpy(out + s.whh1 + (size_t)dst * R, W("rnn1.weight_hh_l0") + (size_t)src * R, R * 4);
-            std::memcpy(out + s.whh2 + (size_t)dst * R, W("rnn2.weight_hh_l0") + (size_t)src * R, R * 4);
+            if (s.nbmax == 0) {
+                std::memcpy(out + s.wih2 + (size_t)dst * R, ih2, R * 4);
+                std::memcpy(out + s.whh1 + (size_t)dst * R, W("rnn1.weight_hh_l0") + (size_t)src * R, R * 4);
+                std::memcpy(out + s.whh2 + (size_t)dst * R, W("rnn2.weight_hh_l0") + (size_t)src * R, R * 4);
+            }
             out[s.bih1 + dst] = W("rnn1.bias_ih_l0")[src];
             out[s.bhh1 + dst] = W("rnn1.bias_hh_l0")[src];
             out[s.bih2 + dst] = W("rnn2.bias_ih_l0")[src];
@@ -229,8 +279,28 @@ void pack_rows_slab(const wrnn_ctx &h, int w, float *out) {
             out[s.q2 + dst] = xcol_dot(ih2, IW, nin, R);
         }
     }
-    for (int r = 0; r < h.UF; ++r) {
-        const int j = w * h.UF + r;
+    if (s.nbmax > 0) {   // this workgroup's block-row (units 4w..4w+3) of each gate, nonzero blocks only
+        LoopMat m[3];
+        loop_mats(h, m);
+        int *col = reinterpret_cast<int *>(out + s.spc);
+        int *cnt = reinterpret_cast<int *>(out + s.spn);
+        for (int k = 0; k < 3; ++k)
+            for (int g = 0; g < 3; ++g) {
+                const int r0 = g * R + 4 * w, sl = k * 3 + g;
+                int n = 0;
+                for (int cb = 0; cb < R; cb += 4) {
+                    if (!block_nonzero(m[k].w, m[k].ld, r0, cb)) continue;
+                    float *blk = out + s.sp + ((size_t)sl * s.nbmax + n) * 16;
+                    for (int r = 0; r < 4; ++r)
+                        for (int c = 0; c < 4; ++c) blk[r * 4 + c] = m[k].w[(size_t)(r0 + r) * m[k].ld + cb + c];
+                    col[sl * s.nbmax + n] = cb / 4;
+                    ++n;
+                }
+                cnt[sl] = n;
+            }
+    }
+    for (int r = 0; r < UF; ++r) {
+        const int j = w * UF + r;
         if (j >= F) continue;
         const float *w1 = W("fc1.weight") + (size_t)j * (R + A);
         std::memcpy(out + s.w1 + (size_t)r * R, w1, R * 4);
@@ -241,8 +311,8 @@ void pack_rows_slab(const wrnn_ctx &h, int w, float *out) {
         std::memcpy(out + s.w3, W("fc3.weight"), (size_t)NC * F * 4);
         std::memcpy(out + s.b3, W("fc3.bias"), (size_t)NC * 4);
     } else {
-        for (int r = 0; r < h.UC; ++r) {
-            const int j = w * h.UC + r;
+        for (int r = 0; r < UC; ++r) {
+            const int j = w * UC + r;
             if (j >= NC) continue;
             std::memcpy(out + s.w3 + (size_t)r * F, W("fc3.weight") + (size_t)j * F, F * 4);
             out[s.b3 + r] = W("fc3.bias")[j];
@@ -252,10 +322,10 @@ void pack_rows_slab(const wrnn_ctx &h, int w, float *out) {
 
 // Weights of the conditioning-terms GEMM: row w·NT + k of [G·NT][KX] against X = [cI | a2 a3 a4 | 1 0 0 0]
 void pack_terms_weights(const wrnn_ctx &h, float *Wt) {
-    const int R = h.cfg.rnn_dims, F = h.cfg.fc_dims, A = h.cfg.aux_dims, U = h.U, UF = h.UF, KX = h.KX;
+    const int R = h.cfg.rnn_dims, F = h.cfg.fc_dims, A = h.cfg.aux_dims, U = h.rU, UF = h.rUF, KX = h.KX;
     auto W = [&](const char *n) { return h.w.at(n).data(); };
-    std::fill(Wt, Wt + (size_t)h.G * h.NT * KX, 0.0f);
-    for (int w = 0; w < h.G; ++w)
+    std::fill(Wt, Wt + (size_t)h.rG * h.NT * KX, 0.0f);
+    for (int w = 0; w < h.rG; ++w)
         for (int k = 0; k < 6 * U + 2 * UF; ++k) {
             float *row = Wt + ((size_t)w * h.NT + k) * KX;
             if (k < 6 * U) {
@@ -285,9 +355,30 @@ void pack_terms_weights(const wrnn_ctx &h, float *Wt) {
 }
 
 size_t rows_lds_bytes(const wrnn_ctx &h, int B, int TB) {
-    return (size_t)rows_lds_layout(h.rs.total, B, TB, h.cfg.rnn_dims, h.cfg.fc_dims, h.cfg.n_classes, h.NK, h.U, h.UF,
-                                   h.G)
+    return (size_t)rows_lds_layout(h.rs.total, B, TB, h.cfg.rnn_dims, h.cfg.fc_dims, h.cfg.n_classes, h.NK, h.rU,
+                                   h.rUF, h.rG)
                .total * sizeof(float);
+}
+
+// (Re)derive the rows-kernel partition: dense = the latency kernel's; sparse = one 4-unit
+// block-row per workgroup (G = R / 4).  Sets rows_ok.
+int rows_tile_for(const wrnn_ctx &h, int B);
+void set_rows_partition(wrnn_ctx &h, int nbmax) {
+    const int R = h.cfg.rnn_dims, F = h.cfg.fc_dims;
+    const bool mol = h.cfg.mode == WRNN_MODE_MOL;
+    h.sparse = nbmax > 0;
+    if (h.sparse) {
+        h.rU = 4;
+        h.rG = R / 4;
+    } else {
+        h.rU = h.U;
+        h.rG = h.G;
+    }
+    h.rUF = (F + h.rG - 1) / h.rG;
+    h.rUC = mol ? 0 : (h.cfg.n_classes + h.rG - 1) / h.rG;
+    h.NT = rows_terms(h.rU, h.rUF);
+    h.rs = make_rows_slab(h, nbmax);
+    h.rows_ok = rows_tile_for(h, 1) > 0;
 }
 
 // Largest tile (<= 16 rows) that fits next to B rows of state; 0 if none does
@@ -323,14 +414,14 @@ hipError_t ensure(T *&p, size_t &cap, size_t n) {
 }
 
 // WRNN_DEBUG_FILE (default wrnn_stamps.bin): int32 header {G, steps, kStamps}, then the stamps
-int dump_stamps(wrnn_t *h, unsigned *d_dbg, int dbg_steps, hipStream_t st) {
-    std::vector<unsigned> host((size_t)h->G * dbg_steps * kStamps);
+int dump_stamps(wrnn_t *h, unsigned *d_dbg, int dbg_steps, hipStream_t st, int G) {
+    std::vector<unsigned> host((size_t)G * dbg_steps * kStamps);
     HIP_TRY(h, hipStreamSynchronize(st));
     HIP_TRY(h, hipMemcpy(host.data(), d_dbg, host.size() * 4, hipMemcpyDeviceToHost));
     HIP_TRY(h, hipFree(d_dbg));
     const char *path = std::getenv("WRNN_DEBUG_FILE");
     if (FILE *f = std::fopen(path ? path : "wrnn_stamps.bin", "wb")) {
-        int hdr[3] = {h->G, dbg_steps, kStamps};
+        int hdr[3] = {G, dbg_steps, kStamps};
         std::fwrite(hdr, sizeof(hdr), 1, f);
         std::fwrite(host.data(), 4, host.size(), f);
         std::fclose(f);
@@ -348,7 +439,7 @@ int grow(wrnn_t *h, float *&p, size_t &cap, size_t n) {
 int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed, int64_t row_offset,
                   float *out, int32_t *labels, hipStream_t st) {
     const wrnn_config &c = h->cfg;
-    const int R = c.rnn_dims, A = c.aux_dims, N = h->G * h->NT;
+    const int R = c.rnn_dims, A = c.aux_dims, N = h->rG * h->NT;
     if (!h->d_flags) {
         HIP_TRY(h, hipMalloc(&h->d_flags, (size_t)kRowsHops * kFlagSlots * kFlagStride * 4));
         HIP_TRY(h, hipMalloc(&h->d_xr, (size_t)kXReps * kXRepStride * 8));
@@ -363,20 +454,20 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
     const int dbg_steps = dbg_env ? std::min(L, std::atoi(dbg_env)) : 0;
     unsigned *d_dbg = nullptr;
     if (dbg_steps > 0) {
-        HIP_TRY(h, hipMalloc(&d_dbg, (size_t)h->G * dbg_steps * kStamps * 4));
-        HIP_TRY(h, hipMemsetAsync(d_dbg, 0, (size_t)h->G * dbg_steps * kStamps * 4, st));
+        HIP_TRY(h, hipMalloc(&d_dbg, (size_t)h->rG * dbg_steps * kStamps * 4));
+        HIP_TRY(h, hipMemsetAsync(d_dbg, 0, (size_t)h->rG * dbg_steps * kStamps * 4, st));
     }
     for (int b0 = 0; b0 < B;) {
         int Bl = std::min(B - b0, kRowsMax);
         while (Bl > 1 && rows_tile_for(*h, Bl) == 0) --Bl;
         const int TB = rows_tile_for(*h, Bl);
         if (TB == 0) return fail(h, WRNN_EUNSUPPORTED, "rows kernel: one row of state does not fit LDS");
-        const int SW = rows_state_width(h->U, h->UF);
+        const int SW = rows_state_width(h->rU, h->rUF);
         const int Lc_max = (int)std::max(1.0, std::min((double)L, budget / ((double)Bl * (N + h->KX))));
         if (grow(h, h->d_X, h->X_cap, (size_t)Lc_max * Bl * h->KX) ||
             grow(h, h->d_T, h->T_cap, (size_t)Lc_max * Bl * N) ||
             grow(h, h->d_act, h->act_cap, (size_t)kRowsHops * 2 * Bl * h->KA) ||
-            grow(h, h->d_state, h->state_cap, (size_t)h->G * Bl * SW + Bl))
+            grow(h, h->d_state, h->state_cap, (size_t)h->rG * Bl * SW + Bl))
             return WRNN_EHIP;
         HIP_TRY(h, hipMemsetAsync(h->d_flags, 0, (size_t)kRowsHops * kFlagSlots * kFlagStride * 4, st));
         HIP_TRY(h, hipMemsetAsync(h->d_xr, 0, (size_t)kXReps * kXRepStride * 8, st));
@@ -415,10 +506,10 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
             a.NC = c.n_classes;
             a.NK = h->NK;
             a.mol = c.mode == WRNN_MODE_MOL;
-            a.U = h->U;
-            a.UF = h->UF;
-            a.UC = h->UC;
-            a.G = h->G;
+            a.U = h->rU;
+            a.UF = h->rUF;
+            a.UC = h->rUC;
+            a.G = h->rG;
             a.NT = h->NT;
             a.TB = TB;
             a.KA = h->KA;
@@ -429,7 +520,7 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
         }
         b0 += Bl;
     }
-    if (d_dbg) return dump_stamps(h, d_dbg, dbg_steps, st);
+    if (d_dbg) return dump_stamps(h, d_dbg, dbg_steps, st, h->rG);
     return WRNN_OK;
 }
 
@@ -503,7 +594,7 @@ int generate_latency(wrnn_t *h, const float *cond, int B, int L, const float *no
         a.dbg_steps = dbg_steps;
         HIP_TRY(h, launch_loop(a, lds_bytes_for(*h, Bc), st));
     }
-    if (d_dbg) return dump_stamps(h, d_dbg, dbg_steps, st);
+    if (d_dbg) return dump_stamps(h, d_dbg, dbg_steps, st, h->G);
     return WRNN_OK;
 }
 
@@ -547,11 +638,12 @@ int wrnn_create(const wrnn_config *cfg, int device, wrnn_t **out) {
     h->CD = c.feat_dims + 4 * c.aux_dims;
     h->s = make_slab_layout(*h);
     // rows per launch: LDS, and the per-thread gather register budget
-    h->rs = make_rows_slab(*h);
-    h->NT = rows_terms(h->U, h->UF);
     h->KX = R + 3 * c.aux_dims + 4;
     h->KA = round4(std::max(R, std::max(F, c.n_classes)));
-    h->rows_ok = rows_tile_for(*h, 1) > 0;
+    set_rows_partition(*h, 0);
+    // dims whose dense weights fit neither kernel may still run with block-sparse GRU weights
+    // (decided at wrnn_set_weights)
+    const bool sparse_possible = R % 4 == 0 && R / 4 <= h->num_cus;
     h->max_rows = 0;
     for (int b = 1; b <= 64; ++b) {
         if (lds_bytes_for(*h, b) > (size_t)h->max_lds) break;
@@ -561,7 +653,7 @@ int wrnn_create(const wrnn_config *cfg, int device, wrnn_t **out) {
         if (fast ? b > 2 : (size_t)b * h->NMAX > (size_t)kPollThreads * kGatherMax) break;
         h->max_rows = b;
     }
-    if (h->max_rows < 1 && !h->rows_ok)
+    if (h->max_rows < 1 && !h->rows_ok && !sparse_possible)
         return fail(h, WRNN_EUNSUPPORTED, "weight slab + one row of state exceeds LDS (" +
                                               std::to_string(lds_bytes_for(*h, 1)) + " B)");
     HIP_TRY(h, prepare_loop_kernel(h->max_lds));
@@ -576,7 +668,7 @@ int wrnn_create(const wrnn_config *cfg, int device, wrnn_t **out) {
     }
     if (h->rows_ok) {
         HIP_TRY(h, rows_occupancy(&per_cu, rows_lds_bytes(*h, 1, 1)));
-        if (per_cu * h->num_cus < h->G) h->rows_ok = false;
+        if (per_cu * h->num_cus < h->rG) h->rows_ok = false;
     }
     h->timeout_ticks = (long long)(c.timeout_ms > 0 ? c.timeout_ms : 2000) * 100000LL;   // 100 MHz
     HIP_TRY(h, hipMalloc(&h->d_ctl, kCtlWords * sizeof(int)));
@@ -608,24 +700,47 @@ int wrnn_set_weights(wrnn_t *h, const wrnn_tensor *tensors, int n) {
     for (const auto &q : need)
         if (!h->w.count(q.name)) { h->ready = false; return WRNN_OK; }   // partial load so far
     // pack and upload
-    std::vector<float> slab((size_t)h->G * h->s.total);
-    for (int w = 0; w < h->G; ++w) pack_slab(*h, w, slab.data() + (size_t)w * h->s.total);
-    if (!h->d_slab) HIP_TRY(h, hipMalloc(&h->d_slab, slab.size() * 4));
-    HIP_TRY(h, hipMemcpy(h->d_slab, slab.data(), slab.size() * 4, hipMemcpyHostToDevice));
+    if (h->max_rows >= 1) {
+        std::vector<float> slab((size_t)h->G * h->s.total);
+        for (int w = 0; w < h->G; ++w) pack_slab(*h, w, slab.data() + (size_t)w * h->s.total);
+        if (!h->d_slab) HIP_TRY(h, hipMalloc(&h->d_slab, slab.size() * 4));
+        HIP_TRY(h, hipMemcpy(h->d_slab, slab.data(), slab.size() * 4, hipMemcpyHostToDevice));
+    }
     const auto &IW = h->w.at("I.weight");
     const auto &Ib = h->w.at("I.bias");
     if (!h->d_IW) HIP_TRY(h, hipMalloc(&h->d_IW, IW.size() * 4));
     if (!h->d_Ib) HIP_TRY(h, hipMalloc(&h->d_Ib, Ib.size() * 4));
     HIP_TRY(h, hipMemcpy(h->d_IW, IW.data(), IW.size() * 4, hipMemcpyHostToDevice));
     HIP_TRY(h, hipMemcpy(h->d_Ib, Ib.data(), Ib.size() * 4, hipMemcpyHostToDevice));
+    // rows kernel: block-sparse GRU weights (pruning.py) are kept as nonzero 4x4 blocks when the
+    // block density is <= 1/2 (WRNN_SPARSE=0 keeps them dense)
+    {
+        const int R = h->cfg.rnn_dims;
+        int nbmax = 0;
+        double density = 1.0;
+        const char *sp_env = std::getenv("WRNN_SPARSE");
+        if (R % 4 == 0 && R / 4 <= h->num_cus && !(sp_env && std::string(sp_env) == "0"))
+            block_stats(*h, &nbmax, &density);
+        set_rows_partition(*h, density <= 0.5 ? std::max(nbmax, 1) : 0);
+        if (h->rows_ok) {
+            int per_cu = 0;
+            HIP_TRY(h, rows_occupancy(&per_cu, rows_lds_bytes(*h, 1, 1)));
+            if (per_cu * h->num_cus < h->rG) h->rows_ok = false;
+        }
+        if (h->max_rows < 1 && !h->rows_ok)
+            return fail(h, WRNN_EUNSUPPORTED, "these dims fit neither kernel's LDS layout with dense GRU weights "
+                                              "(block-sparse 4x4 GRU weights would, see pruning.py)");
+    }
     if (h->rows_ok) {
-        std::vector<float> rslab((size_t)h->G * h->rs.total);
-        for (int w = 0; w < h->G; ++w) pack_rows_slab(*h, w, rslab.data() + (size_t)w * h->rs.total);
-        if (!h->d_rslab) HIP_TRY(h, hipMalloc(&h->d_rslab, rslab.size() * 4));
+        std::vector<float> rslab((size_t)h->rG * h->rs.total);
+        for (int w = 0; w < h->rG; ++w) pack_rows_slab(*h, w, rslab.data() + (size_t)w * h->rs.total);
+        if (h->d_rslab) HIP_TRY(h, hipFree(h->d_rslab));
+        HIP_TRY(h, hipMalloc(&h->d_rslab, rslab.size() * 4));
         HIP_TRY(h, hipMemcpy(h->d_rslab, rslab.data(), rslab.size() * 4, hipMemcpyHostToDevice));
-        std::vector<float> Wt((size_t)h->G * h->NT * h->KX);
+        std::vector<float> Wt((size_t)h->rG * h->NT * h->KX);
         pack_terms_weights(*h, Wt.data());
-        if (!h->d_Wt) HIP_TRY(h, hipMalloc(&h->d_Wt, Wt.size() * 4));
+        if (h->d_Wt) HIP_TRY(h, hipFree(h->d_Wt));
+        HIP_TRY(h, hipMalloc(&h->d_Wt, Wt.size() * 4));
         HIP_TRY(h, hipMemcpy(h->d_Wt, Wt.data(), Wt.size() * 4, hipMemcpyHostToDevice));
     }
     h->ready = true;
@@ -688,13 +803,17 @@ int wrnn_elapsed_ms(wrnn_t *h, float *ms) {
 
 int wrnn_query(const wrnn_t *h, wrnn_info *info) {
     if (!h || !info) return WRNN_EINVAL;
-    info->grid = h->G;
-    info->units_rnn = h->U;
-    info->units_fc = h->UF;
-    info->units_cls = h->UC;
+    const bool rows_only = h->max_rows < 1;      // e.g. rnn 896 with block-sparse GRU weights
+    info->grid = rows_only ? h->rG : h->G;
+    info->units_rnn = rows_only ? h->rU : h->U;
+    info->units_fc = rows_only ? h->rUF : h->UF;
+    info->units_cls = rows_only ? h->rUC : h->UC;
     info->max_rows = h->max_rows;
-    info->lds_bytes = (int)lds_bytes_for(*h, h->max_rows);
-    info->slab_floats = h->s.total;
+    info->lds_bytes = (int)(rows_only ? rows_lds_bytes(*h, 1, 1) : lds_bytes_for(*h, h->max_rows));
+    info->slab_floats = rows_only ? h->rs.total : h->s.total;
+    info->rows_grid = h->rows_ok ? h->rG : 0;
+    info->rows_units_rnn = h->rows_ok ? h->rU : 0;
+    info->sparse_blocks = h->rows_ok ? h->rs.nbmax : 0;
     info->num_cus = h->num_cus;
     return WRNN_OK;
 }

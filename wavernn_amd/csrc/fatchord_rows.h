@@ -23,9 +23,15 @@ enum RowsHop { RH_H1 = 0, RH_H2 = 1, RH_F1 = 2, RH_F2 = 3, RH_LG = 4 };
 
 // Per-workgroup resident weights (floats).  Only the parts that multiply per-step state are
 // here; everything linear in the conditioning is in the precomputed terms.
+//
+// Block-sparse GRU weights (BASELINE config 4, wavernn_amd/pruning.py): with U = 4 a workgroup
+// owns one 4-row block-row per gate of W_ih2[:, :R], W_hh1, W_hh2; only its nonzero 4x4 blocks
+// are kept — sp: [3 matrices][3 gates][nbmax][16] (row-major 4x4), spc: block-column index per
+// block (int bits), spn: [3][3] block counts.  The dense wih2/whh1/whh2 regions are then empty.
 struct RowsSlab {
-    int wih2, whh1, whh2, w1, w2, w3, b3, bih1, bhh1, bih2, bhh2, q1, q2, q3, total;
+    int wih2, whh1, whh2, w1, w2, w3, b3, bih1, bhh1, bih2, bhh2, q1, q2, q3, sp, spc, spn, nbmax, total;
 };
+enum SparseMat { SP_WIH2 = 0, SP_WHH1 = 1, SP_WHH2 = 2 };
 
 // Precomputed per (step, row, workgroup) terms, NT floats: [P1 3U | P2 3U | V1c UF | V2 UF | pad]
 //   P1  = W_ih1[g·R+j]·cI             P2 = W_ih2[g·R+j]·[cI; a2]

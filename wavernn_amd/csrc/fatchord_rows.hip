@@ -62,8 +62,9 @@ __device__ __forceinline__ void store_sc1(float *p, float v) {
 }
 
 // kRF = 512 instantiates the shipped dims (rnn_dims = fc_dims = 512) with compile-time dot
-// lengths; 0 = runtime dims.
-template <bool MOL, int kRF>
+// lengths; 0 = runtime dims.  SPARSE: block-sparse GRU weights (one 4-unit block-row per gate,
+// U = 4), the GRU matvecs run one engine per activation row over the nonzero blocks.
+template <bool MOL, int kRF, bool SPARSE>
 __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, row = lane >> 4;
@@ -73,6 +74,8 @@ __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
     const RowsLds ll = rows_lds_layout(a.s.total, B, TB, R, F, NC, NK, U, UF, G);
     const RowsSlab &s = a.s;
     const float *S = smem + ll.slab;
+    const int *spc = reinterpret_cast<const int *>(S + a.s.spc);     // sparse: block columns, counts
+    const int *spn = reinterpret_cast<const int *>(S + a.s.spn);
     float *tile = smem + ll.tile, *st = smem + ll.st, *xs = smem + ll.x, *ring = smem + ll.ring;
     float *lgs = smem + ll.lg, *nzs = smem + ll.nz;
     int *abort_flag = reinterpret_cast<int *>(smem + ll.flag);
@@ -230,19 +233,36 @@ __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
         {
             float *h2o = actp(RH_H2, t);
             const bool ok = run_stage(RH_H1, R, [&](const float *tl_, int tb0, int nb) {
-                // job types padded to multiples of 4 so the 4 engines of a wave never diverge
-                const int nbb = (nb + kNX - 1) / kNX, n1 = Uv * nbb, nj1 = round4(n1), nj2 = 2 * nj1;
-                const int nj3 = nj2 + nUF2 * nbb;
+                // job types padded to multiples of 4 so the 4 engines of a wave never diverge:
+                // [GRU2 gates | GH1 of the next step | V1h rows]; unit jobs are (unit, 4-row
+                // block) dense, (row) sparse
+                const int nbb = (nb + kNX - 1) / kNX, n1 = SPARSE ? nb : Uv * nbb, nj1 = round4(n1);
+                const int nj2 = 2 * nj1, nj3 = nj2 + nUF2 * nbb;
                 for (int jb = eng; jb < nj3; jb += kDotEngines) {
                     if (jb < nj2) {
-                        const int jj = jb < nj1 ? jb : jb - nj1, u = jj % Uv, bb = jj / Uv;
+                        const bool crit = jb < nj1;
+                        const int jj = crit ? jb : jb - nj1;
                         if (jj >= n1) continue;
-                        const int nx = min(kNX, nb - bb * kNX), b = tb0 + bb * kNX + li;
                         float acc[3];
-                        unit_block(jb < nj1 ? s.wih2 : s.whh1, tl_ + bb * kNX * R, R, nx, u, acc);
-                        if (li < nx) {
+                        int u, b;
+                        bool mine;
+                        if (SPARSE) {
+                            const int m = crit ? SP_WIH2 : SP_WHH1;
+                            sparse_gates4(S + s.sp + m * 3 * s.nbmax * 16, spc + m * 3 * s.nbmax, spn + m * 3, s.nbmax,
+                                          tl_ + jj * R, li, acc);
+                            u = li;
+                            b = tb0 + jj;
+                            mine = li < Uv;
+                        } else {
+                            u = jj % Uv;
+                            const int bb = jj / Uv, nx = min(kNX, nb - bb * kNX);
+                            unit_block(crit ? s.wih2 : s.whh1, tl_ + bb * kNX * R, R, nx, u, acc);
+                            b = tb0 + bb * kNX + li;
+                            mine = li < nx;
+                        }
+                        if (mine) {
                             float *sb = st + b * SW;
-                            if (jb < nj1) {   // GRU2 gates of (b, u)
+                            if (crit) {   // GRU2 gates of (b, u)
                                 const float x = xs[b];
                                 const float *Tb = T + b * NT + 3 * U;
                                 float gi[3], gh[3];
@@ -255,12 +275,12 @@ __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
                                 const float hn = gru_gate_math(gi[0], gi[1], gi[2], gh[0], gh[1], gh[2], sb[O_H2 + u]);
                                 sb[O_H2 + u] = hn;
                                 store_sc1(h2o + (size_t)b * R + w * U + u, hn);
-                            } else {          // GH1 of the next step
+                            } else {      // GH1 of the next step
 #pragma unroll
                                 for (int g = 0; g < 3; ++g) sb[O_GH1 + g * U + u] = acc[g];
                             }
                         }
-                    } else {                  // V1h rows r0, r0+1
+                    } else {              // V1h rows r0, r0+1
                         const int jj = jb - nj2, r0 = 2 * (jj % nUF2), bb = jj / nUF2;
                         const int nx = min(kNX, nb - bb * kNX), b = tb0 + bb * kNX + li;
                         float acc[2];
@@ -282,7 +302,9 @@ __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
         {
             float *f1o = actp(RH_F1, t);
             const bool ok = run_stage(RH_H2, R, [&](const float *tl_, int tb0, int nb) {
-                const int nbb = (nb + kNX - 1) / kNX, n1 = nUF2 * nbb, nj1 = round4(n1), nj2 = nj1 + Uv * nbb;
+                // [fc1 rows | GH2 of the next step]
+                const int nbb = (nb + kNX - 1) / kNX, n1 = nUF2 * nbb, nj1 = round4(n1);
+                const int nj2 = nj1 + (SPARSE ? nb : Uv * nbb);
                 for (int jb = eng; jb < nj2; jb += kDotEngines) {
                     if (jb < nj1) {
                         if (jb >= n1) continue;
@@ -300,11 +322,24 @@ __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
                                 store_sc1(f1o + (size_t)b * F + w * UF + r, v > 0.0f ? v : 0.0f);
                             }
                     } else {
-                        const int jj = jb - nj1, u = jj % Uv, bb = jj / Uv;
-                        const int nx = min(kNX, nb - bb * kNX), b = tb0 + bb * kNX + li;
+                        const int jj = jb - nj1;
                         float acc[3];
-                        unit_block(s.whh2, tl_ + bb * kNX * R, R, nx, u, acc);
-                        if (li < nx)
+                        int u, b;
+                        bool mine;
+                        if (SPARSE) {
+                            sparse_gates4(S + s.sp + SP_WHH2 * 3 * s.nbmax * 16, spc + SP_WHH2 * 3 * s.nbmax,
+                                          spn + SP_WHH2 * 3, s.nbmax, tl_ + jj * R, li, acc);
+                            u = li;
+                            b = tb0 + jj;
+                            mine = li < Uv;
+                        } else {
+                            u = jj % Uv;
+                            const int bb = jj / Uv, nx = min(kNX, nb - bb * kNX);
+                            unit_block(s.whh2, tl_ + bb * kNX * R, R, nx, u, acc);
+                            b = tb0 + bb * kNX + li;
+                            mine = li < nx;
+                        }
+                        if (mine)
 #pragma unroll
                             for (int g = 0; g < 3; ++g) st[b * SW + O_GH2 + g * U + u] = acc[g];
                     }
@@ -460,10 +495,20 @@ hipError_t launch_pack_terms_input(const float *cond, int CD, int Bt, int b0, in
 }
 
 // ------------------------------------------------------------------------ host launchers
+#define WRNN_ROWS_KERNELS                                                                           \
+    (const void *)fatchord_rows_kernel<true, 512, false>, (const void *)fatchord_rows_kernel<true, 0, false>,   \
+        (const void *)fatchord_rows_kernel<false, 512, false>, (const void *)fatchord_rows_kernel<false, 0, false>, \
+        (const void *)fatchord_rows_kernel<true, 0, true>, (const void *)fatchord_rows_kernel<false, 0, true>
+
 static const void *pick_rows_kernel(const RowsArgs &a) {
-    const bool d512 = a.R == 512 && a.F == 512;
-    if (a.mol) return d512 ? (const void *)fatchord_rows_kernel<true, 512> : (const void *)fatchord_rows_kernel<true, 0>;
-    return d512 ? (const void *)fatchord_rows_kernel<false, 512> : (const void *)fatchord_rows_kernel<false, 0>;
+    const bool sparse = a.s.nbmax > 0;
+    const bool d512 = a.R == 512 && a.F == 512 && !sparse;
+    if (a.mol) {
+        if (sparse) return (const void *)fatchord_rows_kernel<true, 0, true>;
+        return d512 ? (const void *)fatchord_rows_kernel<true, 512, false> : (const void *)fatchord_rows_kernel<true, 0, false>;
+    }
+    if (sparse) return (const void *)fatchord_rows_kernel<false, 0, true>;
+    return d512 ? (const void *)fatchord_rows_kernel<false, 512, false> : (const void *)fatchord_rows_kernel<false, 0, false>;
 }
 
 hipError_t launch_rows(const RowsArgs &a, size_t lds_bytes, hipStream_t st) {
@@ -473,8 +518,7 @@ hipError_t launch_rows(const RowsArgs &a, size_t lds_bytes, hipStream_t st) {
 }
 
 hipError_t prepare_rows_kernel(int max_lds_bytes) {
-    for (const void *k : {(const void *)fatchord_rows_kernel<true, 512>, (const void *)fatchord_rows_kernel<true, 0>,
-                          (const void *)fatchord_rows_kernel<false, 512>, (const void *)fatchord_rows_kernel<false, 0>}) {
+    for (const void *k : {WRNN_ROWS_KERNELS}) {
         hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds_bytes);
         if (e != hipSuccess) return e;
     }
@@ -483,8 +527,7 @@ hipError_t prepare_rows_kernel(int max_lds_bytes) {
 
 hipError_t rows_occupancy(int *blocks_per_cu, size_t lds_bytes) {
     int best = 1 << 30;
-    for (const void *k : {(const void *)fatchord_rows_kernel<true, 512>, (const void *)fatchord_rows_kernel<true, 0>,
-                          (const void *)fatchord_rows_kernel<false, 512>, (const void *)fatchord_rows_kernel<false, 0>}) {
+    for (const void *k : {WRNN_ROWS_KERNELS}) {
         int n = 0;
         hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kThreads, lds_bytes);
         if (e != hipSuccess) return e;

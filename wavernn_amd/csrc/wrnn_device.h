@@ -330,6 +330,34 @@ __device__ __forceinline__ void bdot4(const float *__restrict__ W, int ws, const
     for (int i = 0; i < NW; ++i) out[i] = row_reduce_scatter4(acc[i], li);
 }
 
+// Block-sparse gate rows of one 4-unit block-row: out[g] (lane li) = Σ_k blk[g][k] · x[4·col[g][k] …]
+// for unit li & 3, gates g = 0..2.  Lanes of the 16-lane engine split the nonzero blocks; the
+// four unit rows of each block are reduce-scattered so lane li ends up with unit li & 3.
+__device__ __forceinline__ void sparse_gates4(const float *__restrict__ blk, const int *__restrict__ col,
+                                              const int *__restrict__ cnt, int nbmax, const float *__restrict__ x,
+                                              int li, float (&out)[3]) {
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+        float p[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        const float4 *b4 = reinterpret_cast<const float4 *>(blk + (size_t)g * nbmax * 16);
+        const int *cg = col + g * nbmax;
+        for (int k = li; k < cnt[g]; k += 16) {
+            const float4 xv = *reinterpret_cast<const float4 *>(x + 4 * cg[k]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float4 wv = b4[4 * k + r];
+                float a = p[r];
+                a = fmaf(wv.x, xv.x, a);
+                a = fmaf(wv.y, xv.y, a);
+                a = fmaf(wv.z, xv.z, a);
+                a = fmaf(wv.w, xv.w, a);
+                p[r] = a;
+            }
+        }
+        out[g] = row_reduce_scatter4(p, li);
+    }
+}
+
 // ----------------------------------------------------------------------------- samplers
 // One wave samples one row; the result is wave-uniform.
 //

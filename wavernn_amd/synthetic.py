@@ -60,6 +60,8 @@ TINY_RAW = FatchordDims(rnn_dims=64, fc_dims=96, bits=8, compute_dims=16, res_ou
                         res_blocks=1, mode="RAW")
 TINY_MOL = FatchordDims(rnn_dims=64, fc_dims=96, compute_dims=16, res_out_dims=16,
                         res_blocks=1, mode="MOL")
+# BASELINE config 4: rnn_dims 896 with 4x4 block-sparse GRU weights (pruning.prune_state, 95 %)
+SPARSE896_MOL = FatchordDims(rnn_dims=896, mode="MOL")
 
 
 def fatchord_state_shapes(d: FatchordDims) -> Dict[str, Tuple[tuple, str]]:
