@@ -13,6 +13,7 @@ LOOP_CASES = ["loop_raw_tiny_b2", "loop_mol_tiny_b2", "loop_raw_b1", "loop_mol_b
               "loop_raw_b3", "loop_mol_b4"]
 LONG_LOOP_CASES = ["loop_raw_1s", "loop_mol_1s"]
 SPARSE_LOOP_CASES = ["loop_mol_sparse896_b2", "loop_raw_sparse_b2"]
+DM_CASES = ["dm_b1", "dm_tiny_b1"]
 GEN_CASES = ["gen_mol_unbatched", "gen_raw_batched_mulaw", "gen_mol_batched", "gen_raw_tiny_unbatched"]
 
 # MoL parity tolerance per sample under noise injection: ~50-100x the
@@ -25,9 +26,9 @@ def load(name: str) -> dict:
     return {k: z[k] for k in z.files}
 
 
-def dims_of(fx: dict) -> syn.FatchordDims:
+def dims_of(fx: dict):
     text = str(fx["dims"])
-    assert text.startswith("FatchordDims(")
+    assert text.startswith("FatchordDims(") or text.startswith("DeepmindDims(")
     return eval("syn." + text, {"syn": syn})  # repr of a frozen dataclass written by make_golden
 
 
@@ -55,3 +56,14 @@ def gen_inputs(fx: dict):
     assert syn.digest(mel) == str(fx["mel_sha"])
     assert syn.digest(noise) == str(fx["noise_sha"])
     return d, state, mel, noise
+
+
+def dm_inputs(fx: dict):
+    """(dims, state, noise [L][1][2Q]) of a deepmind fixture, regenerated and checked."""
+    d = dims_of(fx)
+    L = int(fx["L"])
+    state = syn.make_deepmind_state(d, int(fx["wseed"]))
+    noise = syn.make_dm_noise(1, L, d.quantisation, int(fx["nseed"]))
+    assert syn.state_digest(state) == str(fx["state_sha"]), "synthetic weight generator drifted"
+    assert syn.digest(noise) == str(fx["noise_sha"]), "synthetic noise drifted"
+    return d, state, noise

@@ -18,6 +18,9 @@ Noise injection (so the fixtures are a pure-arithmetic contract, SURVEY.md §8(b
   * RAW: `torch.distributions.Categorical.sample` is replaced by argmax(probs / q) with
     our q ~ Exp(1) — the exact fast path torch.multinomial(n=1) takes; this script
     re-verifies that equivalence against torch's own sampler before using it.
+  * deepmind (dm_*): `models.deepmind_version.stream` (progress printer, crashes with the
+    reference's own arguments at :159) is replaced by a no-op; the two Categorical.sample
+    calls per step (coarse :130, fine :150) are served q_coarse then q_fine.
 Inputs come from `wavernn_amd.synthetic` (seeded numpy); each fixture stores the
 SHA-256 of its inputs so the tests can prove they regenerate the same inputs.
 """
@@ -192,6 +195,40 @@ def loop_case(fv, name, d: syn.FatchordDims, B: int, L: int, wseed=0, cseed=2, n
     return rec
 
 
+# ------------------------------------------------------------------------- deepmind cases
+def dm_case(fv, name, d: syn.DeepmindDims, L: int, wseed=0, nseed=3):
+    """deepmind_version.WaveRNN.generate(seq_len) (:75-165), batch 1, injected Exp(1) noise."""
+    import models.deepmind_version as dm
+    dm.stream = lambda *a, **k: None
+    state = syn.make_deepmind_state(d, wseed)
+    noise = syn.make_dm_noise(1, L, d.quantisation, nseed)           # [L][1][2Q]
+    Q = d.quantisation
+    draws = noise.reshape(L, 1, 2, Q).transpose(0, 2, 1, 3).reshape(2 * L, 1, Q)   # coarse, fine, …
+    m = dm.WaveRNN(**d.ctor_kwargs())
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in state.items()}, strict=True)
+    orig = torch.distributions.Categorical.sample
+    calls = [0]
+
+    def cat_sample(dist, sample_shape=torch.Size()):
+        q = torch.from_numpy(draws[calls[0]])
+        calls[0] += 1
+        return (dist.probs / q).argmax(-1)
+
+    torch.distributions.Categorical.sample = cat_sample
+    t0 = time.time()
+    try:
+        output, coarse, fine = m.generate(L)
+    finally:
+        torch.distributions.Categorical.sample = orig
+    dt = time.time() - t0
+    assert calls[0] == 2 * L
+    return dict(kind="dm", L=L, wseed=wseed, nseed=nseed, dims=np.array(repr(d)), ref_seconds=dt,
+                state_sha=syn.state_digest(state), noise_sha=syn.digest(noise),
+                coarse=np.asarray(coarse).astype(np.int16).reshape(1, L),
+                fine=np.asarray(fine).astype(np.int16).reshape(1, L),
+                output=np.asarray(output).astype(np.int32).reshape(1, L))
+
+
 # ------------------------------------------------------------------------------ e2e cases
 def gen_case(fv, name, d: syn.FatchordDims, T: int, batched: bool, target: int, overlap: int,
              mu_law: bool, wseed=0, mseed=1, nseed=3, cond_stride=25):
@@ -255,6 +292,9 @@ def cases():
         "gen_raw_batched_mulaw": ("gen", dict(d=R, T=30, batched=True, target=2000, overlap=200, mu_law=True)),
         "gen_mol_batched": ("gen", dict(d=M, T=30, batched=True, target=1500, overlap=300, mu_law=True)),
         "gen_raw_tiny_unbatched": ("gen", dict(d=syn.TINY_RAW, T=24, batched=False, target=1000, overlap=100, mu_law=False)),
+        # deepmind_version dual softmax (config 5 model), batch 1 as the reference generates
+        "dm_b1": ("dm", dict(d=syn.DEFAULT_DM, L=2000)),
+        "dm_tiny_b1": ("dm", dict(d=syn.TINY_DM, L=3000)),
     }
 
 
@@ -266,7 +306,7 @@ def main(argv):
     names = argv or list(todo)
     for name in names:
         kind, kw = todo[name]
-        fn = loop_case if kind == "loop" else gen_case
+        fn = {"loop": loop_case, "gen": gen_case, "dm": dm_case}[kind]
         rec = fn(fv, name, **kw)
         path = os.path.join(HERE, name + ".npz")
         np.savez_compressed(path, **{k: np.asarray(v) for k, v in rec.items()})

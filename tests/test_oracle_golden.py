@@ -31,6 +31,18 @@ def test_long_loop_matches_reference(name):
         assert np.abs(out - fx["samples"]).max() <= gf.MOL_TOL
 
 
+@pytest.mark.parametrize("name", gf.DM_CASES)
+def test_deepmind_loop_matches_reference(name):
+    """deepmind_version.generate (dual coarse/fine softmax): coarse, fine and the combined
+    16-bit output bit-exact."""
+    fx = gf.load(name)
+    d, state, noise = gf.dm_inputs(fx)
+    coarse, fine, output = orc.deepmind_loop(state, 1, int(fx["L"]), noise)
+    np.testing.assert_array_equal(coarse, fx["coarse"].astype(np.int32))
+    np.testing.assert_array_equal(fine, fx["fine"].astype(np.int32))
+    np.testing.assert_array_equal(output, fx["output"].astype(np.int64))
+
+
 @pytest.mark.parametrize("name", gf.GEN_CASES)
 def test_generate_matches_reference(name):
     fx = gf.load(name)

@@ -204,3 +204,54 @@ def digest(*arrays) -> str:
 
 def state_digest(state: Dict[str, np.ndarray]) -> str:
     return digest(*[state[k] for k in sorted(state)])
+
+
+# ---------------------------------------------------------------------- deepmind_version
+@dataclass(frozen=True)
+class DeepmindDims:
+    """Constructor arguments of models/deepmind_version.py:WaveRNN (:9-34)."""
+    hidden_size: int = 896
+    quantisation: int = 256
+
+    @property
+    def split_size(self) -> int:
+        return self.hidden_size // 2
+
+    def ctor_kwargs(self) -> dict:
+        return dict(hidden_size=self.hidden_size, quantisation=self.quantisation)
+
+
+DEFAULT_DM = DeepmindDims()
+TINY_DM = DeepmindDims(hidden_size=64, quantisation=256)
+
+
+def deepmind_state_shapes(d: DeepmindDims) -> Dict[str, tuple]:
+    H, S, Q = d.hidden_size, d.split_size, d.quantisation
+    return {"R.weight": (3 * H, H), "O1.weight": (S, S), "O1.bias": (S,), "O2.weight": (Q, S), "O2.bias": (Q,),
+            "O3.weight": (S, S), "O3.bias": (S,), "O4.weight": (Q, S), "O4.bias": (Q,),
+            "I_coarse.weight": (3 * S, 2), "I_fine.weight": (3 * S, 3),
+            "bias_u": (H,), "bias_r": (H,), "bias_e": (H,)}
+
+
+def make_deepmind_state(d: DeepmindDims, seed: int = 0) -> Dict[str, np.ndarray]:
+    """Random weights U(±1/sqrt(fan_in)) (torch Linear init); the gate biases (zeros in the
+    reference init, :29-31) get U(±0.1) and the two output heads are scaled ×16, so the sampled
+    labels depend on the network arithmetic and not only on the noise."""
+    out: Dict[str, np.ndarray] = {}
+    for key, shape in sorted(deepmind_state_shapes(d).items()):
+        g = _rng(seed, "dm:" + key)
+        if key.startswith("bias_"):
+            out[key] = g.uniform(-0.1, 0.1, size=shape).astype(np.float32)
+            continue
+        fan_in = shape[1] if len(shape) == 2 else deepmind_state_shapes(d)[key.replace("bias", "weight")][1]
+        bound = 1.0 / np.sqrt(float(fan_in))
+        out[key] = g.uniform(-bound, bound, size=shape).astype(np.float32)
+    for k in ("O2.weight", "O4.weight"):
+        out[k] = (out[k] * np.float32(16.0)).astype(np.float32)
+    return out
+
+
+def make_dm_noise(B: int, L: int, Q: int = 256, seed: int = 3) -> np.ndarray:
+    """Exp(1) draws [L][B][2·Q]: the coarse Categorical's q, then the fine one's, per step."""
+    g = np.random.default_rng(seed)
+    return g.exponential(1.0, size=(L, B, 2 * Q)).astype(np.float32)
