@@ -38,6 +38,9 @@ enum wrnn_status {
 enum wrnn_mode {             /* fatchord_version.py:97-104 */
     WRNN_MODE_RAW = 0,       /* softmax over 2**bits classes, Categorical sample (:231-237) */
     WRNN_MODE_MOL = 1,       /* 30-way mixture of logistics (:225-229)                       */
+    WRNN_MODE_DM = 2,        /* deepmind_version.py: dual coarse/fine 8-bit softmax (:75-165);
+                                rnn_dims = hidden_size, n_classes = quantisation; the fc/aux/
+                                feat dims are unused (no conditioning)                         */
 };
 
 typedef struct wrnn_ctx wrnn_t;
@@ -94,14 +97,17 @@ int wrnn_create(const wrnn_config *cfg, int device, wrnn_t **out);
 int wrnn_set_weights(wrnn_t *h, const wrnn_tensor *tensors, int n);
 
 /* Run the whole sample loop (fatchord_version.py:192-241) for B rows × L steps.
- *   cond   [L][B][feat_dims + 4·aux_dims]  upsampled mel ‖ aux, time-major (device)
+ *   cond   [L][B][feat_dims + 4·aux_dims]  upsampled mel ‖ aux, time-major (device);
+ *          NULL in DM mode (deepmind_version.generate(seq_len) has no conditioning)
  *   noise  [L][B][K] injected draws in reference order, or NULL for in-kernel Philox:
  *          MOL K = 11 (u1[10], u2 ∈ (1e-5, 1−1e-5), utils/distribution.py:106,118);
- *          RAW K = n_classes (q ~ Exp(1); Categorical.sample ≡ argmax(probs/q))
+ *          RAW K = n_classes (q ~ Exp(1); Categorical.sample ≡ argmax(probs/q));
+ *          DM  K = 2·n_classes (q_coarse, then q_fine, deepmind_version.py:130,150)
  *   seed, row_offset  Philox key and global id of row 0 (draws are keyed by
  *          (seed, row_offset + b, step, k), so sharding rows across calls/GPUs is invariant)
- *   out    [B][L] fp32 samples (the values appended at :227/:236)          (device)
- *   labels [B][L] int32 class labels, RAW only, or NULL                     (device)
+ *   out    [B][L] fp32 samples (the values appended at :227/:236; DM: the combined 16-bit
+ *          sample coarse·256 + fine − 2^15, utils/dsp.py:33-34)               (device)
+ *   labels [B][L] int32 class labels (RAW) / combined samples (DM), or NULL  (device)
  * Asynchronous on `stream`; kernel-side failures surface through wrnn_check. */
 int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise,
                   uint64_t seed, int64_t row_offset, float *out, int32_t *labels, void *stream);

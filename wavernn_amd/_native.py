@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_lib", "libwavernn_amd.so")
 
 ABI_VERSION = 2
-MODE_RAW, MODE_MOL = 0, 1
+MODE_RAW, MODE_MOL, MODE_DM = 0, 1, 2
 STATUS = {0: "WRNN_OK", -1: "WRNN_EINVAL", -2: "WRNN_EHIP", -3: "WRNN_ENOWEIGHTS", -4: "WRNN_ETIMEOUT",
           -5: "WRNN_ENOMEM", -6: "WRNN_EUNSUPPORTED"}
 

@@ -17,6 +17,7 @@
 #include "../../include/wavernn_amd.h"
 #include "fatchord_loop.h"
 #include "fatchord_rows.h"
+#include "deepmind_rows.h"
 
 namespace wrnn {
 hipError_t launch_ci_gemm(const float *cond, int CD, int Bt, int b0, int Bc, int t0, int L, const float *W, int ldw,
@@ -26,6 +27,9 @@ hipError_t launch_pack_terms_input(const float *cond, int CD, int Bt, int b0, in
 hipError_t launch_rows(const RowsArgs &a, size_t lds_bytes, hipStream_t st);
 hipError_t prepare_rows_kernel(int max_lds_bytes);
 hipError_t rows_occupancy(int *blocks_per_cu, size_t lds_bytes);
+hipError_t launch_dm(const DmArgs &a, size_t lds_bytes, hipStream_t st);
+hipError_t prepare_dm_kernel(int max_lds_bytes);
+hipError_t dm_occupancy(int *blocks_per_cu, size_t lds_bytes);
 hipError_t launch_loop(const LoopArgs &a, size_t lds_bytes, hipStream_t st);
 hipError_t prepare_loop_kernel(int max_lds_bytes);
 hipError_t loop_occupancy(int *blocks_per_cu, size_t lds_bytes);
@@ -66,7 +70,15 @@ struct wrnn_ctx {
     unsigned *d_flags = nullptr;
     unsigned long long *d_xr = nullptr;             // x granules
     rocblas_handle blas = nullptr;
-    int last_path = 0;                              // 1 = latency kernel, 2 = rows kernel
+    int last_path = 0;                              // 1 = latency kernel, 2 = rows kernel, 3 = deepmind
+    // deepmind_version (WRNN_MODE_DM): deepmind_rows.hip
+    DmSlab ds{};
+    int dmU = 0, dmUO = 0, dmUO2 = 0;
+    bool dm = false;
+    float *d_dmslab = nullptr;
+    unsigned *d_dmflags = nullptr;
+    unsigned long long *d_dmxg = nullptr;
+    size_t dmflags_cap = 0, dmxg_cap = 0;
 };
 
 namespace {
@@ -91,6 +103,14 @@ struct Need {
 };
 
 std::vector<Need> required(const wrnn_config &c) {
+    if (c.mode == WRNN_MODE_DM) {   // deepmind_version.py:14-31
+        const int64_t H = c.rnn_dims, S = H / 2, Q = c.n_classes;
+        return {{"R.weight", 3 * H, H},      {"O1.weight", S, S},        {"O1.bias", S, 1},
+                {"O2.weight", Q, S},         {"O2.bias", Q, 1},          {"O3.weight", S, S},
+                {"O3.bias", S, 1},           {"O4.weight", Q, S},        {"O4.bias", Q, 1},
+                {"I_coarse.weight", 3 * S, 2}, {"I_fine.weight", 3 * S, 3}, {"bias_u", H, 1},
+                {"bias_r", H, 1},            {"bias_e", H, 1}};
+    }
     const int64_t R = c.rnn_dims, F = c.fc_dims, A = c.aux_dims, M = c.feat_dims, NC = c.n_classes;
     return {{"I.weight", R, 1 + M + A},      {"I.bias", R, 1},
             {"rnn1.weight_ih_l0", 3 * R, R}, {"rnn1.weight_hh_l0", 3 * R, R},
@@ -388,6 +408,81 @@ int rows_tile_for(const wrnn_ctx &h, int B) {
     return 0;
 }
 
+// ------------------------------------------------------------------ deepmind_version packing
+DmSlab make_dm_slab(const wrnn_ctx &h) {
+    const int H = h.cfg.rnn_dims, S = H / 2;
+    DmSlab s{};
+    int o = 0;
+    auto take = [&](int n) { int at = o; o += round4(n); return at; };
+    s.rw = take(6 * h.dmU * H);
+    s.o1 = take(h.dmUO * S);
+    s.o1b = take(h.dmUO);
+    s.o3 = take(h.dmUO * S);
+    s.o3b = take(h.dmUO);
+    s.o2 = take(h.dmUO2 * S);
+    s.o2b = take(h.dmUO2);
+    s.o4 = take(h.dmUO2 * S);
+    s.o4b = take(h.dmUO2);
+    s.ic = take(3 * h.dmU * 2);
+    s.if_ = take(3 * h.dmU * 3);
+    s.bu = take(2 * h.dmU);
+    s.br = take(2 * h.dmU);
+    s.be = take(2 * h.dmU);
+    s.total = o;
+    return s;
+}
+
+// Workgroup w: coarse units j = w·U + u and fine units S + j; R rows g·H + half·S + j (g = u, r, e,
+// the split of deepmind_version.py:116-119); output rows w·UO + r of O1/O3, w·UO2 + r of O2/O4.
+void pack_dm_slab(const wrnn_ctx &h, int w, float *out) {
+    const int H = h.cfg.rnn_dims, S = H / 2, Q = h.cfg.n_classes, U = h.dmU;
+    const DmSlab &s = h.ds;
+    std::fill(out, out + s.total, 0.0f);
+    auto W = [&](const char *n) { return h.w.at(n).data(); };
+    for (int u = 0; u < U; ++u) {
+        const int j = w * U + u;
+        if (j >= S) continue;
+        for (int half = 0; half < 2; ++half)
+            for (int g = 0; g < 3; ++g) {
+                std::memcpy(out + s.rw + (size_t)((half * 3 + g) * U + u) * H,
+                            W("R.weight") + (size_t)(g * H + half * S + j) * H, H * 4);
+                const float *bias = W(g == 0 ? "bias_u" : g == 1 ? "bias_r" : "bias_e");
+                out[(g == 0 ? s.bu : g == 1 ? s.br : s.be) + half * U + u] = bias[half * S + j];
+            }
+        for (int g = 0; g < 3; ++g) {
+            for (int k = 0; k < 2; ++k) out[s.ic + (g * U + u) * 2 + k] = W("I_coarse.weight")[(g * S + j) * 2 + k];
+            for (int k = 0; k < 3; ++k) out[s.if_ + (g * U + u) * 3 + k] = W("I_fine.weight")[(g * S + j) * 3 + k];
+        }
+    }
+    for (int r = 0; r < h.dmUO; ++r) {
+        const int j = w * h.dmUO + r;
+        if (j >= S) continue;
+        std::memcpy(out + s.o1 + (size_t)r * S, W("O1.weight") + (size_t)j * S, S * 4);
+        std::memcpy(out + s.o3 + (size_t)r * S, W("O3.weight") + (size_t)j * S, S * 4);
+        out[s.o1b + r] = W("O1.bias")[j];
+        out[s.o3b + r] = W("O3.bias")[j];
+    }
+    for (int r = 0; r < h.dmUO2; ++r) {
+        const int j = w * h.dmUO2 + r;
+        if (j >= Q) continue;
+        std::memcpy(out + s.o2 + (size_t)r * S, W("O2.weight") + (size_t)j * S, S * 4);
+        std::memcpy(out + s.o4 + (size_t)r * S, W("O4.weight") + (size_t)j * S, S * 4);
+        out[s.o2b + r] = W("O2.bias")[j];
+        out[s.o4b + r] = W("O4.bias")[j];
+    }
+}
+
+size_t dm_lds_bytes(const wrnn_ctx &h, int B, int TB) {
+    const int S = h.cfg.rnn_dims / 2;
+    return (size_t)dm_lds_layout(h.ds.total, B, TB, S, h.cfg.n_classes, h.dmU, h.G).total * sizeof(float);
+}
+
+int dm_tile_for(const wrnn_ctx &h, int B) {
+    for (int tb = std::min(B, 16); tb >= 1; --tb)
+        if (dm_lds_bytes(h, B, tb) <= (size_t)h.max_lds) return tb;
+    return 0;
+}
+
 size_t lds_bytes_for(const wrnn_ctx &h, int Bc) {
     return (size_t)lds_layout(h.s.total, Bc, h.cfg.rnn_dims, h.cfg.fc_dims, h.cfg.aux_dims, h.cfg.n_classes, h.NK,
                               h.U, h.UF)
@@ -524,6 +619,58 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
     return WRNN_OK;
 }
 
+// deepmind_version: B rows (utterances) in row groups of <= kRowsMax, one launch each
+int generate_dm(wrnn_t *h, int B, int L, const float *noise, uint64_t seed, int64_t row_offset, float *out,
+                int32_t *labels, hipStream_t st) {
+    const int S = h->cfg.rnn_dims / 2, Q = h->cfg.n_classes;
+    for (int b0 = 0; b0 < B;) {
+        int Bl = std::min(B - b0, kRowsMax);
+        while (Bl > 1 && dm_tile_for(*h, Bl) == 0) --Bl;
+        const int TB = dm_tile_for(*h, Bl);
+        if (TB == 0) return fail(h, WRNN_EUNSUPPORTED, "DM: one row of state does not fit LDS");
+        const int SW = dm_state_width(h->dmU);
+        if (grow(h, h->d_act, h->act_cap, (size_t)kDmHops * 2 * Bl * h->KA) ||
+            grow(h, h->d_state, h->state_cap, (size_t)h->G * Bl * SW + 2 * Bl))
+            return WRNN_EHIP;
+        HIP_TRY(h, ensure(h->d_dmflags, h->dmflags_cap, (size_t)kDmHops * kFlagSlots * kFlagStride));
+        HIP_TRY(h, ensure(h->d_dmxg, h->dmxg_cap, (size_t)2 * kXReps * kXRepStride));
+        HIP_TRY(h, hipMemsetAsync(h->d_dmflags, 0, (size_t)kDmHops * kFlagSlots * kFlagStride * 4, st));
+        HIP_TRY(h, hipMemsetAsync(h->d_dmxg, 0, (size_t)2 * kXReps * kXRepStride * 8, st));
+        DmArgs a{};
+        a.slab = h->d_dmslab;
+        a.noise = noise;
+        a.out = out;
+        a.labels = labels;
+        a.act = h->d_act;
+        a.flags = h->d_dmflags;
+        a.xg = h->d_dmxg;
+        a.state = h->d_state;
+        a.ctl = h->d_ctl;
+        a.seed = seed;
+        a.row0 = row_offset + b0;
+        a.timeout_ticks = h->timeout_ticks;
+        a.L = L;
+        a.t0 = 0;
+        a.Lc = L;
+        a.B = Bl;
+        a.Bt = B;
+        a.b0 = b0;
+        a.H = 2 * S;
+        a.S = S;
+        a.Q = Q;
+        a.U = h->dmU;
+        a.UO = h->dmUO;
+        a.UO2 = h->dmUO2;
+        a.G = h->G;
+        a.TB = TB;
+        a.KA = h->KA;
+        a.s = h->ds;
+        HIP_TRY(h, launch_dm(a, dm_lds_bytes(*h, Bl, TB), st));
+        b0 += Bl;
+    }
+    return WRNN_OK;
+}
+
 int generate_latency(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed,
                      int64_t row_offset, float *out, int32_t *labels, hipStream_t st) {
     const wrnn_config &c = h->cfg;
@@ -613,10 +760,12 @@ int wrnn_create(const wrnn_config *cfg, int device, wrnn_t **out) {
     h->device = device;
     const wrnn_config &c = h->cfg;
     const bool mol = c.mode == WRNN_MODE_MOL;
-    if (c.mode != WRNN_MODE_MOL && c.mode != WRNN_MODE_RAW) return fail(h, WRNN_EINVAL, "unknown mode");
-    if (c.rnn_dims <= 0 || c.fc_dims <= 0 || c.aux_dims <= 0 || c.feat_dims <= 0 || c.n_classes <= 0)
+    if (c.mode != WRNN_MODE_MOL && c.mode != WRNN_MODE_RAW && c.mode != WRNN_MODE_DM)
+        return fail(h, WRNN_EINVAL, "unknown mode");
+    if (c.rnn_dims <= 0 || c.n_classes <= 0 ||
+        (c.mode != WRNN_MODE_DM && (c.fc_dims <= 0 || c.aux_dims <= 0 || c.feat_dims <= 0)))
         return fail(h, WRNN_EINVAL, "dims must be positive");
-    if (c.rnn_dims % 4 || c.fc_dims % 4 || c.aux_dims % 4)
+    if (c.mode != WRNN_MODE_DM && (c.rnn_dims % 4 || c.fc_dims % 4 || c.aux_dims % 4))
         return fail(h, WRNN_EUNSUPPORTED, "rnn_dims, fc_dims and aux_dims must be multiples of 4");
     if (mol && c.n_classes != 30) return fail(h, WRNN_EINVAL, "MOL mode has n_classes = 30 (10 logistics)");
     if (!mol && c.n_classes > 64 * kClsPerLaneMax)
@@ -627,6 +776,33 @@ int wrnn_create(const wrnn_config *cfg, int device, wrnn_t **out) {
     h->num_cus = prop.multiProcessorCount;
     h->max_lds = std::max<int>((int)prop.sharedMemPerBlock, (int)prop.maxSharedMemoryPerMultiProcessor);
     h->max_lds = std::min(h->max_lds, 160 * 1024);
+    if (c.mode == WRNN_MODE_DM) {   // deepmind_version: the multi-row dual-softmax kernel only
+        const int H = c.rnn_dims, S = H / 2, Q = c.n_classes;
+        if (S % 4) return fail(h, WRNN_EUNSUPPORTED, "DM hidden_size must be a multiple of 8");
+        if (Q > 256) return fail(h, WRNN_EUNSUPPORTED, "DM quantisation > 256 not supported");
+        const int gt = c.grid > 0 ? c.grid : h->num_cus;
+        h->dm = true;
+        h->dmU = (S + gt - 1) / gt;
+        h->G = (S + h->dmU - 1) / h->dmU;
+        h->dmUO = (S + h->G - 1) / h->G;
+        h->dmUO2 = (Q + h->G - 1) / h->G;
+        h->KA = round4(std::max(S, Q));
+        h->NK = 2 * Q;
+        h->ds = make_dm_slab(*h);
+        if (dm_tile_for(*h, 1) == 0)
+            return fail(h, WRNN_EUNSUPPORTED, "DM weight slab exceeds LDS (" + std::to_string(dm_lds_bytes(*h, 1, 1)) + " B)");
+        HIP_TRY(h, prepare_dm_kernel(h->max_lds));
+        int per_cu = 0;
+        HIP_TRY(h, dm_occupancy(&per_cu, dm_lds_bytes(*h, 1, 1)));
+        if (per_cu * h->num_cus < h->G)
+            return fail(h, WRNN_EUNSUPPORTED, "DM persistent grid is not co-resident");
+        h->timeout_ticks = (long long)(c.timeout_ms > 0 ? c.timeout_ms : 2000) * 100000LL;
+        HIP_TRY(h, hipMalloc(&h->d_ctl, kCtlWords * sizeof(int)));
+        HIP_TRY(h, hipMemset(h->d_ctl, 0, kCtlWords * sizeof(int)));
+        HIP_TRY(h, hipEventCreate(&h->ev0));
+        HIP_TRY(h, hipEventCreate(&h->ev1));
+        return WRNN_OK;
+    }
     const int R = c.rnn_dims, F = c.fc_dims;
     const int gtarget = c.grid > 0 ? c.grid : h->num_cus;
     h->U = (R + gtarget - 1) / gtarget;
@@ -699,6 +875,15 @@ int wrnn_set_weights(wrnn_t *h, const wrnn_tensor *tensors, int n) {
     }
     for (const auto &q : need)
         if (!h->w.count(q.name)) { h->ready = false; return WRNN_OK; }   // partial load so far
+    if (h->dm) {
+        std::vector<float> slab((size_t)h->G * h->ds.total);
+        for (int w = 0; w < h->G; ++w) pack_dm_slab(*h, w, slab.data() + (size_t)w * h->ds.total);
+        if (h->d_dmslab) HIP_TRY(h, hipFree(h->d_dmslab));
+        HIP_TRY(h, hipMalloc(&h->d_dmslab, slab.size() * 4));
+        HIP_TRY(h, hipMemcpy(h->d_dmslab, slab.data(), slab.size() * 4, hipMemcpyHostToDevice));
+        h->ready = true;
+        return WRNN_OK;
+    }
     // pack and upload
     if (h->max_rows >= 1) {
         std::vector<float> slab((size_t)h->G * h->s.total);
@@ -751,8 +936,8 @@ int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise
                   int64_t row_offset, float *out, int32_t *labels, void *stream) {
     if (!h) return WRNN_EINVAL;
     if (!h->ready) return fail(h, WRNN_ENOWEIGHTS, "weights not (fully) set");
-    if (B <= 0 || L <= 0 || !cond || !out) return fail(h, WRNN_EINVAL, "need B > 0, L > 0, cond and out");
-    if (labels && h->cfg.mode != WRNN_MODE_RAW) return fail(h, WRNN_EINVAL, "labels are a RAW-mode output");
+    if (B <= 0 || L <= 0 || !out || (!cond && !h->dm)) return fail(h, WRNN_EINVAL, "need B > 0, L > 0, cond and out");
+    if (labels && h->cfg.mode == WRNN_MODE_MOL) return fail(h, WRNN_EINVAL, "labels are a RAW / DM output");
     HIP_TRY(h, hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
     // path: the latency kernel while the rows fit its LDS layout in one launch, else the
@@ -764,9 +949,10 @@ int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise
     if (rows && !h->rows_ok) rows = false;
     HIP_TRY(h, hipMemsetAsync(h->d_ctl, 0, kCtlWords * sizeof(int), st));
     HIP_TRY(h, hipEventRecord(h->ev0, st));
-    h->last_path = rows ? 2 : 1;
-    const int rc = rows ? generate_rows(h, cond, B, L, noise, seed, row_offset, out, labels, st)
-                        : generate_latency(h, cond, B, L, noise, seed, row_offset, out, labels, st);
+    h->last_path = h->dm ? 3 : rows ? 2 : 1;
+    const int rc = h->dm  ? generate_dm(h, B, L, noise, seed, row_offset, out, labels, st)
+                   : rows ? generate_rows(h, cond, B, L, noise, seed, row_offset, out, labels, st)
+                          : generate_latency(h, cond, B, L, noise, seed, row_offset, out, labels, st);
     if (rc != WRNN_OK) return rc;
     HIP_TRY(h, hipEventRecord(h->ev1, st));
     h->timed = true;
@@ -783,8 +969,11 @@ int wrnn_check(wrnn_t *h, void *stream) {
         static const char *lat_hops[] = {"q1", "h2", "f1", "f2", "logits", "gru1-terms", "gru1-terms"};
         static const char *row_hops[] = {"h1", "h2", "f1", "f2", "logits", "x"};
         const int hop = ctl[3];
-        const char *name = h->last_path == 2 ? (hop >= 0 && hop < 6 ? row_hops[hop] : "?")
-                                             : (hop >= 0 && hop < 7 ? lat_hops[hop] : "?");
+        static const char *dm_hops[] = {"h_coarse", "o1", "coarse logits", "h_fine", "o3", "fine logits",
+                                        "coarse label", "fine label"};
+        const char *name = h->last_path == 3   ? (hop >= 0 && hop < 8 ? dm_hops[hop] : "?")
+                           : h->last_path == 2 ? (hop >= 0 && hop < 6 ? row_hops[hop] : "?")
+                                               : (hop >= 0 && hop < 7 ? lat_hops[hop] : "?");
         return fail(h, WRNN_ETIMEOUT,
                     "persistent kernel aborted: wait on hand-off '" + std::string(name) +
                         "' at step " + std::to_string(ctl[2]) + " in workgroup " + std::to_string(ctl[4]) +
@@ -803,6 +992,19 @@ int wrnn_elapsed_ms(wrnn_t *h, float *ms) {
 
 int wrnn_query(const wrnn_t *h, wrnn_info *info) {
     if (!h || !info) return WRNN_EINVAL;
+    if (h->dm) {
+        *info = wrnn_info{};
+        info->grid = h->G;
+        info->units_rnn = h->dmU;
+        info->units_fc = h->dmUO;
+        info->units_cls = h->dmUO2;
+        info->lds_bytes = (int)dm_lds_bytes(*h, 1, 1);
+        info->slab_floats = h->ds.total;
+        info->num_cus = h->num_cus;
+        info->rows_grid = h->G;
+        info->rows_units_rnn = h->dmU;
+        return WRNN_OK;
+    }
     const bool rows_only = h->max_rows < 1;      // e.g. rnn 896 with block-sparse GRU weights
     info->grid = rows_only ? h->rG : h->G;
     info->units_rnn = rows_only ? h->rU : h->U;
@@ -827,7 +1029,8 @@ void wrnn_destroy(wrnn_t *h) {
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     for (void *p : {(void *)h->d_slab, (void *)h->d_IW, (void *)h->d_Ib, (void *)h->d_cI, (void *)h->d_xg,
                     (void *)h->d_ctl, (void *)h->d_rslab, (void *)h->d_Wt, (void *)h->d_X, (void *)h->d_T,
-                    (void *)h->d_act, (void *)h->d_state, (void *)h->d_flags, (void *)h->d_xr})
+                    (void *)h->d_act, (void *)h->d_state, (void *)h->d_flags, (void *)h->d_xr, (void *)h->d_dmslab,
+                    (void *)h->d_dmflags, (void *)h->d_dmxg})
         if (p) (void)hipFree(p);
     if (h->blas) (void)rocblas_destroy_handle(h->blas);
     delete h;

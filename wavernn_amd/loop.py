@@ -20,12 +20,18 @@ LOOP_KEYS = ("I.weight", "I.bias", "rnn1.weight_ih_l0", "rnn1.weight_hh_l0", "rn
              "fc3.bias")
 
 
+DM_KEYS = ("R.weight", "O1.weight", "O1.bias", "O2.weight", "O2.bias", "O3.weight", "O3.bias", "O4.weight",
+           "O4.bias", "I_coarse.weight", "I_fine.weight", "bias_u", "bias_r", "bias_e")
+
+
 def noise_width(mode: str, n_classes: int) -> int:
     """K of the injected-noise layout [L][B][K] (reference draw order)."""
     return 11 if mode == "MOL" else n_classes
 
 
 class FatchordLoop:
+    keys = LOOP_KEYS
+
     def __init__(self, mode: str, rnn_dims: int, fc_dims: int, aux_dims: int, feat_dims: int,
                  n_classes: int, device: int = 0, grid: int = 0, timeout_ms: int = 0):
         if mode not in ("RAW", "MOL"):
@@ -35,8 +41,10 @@ class FatchordLoop:
         self.device = device
         self.cond_dims = feat_dims + 4 * aux_dims
         self.noise_k = noise_width(mode, n_classes)
-        cfg = nat.Config(nat.ABI_VERSION, nat.MODE_MOL if mode == "MOL" else nat.MODE_RAW, rnn_dims,
-                         fc_dims, aux_dims, feat_dims, n_classes, grid, timeout_ms)
+        self._create(nat.Config(nat.ABI_VERSION, nat.MODE_MOL if mode == "MOL" else nat.MODE_RAW, rnn_dims,
+                                fc_dims, aux_dims, feat_dims, n_classes, grid, timeout_ms), device)
+
+    def _create(self, cfg, device: int) -> None:
         L = nat.lib()
         h = ctypes.c_void_p()
         rc = L.wrnn_create(ctypes.byref(cfg), device, ctypes.byref(h))
@@ -52,9 +60,9 @@ class FatchordLoop:
     def set_weights(self, state: Mapping[str, object]) -> None:
         """Pack the loop's tensors (reference state_dict names) into the kernel layout."""
         keep = []
-        arr = (nat.Tensor * len(LOOP_KEYS))()
+        arr = (nat.Tensor * len(self.keys))()
         n = 0
-        for k in LOOP_KEYS:
+        for k in self.keys:
             if k not in state:
                 raise KeyError(f"missing weight {k!r}")
             v = state[k]
@@ -132,3 +140,39 @@ class FatchordLoop:
             self.close()
         except Exception:
             pass
+
+
+class DeepmindLoop(FatchordLoop):
+    """Handle on the dual-softmax kernel (deepmind_rows.hip) replacing the per-step loop of
+    models/deepmind_version.py:generate (:98-156) for B independent rows."""
+    keys = DM_KEYS
+
+    def __init__(self, hidden_size: int = 896, quantisation: int = 256, device: int = 0, grid: int = 0,
+                 timeout_ms: int = 0):
+        self.mode, self.hidden_size, self.n_classes = "DM", hidden_size, quantisation
+        self.device = device
+        self.noise_k = 2 * quantisation
+        self._create(nat.Config(nat.ABI_VERSION, nat.MODE_DM, hidden_size, 0, 0, 0, quantisation, grid, timeout_ms),
+                     device)
+
+    def generate(self, B: int, L: int, noise: Optional[torch.Tensor] = None, seed: int = 0, row_offset: int = 0,
+                 stream=None, check: bool = True,
+                 device: Optional[torch.device] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """→ (samples [B][L] fp32, combined int32 [B][L]): coarse·256 + fine − 2^15 per step."""
+        dev = device or torch.device("cuda", self.device)
+        if noise is not None:
+            if not (noise.is_cuda and noise.dtype == torch.float32 and noise.is_contiguous()):
+                raise ValueError("noise must be a contiguous fp32 CUDA tensor [L][B][2Q]")
+            if tuple(noise.shape) != (L, B, self.noise_k):
+                raise ValueError(f"noise shape {tuple(noise.shape)} != {(L, B, self.noise_k)}")
+        out = torch.empty(B, L, dtype=torch.float32, device=dev)
+        labels = torch.empty(B, L, dtype=torch.int32, device=dev)
+        if stream is None:
+            stream = torch.cuda.current_stream(dev).cuda_stream
+        rc = nat.lib().wrnn_generate(self._h, None, B, L, noise.data_ptr() if noise is not None else None,
+                                     ctypes.c_uint64(seed & (2 ** 64 - 1)), row_offset, out.data_ptr(),
+                                     labels.data_ptr(), stream)
+        nat.check(self._h, rc)
+        if check:
+            self.check(stream)
+        return out, labels
