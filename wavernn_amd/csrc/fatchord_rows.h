@@ -12,7 +12,7 @@ namespace wrnn {
 // lane stores the step into the workgroup's flag; consumers poll every producer's flag, then
 // load the rows with sc1 LDS-DMA (MI355X_MICROARCH.md "Valid forms", first table row).
 constexpr int kRowsHops = 5;        // h1, h2, f1, f2, logits (RAW)
-constexpr int kFlagStride = 16;     // uints between two producers' flags (64 B)
+constexpr int kFlagStride = 32;     // uints between two producers' flags (one 128-B line each)
 constexpr int kFlagSlots = 256;     // producer slots per hop: >= G, fixed so polls may over-read
 constexpr int kRowsMax = 256;       // rows per launch (x hand-off: <= 4 granules per polling lane)
 constexpr int kXReps = 8;           // replicas of the x granules
