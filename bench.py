@@ -50,6 +50,61 @@ def loop_weight_bytes(d: syn.FatchordDims) -> int:
     return 4 * n
 
 
+def other_configs(dev) -> dict:
+    """BASELINE configs 3-5 on one GPU (synthetic inputs, random weights of each architecture):
+      3: MoL fold-batched generate() of one 60 s utterance (115 folds x 12 100 steps);
+      4: rnn 896 with 95 % 4x4 block-sparse GRU weights, 8 utterances of 5 s (8 rows) per GPU;
+      5: deepmind dual softmax, 32 utterances of 1 s at 16 kHz (32 rows) per GPU."""
+    from wavernn_amd.fatchord_version import WaveRNN
+    from wavernn_amd.loop import DeepmindLoop, FatchordLoop
+    from wavernn_amd.pruning import prune_state
+    res = {}
+    # config 3
+    d = syn.DEFAULT_MOL
+    model = WaveRNN(**d.ctor_kwargs()).to(dev)
+    model.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in syn.make_fatchord_state(d, 0).items()})
+    mel = torch.from_numpy(syn.make_mel(d.feat_dims, syn.frames_for_seconds(60.0, d.sample_rate, d.hop_length), 3))[None]
+    model.generate(mel, None, True, 11000, 550, True, seed=1, verbose=False)     # warm (MIOpen tunes per shape)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    out = model.generate(mel, None, True, 11000, 550, True, seed=2, verbose=False)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t
+    ms = model.loop_handle().elapsed_ms()
+    res["config3_mol_fold_60s"] = {"samples_per_s": out.shape[0] / dt, "rtf": out.shape[0] / dt / d.sample_rate,
+                                   "rows": 115, "loop_steps": 12100, "device_ms": ms, "wall_s": dt,
+                                   "us_per_loop_step": ms * 1e3 / 12100}
+    del model
+    # config 4
+    d4 = syn.SPARSE896_MOL
+    L4, B4 = syn.frames_for_seconds(5.0, d4.sample_rate, d4.hop_length) * d4.hop_length, 8
+    loop = FatchordLoop(d4.mode, d4.rnn_dims, d4.fc_dims, d4.aux_dims, d4.feat_dims, d4.n_classes)
+    loop.set_weights(prune_state(syn.make_fatchord_state(d4, 0), 0.95))
+    mels, aux = syn.make_conditioning(B4, L4, d4.feat_dims, d4.res_out_dims, 4)
+    cond = torch.from_numpy(np.concatenate([mels, aux], 2).transpose(1, 0, 2).copy()).to(dev)
+    loop.generate(cond[:100].contiguous(), seed=1)
+    ms = 0.0
+    loop.generate(cond, seed=2)
+    ms = loop.elapsed_ms()
+    res["config4_sparse896_8utt"] = {"samples_per_s": B4 * L4 / ms * 1e3, "rtf": B4 * L4 / ms * 1e3 / d4.sample_rate,
+                                     "rows": B4, "loop_steps": L4, "device_ms": ms, "us_per_loop_step": ms * 1e3 / L4,
+                                     "sparse_blocks_per_gate_row": loop.info["sparse_blocks"],
+                                     "note": "loop launch from upsampled conditioning (upsample excluded)"}
+    loop.close()
+    # config 5
+    dm = syn.DEFAULT_DM
+    B5, L5 = 32, 16000
+    loop5 = DeepmindLoop(dm.hidden_size, dm.quantisation)
+    loop5.set_weights(syn.make_deepmind_state(dm, 0))
+    loop5.generate(B5, 100, seed=1)
+    loop5.generate(B5, L5, seed=2)
+    ms = loop5.elapsed_ms()
+    res["config5_deepmind_32utt"] = {"samples_per_s": B5 * L5 / ms * 1e3, "rtf": B5 * L5 / ms * 1e3 / 16000.0,
+                                     "rows": B5, "loop_steps": L5, "device_ms": ms, "us_per_loop_step": ms * 1e3 / L5}
+    loop5.close()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -59,6 +114,7 @@ def main():
     ap.add_argument("--mode", default="MOL", choices=["MOL", "RAW"])
     ap.add_argument("--batched", action="store_true", help="fold-batched generate (target 11000, overlap 550)")
     ap.add_argument("--cpu-steps", type=int, default=50000, help="oracle steps timed for cpu_baseline (0: skip)")
+    ap.add_argument("--other-configs", type=int, default=1, help="also time BASELINE configs 3/4/5 on this GPU (N=1)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -173,6 +229,8 @@ def main():
                 "note": "same 5 s utterance, generate(batched=True) as gen_wavernn.py runs it with the 800k "
                         "hparams; one multi-row persistent launch (fatchord_rows.hip) + conditioning-terms GEMM",
             }
+        if args.other_configs and world == 1 and args.mode == "MOL":
+            rec["other_configs"] = other_configs(dev)
         if args.cpu_steps > 0 and world == 1:
             from oracle import oracle
             cpu = cond.transpose(0, 1).cpu().numpy()
