@@ -110,6 +110,23 @@ def test_rows_time_chunks_carry_state(mode, monkeypatch):
         assert np.abs(out.cpu().numpy() - ref).max() <= gf.MOL_TOL
 
 
+def test_rows_mol_head_from_hbm(monkeypatch):
+    """MoL with more rows than one LDS tile next to the replicated head (rnn 512, B = 24): the
+    launch leaves the head in HBM for bigger tiles; samples still match the oracle."""
+    from oracle import oracle
+    monkeypatch.setenv("WRNN_PATH", "rows")
+    d = syn.DEFAULT_MOL
+    B, L = 24, 150
+    state = syn.make_fatchord_state(d, 61)
+    mels, aux = syn.make_conditioning(B, L, d.feat_dims, d.res_out_dims, 62)
+    noise = syn.make_noise("MOL", B, L, d.n_classes, 63)
+    ref, _ = oracle.fatchord_loop(state, "MOL", mels, aux, noise)
+    loop = _loop(d)
+    loop.set_weights(state)
+    out, _ = loop.generate(_cond(mels, aux), noise=torch.from_numpy(noise).to(DEV))
+    assert np.abs(out.cpu().numpy() - ref).max() <= gf.MOL_TOL
+
+
 def test_rows_many_rows_tiled():
     """More rows than one LDS tile and more than one sampled row per workgroup (tiny dims,
     G = 64 workgroups, B = 150): oracle parity."""

@@ -210,8 +210,10 @@ RowsSlab make_rows_slab(const wrnn_ctx &h, int nbmax) {
     s.nbmax = nbmax;
     s.w1 = take(h.rUF * R);
     s.w2 = take(h.rUF * F);
-    s.w3 = take((mol ? NC : h.rUC) * F);
-    s.b3 = take(mol ? NC : h.rUC);
+    if (!mol) {
+        s.w3 = take(h.rUC * F);
+        s.b3 = take(h.rUC);
+    }
     s.bih1 = take(3 * h.rU);
     s.bhh1 = take(3 * h.rU);
     s.bih2 = take(3 * h.rU);
@@ -219,6 +221,11 @@ RowsSlab make_rows_slab(const wrnn_ctx &h, int nbmax) {
     s.q1 = take(3 * h.rU);
     s.q2 = take(3 * h.rU);
     s.q3 = take(h.rUF);
+    s.body = o;          // everything before the MoL head: always LDS-resident
+    if (mol) {           // the replicated 30-row head last, so a launch may leave it in HBM
+        s.w3 = take(NC * F);
+        s.b3 = take(NC);
+    }
     s.total = o;
     return s;
 }
@@ -374,15 +381,15 @@ void pack_terms_weights(const wrnn_ctx &h, float *Wt) {
         }
 }
 
-size_t rows_lds_bytes(const wrnn_ctx &h, int B, int TB) {
-    return (size_t)rows_lds_layout(h.rs.total, B, TB, h.cfg.rnn_dims, h.cfg.fc_dims, h.cfg.n_classes, h.NK, h.rU,
-                                   h.rUF, h.rG)
+size_t rows_lds_bytes(const wrnn_ctx &h, int B, int TB, bool head_lds = true) {
+    return (size_t)rows_lds_layout(head_lds ? h.rs.total : h.rs.body, B, TB, h.cfg.rnn_dims, h.cfg.fc_dims,
+                                   h.cfg.n_classes, h.NK, h.rU, h.rUF, h.rG)
                .total * sizeof(float);
 }
 
 // (Re)derive the rows-kernel partition: dense = the latency kernel's; sparse = one 4-unit
 // block-row per workgroup (G = R / 4).  Sets rows_ok.
-int rows_tile_for(const wrnn_ctx &h, int B);
+int rows_tile_for(const wrnn_ctx &h, int B, bool head_lds = true);
 void set_rows_partition(wrnn_ctx &h, int nbmax) {
     const int R = h.cfg.rnn_dims, F = h.cfg.fc_dims;
     const bool mol = h.cfg.mode == WRNN_MODE_MOL;
@@ -401,10 +408,11 @@ void set_rows_partition(wrnn_ctx &h, int nbmax) {
     h.rows_ok = rows_tile_for(h, 1) > 0;
 }
 
-// Largest tile (<= 16 rows) that fits next to B rows of state; 0 if none does
-int rows_tile_for(const wrnn_ctx &h, int B) {
-    for (int tb = std::min(B, 16); tb >= 1; --tb)
-        if (rows_lds_bytes(h, B, tb) <= (size_t)h.max_lds) return tb;
+// Largest tile (<= 16 rows; up to 32 with the MoL head left in HBM) that fits next to B rows of
+// state; 0 if none does
+int rows_tile_for(const wrnn_ctx &h, int B, bool head_lds) {
+    for (int tb = std::min(B, head_lds ? 16 : 32); tb >= 1; --tb)
+        if (rows_lds_bytes(h, B, tb, head_lds) <= (size_t)h.max_lds) return tb;
     return 0;
 }
 
@@ -554,8 +562,13 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
     }
     for (int b0 = 0; b0 < B;) {
         int Bl = std::min(B - b0, kRowsMax);
-        while (Bl > 1 && rows_tile_for(*h, Bl) == 0) --Bl;
-        const int TB = rows_tile_for(*h, Bl);
+        while (Bl > 1 && rows_tile_for(*h, Bl) == 0 && rows_tile_for(*h, Bl, false) == 0) --Bl;
+        // the MoL head stays in LDS while all rows fit one tile next to it; beyond that, larger
+        // tiles are worth more than an LDS-resident head (the samplers then read it from L2)
+        const bool mol = c.mode == WRNN_MODE_MOL;
+        const int tb_in = rows_tile_for(*h, Bl);
+        const bool head_lds = !mol || tb_in >= std::min(Bl, 16) || rows_tile_for(*h, Bl, false) == 0;
+        const int TB = head_lds ? tb_in : rows_tile_for(*h, Bl, false);
         if (TB == 0) return fail(h, WRNN_EUNSUPPORTED, "rows kernel: one row of state does not fit LDS");
         const int SW = rows_state_width(h->rU, h->rUF);
         const int Lc_max = (int)std::max(1.0, std::min((double)L, budget / ((double)Bl * (N + h->KX))));
@@ -611,7 +624,8 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
             a.s = h->rs;
             a.dbg = (b0 == 0 && t0 == 0) ? d_dbg : nullptr;
             a.dbg_steps = std::min(dbg_steps, Lc);
-            HIP_TRY(h, launch_rows(a, rows_lds_bytes(*h, Bl, TB), st));
+            a.head_lds = head_lds ? 1 : 0;
+            HIP_TRY(h, launch_rows(a, rows_lds_bytes(*h, Bl, TB, head_lds), st));
         }
         b0 += Bl;
     }

@@ -29,7 +29,9 @@ enum RowsHop { RH_H1 = 0, RH_H2 = 1, RH_F1 = 2, RH_F2 = 3, RH_LG = 4 };
 // are kept — sp: [3 matrices][3 gates][nbmax][16] (row-major 4x4), spc: block-column index per
 // block (int bits), spn: [3][3] block counts.  The dense wih2/whh1/whh2 regions are then empty.
 struct RowsSlab {
-    int wih2, whh1, whh2, w1, w2, w3, b3, bih1, bhh1, bih2, bhh2, q1, q2, q3, sp, spc, spn, nbmax, total;
+    int wih2, whh1, whh2, w1, w2, w3, b3, bih1, bhh1, bih2, bhh2, q1, q2, q3, sp, spc, spn, nbmax;
+    int body;      // floats before the MoL head (which is last); RAW: == total
+    int total;
 };
 enum SparseMat { SP_WIH2 = 0, SP_WHH1 = 1, SP_WHH2 = 2 };
 
@@ -62,6 +64,7 @@ struct RowsArgs {
     RowsSlab s;
     unsigned *dbg;                // WRNN_DEBUG_STAMPS: [G][dbg_steps][kStamps] s_memrealtime per stage
     int dbg_steps;
+    int head_lds;                 // MoL: 1 = head in LDS, 0 = samplers read it from HBM (workgroup 0's slab)
 };
 
 struct RowsLds {

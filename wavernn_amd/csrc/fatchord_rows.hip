@@ -39,9 +39,12 @@ __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
     const int w = blockIdx.x;
     const int R = kRF ? kRF : a.R, F = kRF ? kRF : a.F, NC = a.NC, NK = a.NK, U = a.U, UF = a.UF, UC = a.UC, G = a.G, B = a.B;
     const int NT = a.NT, TB = a.TB, KA = a.KA;
-    const RowsLds ll = rows_lds_layout(a.s.total, B, TB, R, F, NC, NK, U, UF, G);
+    const int slab_lds = (MOL && !a.head_lds) ? a.s.body : a.s.total;   // floats resident in LDS
+    const RowsLds ll = rows_lds_layout(slab_lds, B, TB, R, F, NC, NK, U, UF, G);
     const RowsSlab &s = a.s;
     const float *S = smem + ll.slab;
+    // MoL head [NC][F] then bias [NC]: LDS, or (large B) the HBM copy in workgroup 0's slab
+    const float *head = (MOL && !a.head_lds) ? a.slab + a.s.w3 : S + a.s.w3;
     const int *spc = reinterpret_cast<const int *>(S + a.s.spc);     // sparse: block columns, counts
     const int *spn = reinterpret_cast<const int *>(S + a.s.spn);
     float *tile = smem + ll.tile, *st = smem + ll.st, *xs = smem + ll.x, *ring = smem + ll.ring;
@@ -99,7 +102,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
     {
         const float4 *src = reinterpret_cast<const float4 *>(a.slab + (size_t)w * s.total);
         float4 *dst = reinterpret_cast<float4 *>(smem + ll.slab);
-        for (int i = tid; i < s.total / 4; i += kThreads) dst[i] = src[i];
+        for (int i = tid; i < slab_lds / 4; i += kThreads) dst[i] = src[i];
         const float *cs = a.state + (size_t)w * B * SW;
         for (int i = tid; i < B * SW; i += kThreads) st[i] = a.t0 > 0 ? cs[i] : 0.0f;
         const float *cx = a.state + (size_t)G * B * SW;
@@ -386,9 +389,9 @@ __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
                     for (int sr = 0; sr < NS && w + sr * G < B; ++sr)
                         for (int c0 = eng; c0 < NC; c0 += 2 * kDotEngines) {
                             const int ca = c0, cb = min(c0 + kDotEngines, NC - 1);
-                            const float2 v = row_dot2(S + s.w3 + ca * F, S + s.w3 + cb * F, tile + sr * ll.KT, F / 4, li);
-                            if (li == 0) lgs[sr * ll.ncp + ca] = v.x + S[s.b3 + ca];
-                            if (li == 0 && c0 + kDotEngines < NC) lgs[sr * ll.ncp + cb] = v.y + S[s.b3 + cb];
+                            const float2 v = row_dot2(head + ca * F, head + cb * F, tile + sr * ll.KT, F / 4, li);
+                            if (li == 0) lgs[sr * ll.ncp + ca] = v.x + head[s.b3 - s.w3 + ca];
+                            if (li == 0 && c0 + kDotEngines < NC) lgs[sr * ll.ncp + cb] = v.y + head[s.b3 - s.w3 + cb];
                         }
                 bar();
             }
