@@ -164,6 +164,73 @@ def test_paths_agree_under_philox(mode, monkeypatch):
         assert (res["latency"][0] - res["rows"][0]).abs().max().item() <= 2 * gf.MOL_TOL
 
 
+SPLIT_CASES = ["loop_mol_b1", "loop_mol_b4", "loop_mol_1s"]
+
+
+def _split_loop(d):
+    loop = _loop(d)
+    assert loop.info["split_grid"] == 512 // 4 + 512 // 16, loop.info
+    return loop
+
+
+@pytest.mark.parametrize("name", SPLIT_CASES)
+def test_split_vs_reference_fixture(name, monkeypatch):
+    """The batch-1 role-split kernel (GRU workgroups + FC workgroups) on the MoL fixtures; a
+    multi-row fixture runs its rows one launch after another."""
+    monkeypatch.setenv("WRNN_PATH", "split")
+    fx = gf.load(name)
+    d, state, mels, aux, noise = gf.loop_inputs(fx)
+    loop = _split_loop(d)
+    loop.set_weights(state)
+    out, _ = loop.generate(_cond(mels, aux), noise=torch.from_numpy(noise).to(DEV))
+    assert loop.info["last_path"] == 4
+    err = np.abs(out.cpu().numpy() - fx["samples"])
+    assert err.max() <= gf.MOL_TOL, f"max |Δ| {err.max()} at {np.unravel_index(err.argmax(), err.shape)}"
+
+
+def test_split_is_the_batch1_default_and_carries_time_chunks(monkeypatch):
+    """B = 1 MoL takes the role-split kernel by default; with a tiny terms budget the utterance
+    runs as several launches that carry h1 / h2 / the GRU1 terms / GH2 / x across the
+    boundaries: oracle parity, and Philox output identical to the single-launch run."""
+    from oracle import oracle
+    monkeypatch.delenv("WRNN_PATH", raising=False)
+    d = syn.DEFAULT_MOL
+    L = 1500
+    state = syn.make_fatchord_state(d, 71)
+    mels, aux = syn.make_conditioning(1, L, d.feat_dims, d.res_out_dims, 72)
+    noise = syn.make_noise("MOL", 1, L, d.n_classes, 73)
+    ref, _ = oracle.fatchord_loop(state, "MOL", mels, aux, noise)
+    loop = _split_loop(d)
+    loop.set_weights(state)
+    cond = _cond(mels, aux)
+    whole, _ = loop.generate(cond, seed=5)
+    assert loop.info["last_path"] == 4
+    monkeypatch.setenv("WRNN_TERMS_MB", "8")     # 8 MiB: ~370 steps per launch
+    out, _ = loop.generate(cond, noise=torch.from_numpy(noise).to(DEV))
+    assert np.abs(out.cpu().numpy() - ref).max() <= gf.MOL_TOL
+    chunked, _ = loop.generate(cond, seed=5)
+    # the terms GEMM may tile differently for a different launch length: fp tolerance
+    assert (chunked - whole).abs().max().item() <= 2 * gf.MOL_TOL
+
+
+def test_split_agrees_with_latency_under_philox(monkeypatch):
+    """Same Philox keying as the other kernels: the split and uniform latency kernels generate
+    the same MoL audio within the fp tolerance."""
+    d = syn.DEFAULT_MOL
+    L = 2000
+    state = syn.make_fatchord_state(d, 81)
+    mels, aux = syn.make_conditioning(1, L, d.feat_dims, d.res_out_dims, 82)
+    cond = _cond(mels, aux)
+    res = {}
+    for p in ("split", "latency"):
+        monkeypatch.setenv("WRNN_PATH", p)
+        loop = _loop(d)
+        loop.set_weights(state)
+        res[p], _ = loop.generate(cond, seed=91, row_offset=3)
+        assert loop.info["last_path"] == (4 if p == "split" else 1)
+    assert (res["split"] - res["latency"]).abs().max().item() <= 2 * gf.MOL_TOL
+
+
 @pytest.mark.parametrize("name", gf.SPARSE_LOOP_CASES)
 def test_sparse_loop_vs_reference_fixture(name, monkeypatch):
     """Config 4: 4x4 block-sparse GRU weights (pruning.py) run in the multi-row kernel with only

@@ -18,6 +18,7 @@
 #include "fatchord_loop.h"
 #include "fatchord_rows.h"
 #include "deepmind_rows.h"
+#include "fatchord_split.h"
 
 namespace wrnn {
 hipError_t launch_ci_gemm(const float *cond, int CD, int Bt, int b0, int Bc, int t0, int L, const float *W, int ldw,
@@ -34,6 +35,10 @@ hipError_t launch_loop(const LoopArgs &a, size_t lds_bytes, hipStream_t st);
 hipError_t prepare_loop_kernel(int max_lds_bytes);
 hipError_t loop_occupancy(int *blocks_per_cu, size_t lds_bytes);
 bool loop_has_fast_path(int R, int F, int A, int NC, bool mol, int U, int UF, int UC);
+hipError_t launch_split(const SplitArgs &a, size_t lds_bytes, hipStream_t st);
+hipError_t prepare_split_kernel(int max_lds_bytes);
+hipError_t split_occupancy(int *blocks_per_cu, size_t lds_bytes);
+bool split_has_kernel(int R, int F);
 }  // namespace wrnn
 
 using namespace wrnn;
@@ -70,7 +75,7 @@ struct wrnn_ctx {
     unsigned *d_flags = nullptr;
     unsigned long long *d_xr = nullptr;             // x granules
     rocblas_handle blas = nullptr;
-    int last_path = 0;                              // 1 = latency kernel, 2 = rows kernel, 3 = deepmind
+    int last_path = 0;                              // 1 = latency, 2 = rows, 3 = deepmind, 4 = split
     // deepmind_version (WRNN_MODE_DM): deepmind_rows.hip
     DmSlab ds{};
     int dmU = 0, dmUO = 0, dmUO2 = 0;
@@ -79,6 +84,12 @@ struct wrnn_ctx {
     unsigned *d_dmflags = nullptr;
     unsigned long long *d_dmxg = nullptr;
     size_t dmflags_cap = 0, dmxg_cap = 0;
+    // batch-1 MoL role-split kernel: fatchord_split.hip
+    bool split_ok = false;
+    int sGg = 0, sGf = 0;
+    SplitGruSlab sgs{};
+    SplitFcSlab sfs{};
+    float *d_sgslab = nullptr, *d_sfslab = nullptr, *d_sWt = nullptr;
 };
 
 namespace {
@@ -497,6 +508,121 @@ size_t lds_bytes_for(const wrnn_ctx &h, int Bc) {
                .total * sizeof(float);
 }
 
+// ------------------------------------------------------------- batch-1 role-split kernel
+// GRU workgroup g owns units 4g..4g+3 (rows u·3 + gate), FC workgroup f owns fc rows 16f..16f+15;
+// the MoL head is first in both slabs (same LDS address in every workgroup).
+void make_split_slabs(wrnn_ctx &h) {
+    const int R = h.cfg.rnn_dims, F = h.cfg.fc_dims, NC = h.cfg.n_classes;
+    constexpr int U = kSplitUnits, NF = kSplitFcRows;
+    int o = 0;
+    auto take = [&](int n) { int at = o; o += round4(n); return at; };
+    SplitGruSlab &g = h.sgs;
+    g.w3 = take(NC * F);
+    g.b3 = take(NC);
+    g.wih2 = take(3 * U * R);
+    g.whh1 = take(3 * U * R);
+    g.whh2 = take(3 * U * R);
+    g.q1a = take(3 * R);
+    g.q2 = take(3 * U);
+    g.wi0 = take(U);
+    g.bih1 = take(3 * U);
+    g.bhh1 = take(3 * U);
+    g.bih2 = take(3 * U);
+    g.bhh2 = take(3 * U);
+    g.total = o;
+    o = 0;
+    SplitFcSlab &f = h.sfs;
+    f.w3 = take(NC * F);
+    f.b3 = take(NC);
+    f.w1 = take(NF * R);
+    f.w2 = take(NF * F);
+    f.total = o;
+}
+
+size_t split_lds_bytes(const wrnn_ctx &h) {
+    return (size_t)split_lds_layout(std::max(h.sgs.total, h.sfs.total), h.cfg.rnn_dims, h.cfg.fc_dims).total *
+           sizeof(float);
+}
+
+void pack_split_slabs(const wrnn_ctx &h, std::vector<float> &gs, std::vector<float> &fs) {
+    const int R = h.cfg.rnn_dims, F = h.cfg.fc_dims, A = h.cfg.aux_dims, NC = h.cfg.n_classes;
+    constexpr int U = kSplitUnits, NF = kSplitFcRows;
+    auto W = [&](const char *n) { return h.w.at(n).data(); };
+    const float *IW = W("I.weight");
+    const int nin = 1 + h.cfg.feat_dims + A;
+    const SplitGruSlab &sg = h.sgs;
+    const SplitFcSlab &sf = h.sfs;
+    gs.assign((size_t)h.sGg * sg.total, 0.0f);
+    fs.assign((size_t)h.sGf * sf.total, 0.0f);
+    std::vector<float> q1a(3 * R);
+    for (int r = 0; r < 3 * R; ++r) q1a[r] = xcol_dot(W("rnn1.weight_ih_l0") + (size_t)r * R, IW, nin, R);
+    for (int w = 0; w < h.sGg; ++w) {
+        float *out = gs.data() + (size_t)w * sg.total;
+        std::memcpy(out + sg.w3, W("fc3.weight"), (size_t)NC * F * 4);
+        std::memcpy(out + sg.b3, W("fc3.bias"), (size_t)NC * 4);
+        std::memcpy(out + sg.q1a, q1a.data(), (size_t)3 * R * 4);
+        for (int u = 0; u < U; ++u) {
+            const int j = w * U + u;
+            out[sg.wi0 + u] = IW[(size_t)j * nin];
+            for (int q = 0; q < 3; ++q) {
+                const int src = q * R + j, dst = u * 3 + q;
+                const float *ih2 = W("rnn2.weight_ih_l0") + (size_t)src * (R + A);
+                std::memcpy(out + sg.wih2 + (size_t)dst * R, ih2, R * 4);
+                std::memcpy(out + sg.whh1 + (size_t)dst * R, W("rnn1.weight_hh_l0") + (size_t)src * R, R * 4);
+                std::memcpy(out + sg.whh2 + (size_t)dst * R, W("rnn2.weight_hh_l0") + (size_t)src * R, R * 4);
+                out[sg.q2 + dst] = xcol_dot(ih2, IW, nin, R);
+                out[sg.bih1 + dst] = W("rnn1.bias_ih_l0")[src];
+                out[sg.bhh1 + dst] = W("rnn1.bias_hh_l0")[src];
+                out[sg.bih2 + dst] = W("rnn2.bias_ih_l0")[src];
+                out[sg.bhh2 + dst] = W("rnn2.bias_hh_l0")[src];
+            }
+        }
+    }
+    for (int w = 0; w < h.sGf; ++w) {
+        float *out = fs.data() + (size_t)w * sf.total;
+        std::memcpy(out + sf.w3, W("fc3.weight"), (size_t)NC * F * 4);
+        std::memcpy(out + sf.b3, W("fc3.bias"), (size_t)NC * 4);
+        for (int e = 0; e < NF; ++e) {
+            const int r = w * NF + e;
+            std::memcpy(out + sf.w1 + (size_t)e * R, W("fc1.weight") + (size_t)r * (R + A), R * 4);
+            std::memcpy(out + sf.w2 + (size_t)e * F, W("fc2.weight") + (size_t)r * (F + A), F * 4);
+        }
+    }
+}
+
+// Terms-GEMM weights [(Gg + Gf)·kSplitTerms][KX] against X = [cI | a2 a3 a4 | 1 0 0 0]
+// (fatchord_split.h, SplitTerm)
+void pack_split_terms_weights(const wrnn_ctx &h, std::vector<float> &Wt) {
+    const int R = h.cfg.rnn_dims, F = h.cfg.fc_dims, A = h.cfg.aux_dims, KX = h.KX;
+    constexpr int U = kSplitUnits, NF = kSplitFcRows;
+    auto W = [&](const char *n) { return h.w.at(n).data(); };
+    Wt.assign((size_t)(h.sGg + h.sGf) * kSplitTerms * KX, 0.0f);
+    for (int w = 0; w < h.sGg; ++w)
+        for (int u = 0; u < U; ++u) {
+            const int j = w * U + u;
+            for (int q = 0; q < 3; ++q) {
+                const int src = q * R + j;
+                float *p1 = Wt.data() + ((size_t)w * kSplitTerms + ST_P1 + u * 3 + q) * KX;
+                float *p2 = Wt.data() + ((size_t)w * kSplitTerms + ST_P2 + u * 3 + q) * KX;
+                std::memcpy(p1, W("rnn1.weight_ih_l0") + (size_t)src * R, R * 4);
+                const float *ih2 = W("rnn2.weight_ih_l0") + (size_t)src * (R + A);
+                std::memcpy(p2, ih2, R * 4);
+                std::memcpy(p2 + R, ih2 + R, A * 4);                            // a2
+            }
+            Wt[((size_t)w * kSplitTerms + ST_CI + u) * KX + j] = 1.0f;          // cI_j itself
+        }
+    for (int f = 0; f < h.sGf; ++f)
+        for (int e = 0; e < NF; ++e) {
+            const int r = f * NF + e;
+            float *v1 = Wt.data() + ((size_t)(h.sGg + f) * kSplitTerms + ST_V1 + e) * KX;
+            float *v2 = Wt.data() + ((size_t)(h.sGg + f) * kSplitTerms + ST_V2 + e) * KX;
+            std::memcpy(v1 + R + A, W("fc1.weight") + (size_t)r * (R + A) + R, A * 4);   // a3
+            v1[R + 3 * A] = W("fc1.bias")[r];
+            std::memcpy(v2 + R + 2 * A, W("fc2.weight") + (size_t)r * (F + A) + F, A * 4);   // a4
+            v2[R + 3 * A] = W("fc2.bias")[r];
+        }
+}
+
 }  // namespace
 
 namespace {
@@ -685,6 +811,79 @@ int generate_dm(wrnn_t *h, int B, int L, const float *noise, uint64_t seed, int6
     return WRNN_OK;
 }
 
+// One MoL row through the role-split kernel: time chunks sized so terms + GEMM input stay within
+// WRNN_TERMS_MB (default 2048 MiB).  Each chunk's terms cover one step past its end (step t's
+// launch publishes the GRU1 terms of t + 1); the recurrent state is carried in d_state.
+int generate_split(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed,
+                   int64_t row_offset, float *out, hipStream_t st) {
+    const wrnn_config &c = h->cfg;
+    const int R = c.rnn_dims, A = c.aux_dims, G = h->sGg + h->sGf, N = G * kSplitTerms;
+    if (!h->blas && rocblas_create_handle(&h->blas) != rocblas_status_success)
+        return fail(h, WRNN_EHIP, "rocblas_create_handle failed");
+    if (rocblas_set_stream(h->blas, st) != rocblas_status_success) return fail(h, WRNN_EHIP, "rocblas_set_stream failed");
+    const char *mb_env = std::getenv("WRNN_TERMS_MB");
+    const double budget = (mb_env ? std::atof(mb_env) : 2048.0) * (1 << 20) / 4.0;   // floats
+    const int Lc_max = (int)std::max(1.0, std::min((double)L, budget / (double)(N + h->KX) - 1.0));
+    const char *rep_env = std::getenv("WRNN_REPLICAS");
+    const int reps = std::max(1, std::min(32, rep_env ? std::atoi(rep_env) : 8));
+    const long long vec_max = std::max<long long>({(long long)kTermsPerUnit * R, (long long)R, (long long)c.fc_dims});
+    const long long rep_stride = (((vec_max + kOverRead) * 8 + 65535) / 65536) * 65536 / 8;
+    const size_t need_xg = (size_t)kSplitHops * reps * rep_stride;
+    HIP_TRY(h, ensure(h->d_xg, h->xg_cap, need_xg));
+    if (grow(h, h->d_X, h->X_cap, (size_t)(Lc_max + 1) * h->KX) || grow(h, h->d_T, h->T_cap, (size_t)(Lc_max + 1) * N) ||
+        grow(h, h->d_state, h->state_cap, (size_t)G * split_state_w(R)))
+        return WRNN_EHIP;
+    const char *dbg_env = std::getenv("WRNN_DEBUG_STAMPS");
+    const int dbg_steps = dbg_env ? std::min(L, std::atoi(dbg_env)) : 0;
+    unsigned *d_dbg = nullptr;
+    if (dbg_steps > 0) {
+        HIP_TRY(h, hipMalloc(&d_dbg, (size_t)G * dbg_steps * kStamps * 4));
+        HIP_TRY(h, hipMemsetAsync(d_dbg, 0, (size_t)G * dbg_steps * kStamps * 4, st));
+    }
+    const float one = 1.0f, zero = 0.0f;
+    for (int b0 = 0; b0 < B; ++b0) {
+        HIP_TRY(h, hipMemsetAsync(h->d_xg, 0, need_xg * 8, st));
+        for (int t0 = 0; t0 < L; t0 += Lc_max) {
+            const int Lc = std::min(Lc_max, L - t0);
+            const int rows = std::min(Lc + 1, L - t0);     // terms rows: steps [t0, t0 + rows)
+            HIP_TRY(h, launch_ci_gemm(cond, h->CD, B, b0, 1, t0, rows, h->d_IW, 1 + c.feat_dims + A, h->d_Ib, R,
+                                      c.feat_dims + A, h->d_X, h->KX, st));
+            HIP_TRY(h, launch_pack_terms_input(cond, h->CD, B, b0, 1, t0, rows, c.feat_dims, A, R, h->KX, h->d_X, st));
+            if (rocblas_sgemm(h->blas, rocblas_operation_transpose, rocblas_operation_none, N, rows, h->KX, &one,
+                              h->d_sWt, h->KX, h->d_X, h->KX, &zero, h->d_T, N) != rocblas_status_success)
+                return fail(h, WRNN_EHIP, "rocblas_sgemm (conditioning terms) failed");
+            SplitArgs a{};
+            a.gslab = h->d_sgslab;
+            a.fslab = h->d_sfslab;
+            a.terms = h->d_T;
+            a.noise = noise;
+            a.out = out;
+            a.state = h->d_state;
+            a.xg = h->d_xg;
+            a.ctl = h->d_ctl;
+            a.seed = seed;
+            a.row0 = row_offset + b0;
+            a.timeout_ticks = h->timeout_ticks;
+            a.rep_stride = rep_stride;
+            a.L = L;
+            a.t0 = t0;
+            a.Lc = Lc;
+            a.Bt = B;
+            a.b0 = b0;
+            a.Gg = h->sGg;
+            a.Gf = h->sGf;
+            a.reps = reps;
+            a.gs = h->sgs;
+            a.fs = h->sfs;
+            a.dbg = (b0 == 0 && t0 == 0) ? d_dbg : nullptr;
+            a.dbg_steps = std::min(dbg_steps, Lc);
+            HIP_TRY(h, launch_split(a, split_lds_bytes(*h), st));
+        }
+    }
+    if (d_dbg) return dump_stamps(h, d_dbg, dbg_steps, st, G);
+    return WRNN_OK;
+}
+
 int generate_latency(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed,
                      int64_t row_offset, float *out, int32_t *labels, hipStream_t st) {
     const wrnn_config &c = h->cfg;
@@ -692,9 +891,11 @@ int generate_latency(wrnn_t *h, const float *cond, int B, int L, const float *no
     const int Bc_max = std::min(B, h->max_rows);
     // workspaces (grow-only)
     if (grow(h, h->d_cI, h->cI_cap, (size_t)L * Bc_max * R)) return WRNN_EHIP;
-    // hand-off replicas (WRNN_REPLICAS, default 8), each padded to a 64 KiB boundary
+    // hand-off replicas (WRNN_REPLICAS, default 8), each padded to a 64 KiB boundary; at most
+    // 64 / kTermsPerUnit, since one wave publishes every term of a unit to every replica at once
+    // (8 measured best: 8.18 us/step at rnn 512 B=1; 4 -> 8.27, 16 -> 8.77, 2 -> 8.84)
     const char *rep_env = std::getenv("WRNN_REPLICAS");
-    const int reps = std::max(1, std::min(64, rep_env ? std::atoi(rep_env) : 8));
+    const int reps = std::max(1, std::min(64 / kTermsPerUnit, rep_env ? std::atoi(rep_env) : 8));
     // replica stride ≥ 64 KiB: keeps replicas on different lines/channels and makes the
     // pollers' fixed-count over-reads (slots ≥ n) land in allocated memory
     const long long vec_max = std::max<long long>({(long long)Bc_max * h->NMAX, (long long)Bc_max * R * kTermsPerUnit,
@@ -860,6 +1061,18 @@ int wrnn_create(const wrnn_config *cfg, int device, wrnn_t **out) {
         HIP_TRY(h, rows_occupancy(&per_cu, rows_lds_bytes(*h, 1, 1)));
         if (per_cu * h->num_cus < h->rG) h->rows_ok = false;
     }
+    // one MoL row: the role-split kernel (compile-time dims) when its grid and LDS fit; an
+    // explicit grid request keeps the uniform kernels
+    if (mol && c.grid <= 0 && split_has_kernel(R, F) && R % kSplitUnits == 0 && F % kSplitFcRows == 0) {
+        h->sGg = R / kSplitUnits;
+        h->sGf = F / kSplitFcRows;
+        make_split_slabs(*h);
+        if (h->sGg + h->sGf <= h->num_cus && split_lds_bytes(*h) <= (size_t)h->max_lds) {
+            HIP_TRY(h, prepare_split_kernel(h->max_lds));
+            HIP_TRY(h, split_occupancy(&per_cu, split_lds_bytes(*h)));
+            h->split_ok = per_cu >= 1;
+        }
+    }
     h->timeout_ticks = (long long)(c.timeout_ms > 0 ? c.timeout_ms : 2000) * 100000LL;   // 100 MHz
     HIP_TRY(h, hipMalloc(&h->d_ctl, kCtlWords * sizeof(int)));
     HIP_TRY(h, hipMemset(h->d_ctl, 0, kCtlWords * sizeof(int)));
@@ -942,6 +1155,18 @@ int wrnn_set_weights(wrnn_t *h, const wrnn_tensor *tensors, int n) {
         HIP_TRY(h, hipMalloc(&h->d_Wt, Wt.size() * 4));
         HIP_TRY(h, hipMemcpy(h->d_Wt, Wt.data(), Wt.size() * 4, hipMemcpyHostToDevice));
     }
+    if (h->split_ok) {
+        std::vector<float> gs, fs, Wt;
+        pack_split_slabs(*h, gs, fs);
+        pack_split_terms_weights(*h, Wt);
+        for (auto pr : {std::make_pair(&h->d_sgslab, &gs), std::make_pair(&h->d_sfslab, &fs),
+                        std::make_pair(&h->d_sWt, &Wt)}) {
+            if (*pr.first) HIP_TRY(h, hipFree(*pr.first));
+            *pr.first = nullptr;
+            HIP_TRY(h, hipMalloc(pr.first, pr.second->size() * 4));
+            HIP_TRY(h, hipMemcpy(*pr.first, pr.second->data(), pr.second->size() * 4, hipMemcpyHostToDevice));
+        }
+    }
     h->ready = true;
     return WRNN_OK;
 }
@@ -954,19 +1179,23 @@ int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise
     if (labels && h->cfg.mode == WRNN_MODE_MOL) return fail(h, WRNN_EINVAL, "labels are a RAW / DM output");
     HIP_TRY(h, hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
-    // path: the latency kernel while the rows fit its LDS layout in one launch, else the
-    // multi-row kernel; WRNN_PATH=latency|rows forces one (tests, benchmarks)
+    // path: one MoL row → the role-split kernel; otherwise the latency kernel while the rows
+    // fit its LDS layout in one launch, else the multi-row kernel.  WRNN_PATH=split|latency|rows
+    // forces one (tests, benchmarks)
     const char *path_env = std::getenv("WRNN_PATH");
+    const std::string pe = path_env ? path_env : "";
     bool rows = h->max_rows < 1 || B > h->max_rows;
-    if (path_env && std::string(path_env) == "rows") rows = true;
-    if (path_env && std::string(path_env) == "latency" && h->max_rows >= 1) rows = false;
+    if (pe == "rows") rows = true;
+    if (pe == "latency" && h->max_rows >= 1) rows = false;
     if (rows && !h->rows_ok) rows = false;
+    const bool split = h->split_ok && (pe == "split" || (pe.empty() && B == 1));
     HIP_TRY(h, hipMemsetAsync(h->d_ctl, 0, kCtlWords * sizeof(int), st));
     HIP_TRY(h, hipEventRecord(h->ev0, st));
-    h->last_path = h->dm ? 3 : rows ? 2 : 1;
-    const int rc = h->dm  ? generate_dm(h, B, L, noise, seed, row_offset, out, labels, st)
-                   : rows ? generate_rows(h, cond, B, L, noise, seed, row_offset, out, labels, st)
-                          : generate_latency(h, cond, B, L, noise, seed, row_offset, out, labels, st);
+    h->last_path = h->dm ? 3 : split ? 4 : rows ? 2 : 1;
+    const int rc = h->dm    ? generate_dm(h, B, L, noise, seed, row_offset, out, labels, st)
+                   : split ? generate_split(h, cond, B, L, noise, seed, row_offset, out, st)
+                   : rows  ? generate_rows(h, cond, B, L, noise, seed, row_offset, out, labels, st)
+                           : generate_latency(h, cond, B, L, noise, seed, row_offset, out, labels, st);
     if (rc != WRNN_OK) return rc;
     HIP_TRY(h, hipEventRecord(h->ev1, st));
     h->timed = true;
@@ -985,7 +1214,9 @@ int wrnn_check(wrnn_t *h, void *stream) {
         const int hop = ctl[3];
         static const char *dm_hops[] = {"h_coarse", "o1", "coarse logits", "h_fine", "o3", "fine logits",
                                         "coarse label", "fine label"};
-        const char *name = h->last_path == 3   ? (hop >= 0 && hop < 8 ? dm_hops[hop] : "?")
+        static const char *split_hops[] = {"y", "f1", "f2", "h2", "h2", "gru1-terms", "gru1-terms"};
+        const char *name = h->last_path == 4   ? (hop >= 0 && hop < 7 ? split_hops[hop] : "?")
+                           : h->last_path == 3 ? (hop >= 0 && hop < 8 ? dm_hops[hop] : "?")
                            : h->last_path == 2 ? (hop >= 0 && hop < 6 ? row_hops[hop] : "?")
                                                : (hop >= 0 && hop < 7 ? lat_hops[hop] : "?");
         return fail(h, WRNN_ETIMEOUT,
@@ -1017,6 +1248,7 @@ int wrnn_query(const wrnn_t *h, wrnn_info *info) {
         info->num_cus = h->num_cus;
         info->rows_grid = h->G;
         info->rows_units_rnn = h->dmU;
+        info->last_path = h->last_path;
         return WRNN_OK;
     }
     const bool rows_only = h->max_rows < 1;      // e.g. rnn 896 with block-sparse GRU weights
@@ -1031,6 +1263,8 @@ int wrnn_query(const wrnn_t *h, wrnn_info *info) {
     info->rows_units_rnn = h->rows_ok ? h->rU : 0;
     info->sparse_blocks = h->rows_ok ? h->rs.nbmax : 0;
     info->num_cus = h->num_cus;
+    info->split_grid = h->split_ok ? h->sGg + h->sGf : 0;
+    info->last_path = h->last_path;
     return WRNN_OK;
 }
 
@@ -1044,7 +1278,8 @@ void wrnn_destroy(wrnn_t *h) {
     for (void *p : {(void *)h->d_slab, (void *)h->d_IW, (void *)h->d_Ib, (void *)h->d_cI, (void *)h->d_xg,
                     (void *)h->d_ctl, (void *)h->d_rslab, (void *)h->d_Wt, (void *)h->d_X, (void *)h->d_T,
                     (void *)h->d_act, (void *)h->d_state, (void *)h->d_flags, (void *)h->d_xr, (void *)h->d_dmslab,
-                    (void *)h->d_dmflags, (void *)h->d_dmxg})
+                    (void *)h->d_dmflags, (void *)h->d_dmxg, (void *)h->d_sgslab, (void *)h->d_sfslab,
+                    (void *)h->d_sWt})
         if (p) (void)hipFree(p);
     if (h->blas) (void)rocblas_destroy_handle(h->blas);
     delete h;

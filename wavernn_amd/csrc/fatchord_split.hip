@@ -1,0 +1,324 @@
+// fatchord_split.hip — role-split persistent kernel for ONE MoL row (the batch-1 headline).
+//
+// Same loop as fatchord_loop.hip (models/fatchord_version.py:201-241), but the workgroups take
+// two roles so that every critical hand-off has few participants (a hop's cost grows with the
+// number of producers and pollers: 2 → 0.47 µs, 32 → 1.0, 256 → 1.7 µs, tools/hopbench.hip):
+//
+//   GRU workgroups (Gg = R/4): 4 hidden units of both GRUs.  GRU1 runs for ALL units in every
+//     GRU workgroup (local gate math on gathered terms, as in fatchord_loop.hip), GRU2 for the
+//     own units; each publishes y_j = x_I,j + h1_j + h2_j (fc1's input, :212-216) and h2_j.
+//   FC workgroups (Gf = F/16): 16 rows of fc1 and of fc2, one per 16-lane engine.
+//   Every workgroup gathers f2 and runs fc3 + the MoL sampler redundantly (bit-identical), so
+//     the sample needs no hand-off of its own.
+//
+// Critical path per step:
+//   x_{t-1} → GRU1 (all units) → W_ih2[:, :R]·h1 → GRU2 gates → [hop Y: Gg → Gf]
+//   → W1[:, :R]·y → [hop F1: Gf → Gf] → W2[:, :F]·f1 → [hop F2: Gf → all] → fc3 → sample → x_t
+// Off the critical path, while fc1/fc2 run in the FC workgroups, the GRU workgroups compute
+// GH1 = W_hh1·h1_t → publish step t+1's GRU1 terms, gather h2_t → GH2 = W_hh2·h2_t, and
+// gather step t+1's terms of all units.  Everything that depends only on the conditioning
+// (P1 = W_ih1·cI, P2 = W_ih2·[cI; a2], V1c = W1[:, R:]·a3 + b1, V2 = W2[:, F:]·a4 + b2, and
+// cI itself) comes from one fp32 GEMM before the launch (capi.cpp) and is streamed into an LDS
+// ring by the loader wave, so the LDS holds only the loop matrices and the MoL head.
+//
+// Arithmetic is fp32; the sums are re-associated like fatchord_loop.hip's (tolerance-checked
+// against the oracle).  Every wait is bounded; a timeout sets the abort word.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fatchord_split.h"
+#include "wrnn_device.h"
+
+namespace wrnn {
+
+#define SSTAMP(k)                                                                                          \
+    do {                                                                                                   \
+        if (dbg_on && tid == 0) stamp[(t & 1) * kStamps + (k)] = (unsigned)__builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+
+template <int kR, int kF>
+__global__ __launch_bounds__(kThreads) void fatchord_split_kernel(SplitArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int R = kR, F = kF, NC = 30, RT = kTermsPerUnit * R;
+    constexpr int NG_R = R / kPollThreads, NG_F = F / kPollThreads;
+    static_assert(R % kPollThreads == 0 && F % kPollThreads == 0 && NG_R <= 16 && NG_F <= 16, "poll layout");
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, row = lane >> 4;
+    const int w = blockIdx.x;
+    const bool gru = w < a.Gg;
+    const int g = gru ? w : w - a.Gg;                 // index within the role
+    const SplitLds ll = split_lds_layout(a.gs.total > a.fs.total ? a.gs.total : a.fs.total, R, F);
+    const float *S = smem + ll.slab;
+    float *va = smem + ll.va, *vb = smem + ll.vb, *f2 = smem + ll.f2, *lg = smem + ll.lg, *sg = smem + ll.sg;
+    float *ring = smem + ll.ring, *nzr = smem + ll.nz, *gh2 = smem + ll.gh2, *gh1 = smem + ll.gh1;
+    float *h2own = smem + ll.h2own, *xprev = smem + ll.xprev;
+    int *abort_flag = reinterpret_cast<int *>(smem + ll.flag);
+    unsigned *stamp = reinterpret_cast<unsigned *>(smem + ll.stamp);
+    const bool loader = wave == kLoaderWave;
+    const bool dbg_on = a.dbg != nullptr;
+    const int N = (a.Gg + a.Gf) * kSplitTerms;        // terms per step, all workgroups
+    const int term0 = w * kSplitTerms;                // this workgroup's columns
+    const int t_end = a.t0 + a.Lc;
+    const int t_terms = min(t_end, a.L - 1);          // last step with a terms row in this launch
+    const size_t hop_stride = (size_t)a.reps * a.rep_stride;
+    const size_t poll_off = (size_t)(w % a.reps) * a.rep_stride;
+    auto XG = [&](int hop) { return a.xg + (size_t)hop * hop_stride; };
+    auto RING = [&](int t) { return ring + (t & (kSplitRing - 1)) * kSplitTerms; };
+    auto NZ = [&](int t) { return nzr + (t & (kSplitRing - 1)) * kSplitNoise; };
+
+    // the sampler's 11 noise terms of step t (lanes 0..10 of one wave): u1 → log(-log u1)
+    // (distribution.py:107), u2 → log u2 − log(1 − u2) (:119), prepared ahead of time
+    auto fill_noise = [&](int t) {
+        if (lane < 11) {
+            float uu;
+            if (a.noise) uu = a.noise[((size_t)t * a.Bt + a.b0) * 11 + lane];
+            else uu = philox_noise(a.seed, (unsigned long long)a.row0, (uint32_t)t, (uint32_t)lane, 1);
+            NZ(t)[lane] = mol_noise_term(uu, lane);
+        }
+    };
+    // GRU1 terms of step t for the own units → every replica of the S(t) vector (one wave):
+    //   S_r = (GH1_r + b_hh,r) + (P1_r + b_ih,r), S_z likewise, Gi_n = P1_n + b_ih,n, Gh_n = GH1_n + b_hh,n
+    auto publish_terms = [&](int t, bool zero_gh) {
+        const float *p1 = RING(t) + ST_P1;
+        for (int idx = lane; idx < kSplitUnits * kTermsPerUnit * a.reps; idx += 64) {
+            const int k16 = idx / a.reps, rep = idx - k16 * a.reps;
+            const int u = k16 >> 2, term = k16 & 3;
+            const float *bh = S + a.gs.bhh1 + u * 3, *bi = S + a.gs.bih1 + u * 3;
+            const float g_r = zero_gh ? 0.0f : gh1[u * 3 + 0];
+            const float g_z = zero_gh ? 0.0f : gh1[u * 3 + 1];
+            const float g_n = zero_gh ? 0.0f : gh1[u * 3 + 2];
+            float v;
+            if (term == 0) v = (g_r + bh[0]) + (p1[u * 3 + 0] + bi[0]);
+            else if (term == 1) v = (g_z + bh[1]) + (p1[u * 3 + 1] + bi[1]);
+            else if (term == 2) v = p1[u * 3 + 2] + bi[2];
+            else v = g_n + bh[2];
+            publish(XG(SH_S0 + (t & 1)) + (size_t)rep * a.rep_stride + (size_t)(g * kSplitUnits + u) * kTermsPerUnit + term,
+                    (uint32_t)t + 1u, v);
+        }
+    };
+    auto gather_terms = [&](int t) {
+        gather_chunked<NG_R, kPollThreads>(XG(SH_S0 + (t & 1)) + poll_off, RT, RT, (uint32_t)t + 1u, a.ctl,
+                                           a.timeout_ticks, t, SH_S0 + (t & 1), abort_flag, lane,
+                                           [&](int, int j, float v) { sg[j] = v; });
+    };
+
+    // ---- prologue: slab → LDS, state (zero, or carried from the previous time chunk), the
+    // terms and noise of the first two steps; at t = 0 the GRU1 terms of step 0 (GH1 = 0)
+    {
+        const float *src = gru ? a.gslab + (size_t)g * a.gs.total : a.fslab + (size_t)g * a.fs.total;
+        const int n4 = (gru ? a.gs.total : a.fs.total) / 4;
+        for (int i = tid; i < n4; i += kThreads)
+            reinterpret_cast<float4 *>(smem + ll.slab)[i] = reinterpret_cast<const float4 *>(src)[i];
+        const bool resume = a.t0 > 0 && gru;
+        const float *st = a.state + (size_t)w * split_state_w(R);
+        for (int i = tid; i < R; i += kThreads) {
+            va[i] = resume ? st[i] : 0.0f;
+            vb[i] = resume ? st[R + i] : 0.0f;
+        }
+        if (gru)
+            for (int i = tid; i < RT; i += kThreads) sg[i] = resume ? st[2 * R + i] : 0.0f;
+        if (tid < 24) gh2[tid] = resume ? st[6 * R + tid] : 0.0f;
+        if (tid < 4) {
+            h2own[tid] = resume ? st[6 * R + 24 + tid] : 0.0f;
+            abort_flag[tid] = 0;
+        }
+        if (tid == 0) xprev[0] = a.t0 > 0 ? a.state[(size_t)w * split_state_w(R) + 6 * R + 28] : 0.0f;
+        for (int t = a.t0; t < a.t0 + 2; ++t) {
+            if (t <= t_terms)
+                for (int i = tid; i < kSplitTerms; i += kThreads)
+                    RING(t)[i] = a.terms[(size_t)(t - a.t0) * N + term0 + i];
+            if (wave == 1 && t < a.L) fill_noise(t);
+        }
+    }
+    __syncthreads();
+    if (gru && a.t0 == 0) {
+        if (wave == 1) publish_terms(0, true);
+        if (wave == 3) gather_terms(0);
+    }
+    __syncthreads();
+    if (*abort_flag) return;
+
+    // loader wave, after the first barrier of step t: the output of step t-1, the noise of
+    // step t+2 and its terms (LDS-DMA, waited for before the step's last barrier)
+    auto loader_top = [&](int t) {
+        if (dbg_on && t > a.t0 && t - 1 - a.t0 < a.dbg_steps && lane < kStamps)
+            a.dbg[((size_t)w * a.dbg_steps + (t - 1 - a.t0)) * kStamps + lane] = stamp[((t - 1) & 1) * kStamps + lane];
+        if (w == 0 && lane == 0 && t > a.t0) a.out[(size_t)a.b0 * a.L + (t - 1)] = xprev[0];
+        const int t2 = t + 2;
+        if (t2 < a.L) fill_noise(t2);
+        if (t2 <= t_terms && lane < kSplitTerms / 4)
+            __builtin_amdgcn_global_load_lds(WRNN_GPTR(a.terms + (size_t)(t2 - a.t0) * N + term0 + lane * 4),
+                                             WRNN_LPTR(RING(t2)), 16, 0, 0);
+    };
+
+    float x = xprev[0];   // x_{t-1}, wave-uniform in every compute wave
+    for (int t = a.t0; t < t_end; ++t) {
+        const uint32_t tag = (uint32_t)t + 1u;
+        const bool more = t + 1 < a.L;
+        SSTAMP(0);
+        if (gru) {
+            // ---- A: GRU1 (:208-210) for all units from the gathered terms
+            if (!loader)
+                for (int j = tid; j < R; j += kCompute) {
+                    const float4 st = reinterpret_cast<const float4 *>(sg)[j];
+                    const float r = sigmoid_(fmaf(x, S[a.gs.q1a + j], st.x));
+                    const float z = sigmoid_(fmaf(x, S[a.gs.q1a + R + j], st.y));
+                    const float n = tanh_(fmaf(x, S[a.gs.q1a + 2 * R + j], st.z) + st.w * r);
+                    va[j] = (va[j] - n) * z + n;
+                }
+            bar();
+            SSTAMP(1);
+            if (loader) loader_top(t);
+
+            // ---- B: GRU2 (:213-214), wave u → unit u (gate rows on DPP rows 0..2)
+            if (!loader) {
+                const int u = wave, j = g * kSplitUnits + u;
+                const float v = row_dot(S + a.gs.wih2 + (u * 3 + (row < 3 ? row : 0)) * R, va, R / 4, li);
+                const float *tr = RING(t);
+                float gi[3], gh[3];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    gi[q] = (lane_bcast(v, 16 * q) + fmaf(x, S[a.gs.q2 + u * 3 + q], tr[ST_P2 + u * 3 + q])) +
+                            S[a.gs.bih2 + u * 3 + q];
+                    gh[q] = gh2[(t & 1) * 12 + u * 3 + q] + S[a.gs.bhh2 + u * 3 + q];
+                }
+                const float hn = gru_gate_math(gi[0], gi[1], gi[2], gh[0], gh[1], gh[2], h2own[u]);
+                // y = (x_I + h1) + h2 (:212, :216), x_I = cI + W_I[:, 0]·x
+                const float y = (fmaf(S[a.gs.wi0 + u], x, tr[ST_CI + u]) + va[j]) + hn;
+                if (lane < a.reps) publish(XG(SH_Y) + (size_t)lane * a.rep_stride + j, tag, y);
+                else if (lane < 2 * a.reps)
+                    publish(XG(SH_H2A + (t & 1)) + (size_t)(lane - a.reps) * a.rep_stride + j, tag, hn);
+                if (lane == 0) h2own[u] = hn;
+                if (dbg_on && tid == 0) stamp[(t & 1) * kStamps + 2] = (unsigned)__builtin_amdgcn_s_memrealtime();
+            }
+
+            // ---- C: while fc1/fc2 run elsewhere: f2 (wave 0), step t+1's GRU1 terms (wave 1
+            // publishes, wave 3 gathers), h2 → GH2 (wave 2)
+            if (wave == 0) {
+                gather<NG_F, kPollThreads>(XG(SH_F2) + poll_off, 0, F, F, tag, a.ctl, a.timeout_ticks, t, SH_F2,
+                                           abort_flag, lane, [&](int, int k, float v) { f2[k] = v; });
+            } else if (wave == 1) {
+                if (more) {
+                    const float3 v = row_dot3(S + a.gs.whh1 + (row * 3 + 0) * R, S + a.gs.whh1 + (row * 3 + 1) * R,
+                                              S + a.gs.whh1 + (row * 3 + 2) * R, va, R / 4, li);
+                    if (li == 0) {
+                        gh1[row * 3 + 0] = v.x;
+                        gh1[row * 3 + 1] = v.y;
+                        gh1[row * 3 + 2] = v.z;
+                    }
+                    publish_terms(t + 1, false);
+                }
+            } else if (wave == 2) {
+                if (more) {
+                    gather<NG_R, kPollThreads>(XG(SH_H2A + (t & 1)) + poll_off, 0, R, R, tag, a.ctl, a.timeout_ticks,
+                                               t, SH_H2A + (t & 1), abort_flag, lane,
+                                               [&](int, int k, float v) { vb[k] = v; });
+                    const float3 v = row_dot3(S + a.gs.whh2 + (row * 3 + 0) * R, S + a.gs.whh2 + (row * 3 + 1) * R,
+                                              S + a.gs.whh2 + (row * 3 + 2) * R, vb, R / 4, li);
+                    float *o = gh2 + ((t + 1) & 1) * 12 + row * 3;
+                    if (li == 0) {
+                        o[0] = v.x;
+                        o[1] = v.y;
+                        o[2] = v.z;
+                    }
+                }
+            } else if (wave == 3) {
+                if (more) gather_terms(t + 1);
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // loader: this step's DMA landed
+            }
+            bar();
+            SSTAMP(3);
+            if (*abort_flag) return;
+        } else {
+            // ---- A': y (hop Y)
+            if (wave == 0)
+                gather<NG_R, kPollThreads>(XG(SH_Y) + poll_off, 0, R, R, tag, a.ctl, a.timeout_ticks, t, SH_Y,
+                                           abort_flag, lane, [&](int, int k, float v) { va[k] = v; });
+            bar();
+            SSTAMP(1);
+            if (*abort_flag) return;
+            if (loader) loader_top(t);
+            const int e = wave * 4 + row;                 // engine = fc row within the workgroup
+            // ---- B': fc1 (:216-218), relu → hop F1
+            if (!loader) {
+                const float v = row_dot(S + a.fs.w1 + e * R, va, R / 4, li) + RING(t)[ST_V1 + e];
+                if (li < a.reps)
+                    publish(XG(SH_F1) + (size_t)li * a.rep_stride + g * kSplitFcRows + e, tag, v > 0.0f ? v : 0.0f);
+                if (dbg_on && tid == 0) stamp[(t & 1) * kStamps + 6] = (unsigned)__builtin_amdgcn_s_memrealtime();
+            }
+            if (wave == 0)
+                gather<NG_F, kPollThreads>(XG(SH_F1) + poll_off, 0, F, F, tag, a.ctl, a.timeout_ticks, t, SH_F1,
+                                           abort_flag, lane, [&](int, int k, float v) { vb[k] = v; });
+            bar();
+            SSTAMP(2);
+            if (*abort_flag) return;
+            // ---- C': fc2 (:220-221), relu → hop F2
+            if (!loader) {
+                const float v = row_dot(S + a.fs.w2 + e * F, vb, F / 4, li) + RING(t)[ST_V2 + e];
+                if (li < a.reps)
+                    publish(XG(SH_F2) + (size_t)li * a.rep_stride + g * kSplitFcRows + e, tag, v > 0.0f ? v : 0.0f);
+                if (dbg_on && tid == 0) stamp[(t & 1) * kStamps + 7] = (unsigned)__builtin_amdgcn_s_memrealtime();
+            }
+            if (wave == 0)
+                gather<NG_F, kPollThreads>(XG(SH_F2) + poll_off, 0, F, F, tag, a.ctl, a.timeout_ticks, t, SH_F2,
+                                           abort_flag, lane, [&](int, int k, float v) { f2[k] = v; });
+            if (loader) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            bar();
+            SSTAMP(3);
+            if (*abort_flag) return;
+        }
+
+        // ---- D: fc3 (:223), 30 rows over the 16 engines: rows e and e + 16
+        if (!loader) {
+            const int e = wave * 4 + row, e2 = e + 16 < NC ? e + 16 : NC - 1;
+            const float2 v = row_dot2(S + a.gs.w3 + e * F, S + a.gs.w3 + e2 * F, f2, F / 4, li);
+            if (li == 0) {
+                lg[e] = v.x + S[a.gs.b3 + e];
+                if (e + 16 < NC) lg[e + 16] = v.y + S[a.gs.b3 + e + 16];
+            }
+        }
+        bar();
+        SSTAMP(4);
+        // ---- E: sample (:225-229) in every compute wave: x_t stays in registers
+        if (!loader) {
+            x = mol_sample(lg, NZ(t), lane);
+            if (tid == 0) xprev[0] = x;
+        }
+        SSTAMP(5);
+    }
+    __syncthreads();
+    if (w == 0 && tid == 0) a.out[(size_t)a.b0 * a.L + (t_end - 1)] = xprev[0];
+    // carry the recurrent state to the next time chunk
+    float *st = a.state + (size_t)w * split_state_w(R);
+    for (int i = tid; i < R; i += kThreads) {
+        st[i] = va[i];
+        st[R + i] = vb[i];
+    }
+    if (gru)
+        for (int i = tid; i < RT; i += kThreads) st[2 * R + i] = sg[i];
+    if (tid < 24) st[6 * R + tid] = gh2[tid];
+    if (tid < 4) st[6 * R + 24 + tid] = h2own[tid];
+    if (tid == 0) st[6 * R + 28] = xprev[0];
+}
+
+#define WRNN_K_SPLIT512 fatchord_split_kernel<512, 512>
+
+bool split_has_kernel(int R, int F) { return R == 512 && F == 512; }
+
+hipError_t launch_split(const SplitArgs &a, size_t lds_bytes, hipStream_t st) {
+    SplitArgs args = a;
+    void *params[] = {&args};
+    return hipLaunchKernel((const void *)WRNN_K_SPLIT512, dim3(a.Gg + a.Gf), dim3(kThreads), params, lds_bytes, st);
+}
+
+hipError_t prepare_split_kernel(int max_lds_bytes) {
+    return hipFuncSetAttribute((const void *)WRNN_K_SPLIT512, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               max_lds_bytes);
+}
+
+hipError_t split_occupancy(int *blocks_per_cu, size_t lds_bytes) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, (const void *)WRNN_K_SPLIT512, kThreads,
+                                                        lds_bytes);
+}
+
+}  // namespace wrnn
