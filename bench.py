@@ -29,7 +29,7 @@ sys.path.insert(0, REPO)
 from wavernn_amd import synthetic as syn  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
-PMC_PROFILE = os.path.join(REPO, "profiles", "r01_v6_pmc_traffic.json")
+PMC_PROFILE = os.environ.get("WRNN_PMC_PROFILE", os.path.join(REPO, "profiles", "r01_v7_pmc_traffic.json"))
 
 
 def pmc_traffic_bytes(mode: str, batched: bool, seconds: float):
@@ -207,7 +207,7 @@ def main():
                 "traffic": pmc_traffic_bytes(args.mode, args.batched, args.seconds),
                 "note": "achieved = algorithmic bytes (all loop weights fp32 per step + 836 B/row-step) per launch "
                         "/ launch time (HIP events); weights are LDS-resident, the kernel is hand-off-latency bound. "
-                        "traffic = FETCH_SIZE+WRITE_SIZE bytes per launch from profiles/r01_v6_pmc_traffic.json: "
+                        f"traffic = FETCH_SIZE+WRITE_SIZE bytes per launch from profiles/{os.path.basename(PMC_PROFILE)}: "
                         "granule polling/publishing, not weight streaming",
             },
         }

@@ -2,8 +2,8 @@
 
     python tools/pmc_summary.py gpurun_out profiles/r01_v4_pmc_traffic.json
 
-Takes, per counter, the dispatch of the persistent loop kernel (the longest fatchord_loop_kernel
-dispatch in that pass) and stores its value (KiB per dispatch, as rocprofv3 reports these
+Takes, per counter, the dispatch of the headline's persistent loop kernel (the longest
+fatchord_split_kernel / fatchord_loop_kernel dispatch in that pass) and stores its value (KiB per dispatch, as rocprofv3 reports these
 derived counters) and duration; bench.py reads the sum as `roofline.traffic`."""
 import csv
 import json
@@ -14,7 +14,7 @@ def loop_dispatch(path):
     best = None
     with open(path) as f:
         for r in csv.DictReader(f):
-            if "fatchord_loop_kernel" not in r["Kernel_Name"]:
+            if "fatchord_split_kernel" not in r["Kernel_Name"] and "fatchord_loop_kernel" not in r["Kernel_Name"]:
                 continue
             dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
             if best is None or dur > best[2]:

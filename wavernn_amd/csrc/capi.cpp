@@ -664,7 +664,7 @@ int grow(wrnn_t *h, float *&p, size_t &cap, size_t n) {
 }
 
 // B rows through the multi-row kernel: row groups of <= kRowsMax, time chunks sized so the
-// precomputed terms stay within WRNN_TERMS_MB (default 2048 MiB).
+// precomputed terms stay within WRNN_TERMS_MB (default 8192 MiB).
 int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed, int64_t row_offset,
                   float *out, int32_t *labels, hipStream_t st) {
     const wrnn_config &c = h->cfg;
@@ -677,7 +677,7 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
         return fail(h, WRNN_EHIP, "rocblas_create_handle failed");
     if (rocblas_set_stream(h->blas, st) != rocblas_status_success) return fail(h, WRNN_EHIP, "rocblas_set_stream failed");
     const char *mb_env = std::getenv("WRNN_TERMS_MB");
-    const double budget = (mb_env ? std::atof(mb_env) : 2048.0) * (1 << 20) / 4.0;   // floats
+    const double budget = (mb_env ? std::atof(mb_env) : 8192.0) * (1 << 20) / 4.0;   // floats
     const float one = 1.0f, zero = 0.0f;
     const char *dbg_env = std::getenv("WRNN_DEBUG_STAMPS");
     const int dbg_steps = dbg_env ? std::min(L, std::atoi(dbg_env)) : 0;
@@ -812,7 +812,7 @@ int generate_dm(wrnn_t *h, int B, int L, const float *noise, uint64_t seed, int6
 }
 
 // One MoL row through the role-split kernel: time chunks sized so terms + GEMM input stay within
-// WRNN_TERMS_MB (default 2048 MiB).  Each chunk's terms cover one step past its end (step t's
+// WRNN_TERMS_MB (default 8192 MiB).  Each chunk's terms cover one step past its end (step t's
 // launch publishes the GRU1 terms of t + 1); the recurrent state is carried in d_state.
 int generate_split(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed,
                    int64_t row_offset, float *out, hipStream_t st) {
@@ -822,7 +822,7 @@ int generate_split(wrnn_t *h, const float *cond, int B, int L, const float *nois
         return fail(h, WRNN_EHIP, "rocblas_create_handle failed");
     if (rocblas_set_stream(h->blas, st) != rocblas_status_success) return fail(h, WRNN_EHIP, "rocblas_set_stream failed");
     const char *mb_env = std::getenv("WRNN_TERMS_MB");
-    const double budget = (mb_env ? std::atof(mb_env) : 2048.0) * (1 << 20) / 4.0;   // floats
+    const double budget = (mb_env ? std::atof(mb_env) : 8192.0) * (1 << 20) / 4.0;   // floats
     const int Lc_max = (int)std::max(1.0, std::min((double)L, budget / (double)(N + h->KX) - 1.0));
     const char *rep_env = std::getenv("WRNN_REPLICAS");
     const int reps = std::max(1, std::min(32, rep_env ? std::atoi(rep_env) : 8));
