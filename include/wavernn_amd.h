@@ -129,6 +129,48 @@ int wrnn_query(const wrnn_t *h, wrnn_info *info);
 const char *wrnn_last_error(const wrnn_t *h);
 void wrnn_destroy(wrnn_t *h);
 
+/* ---- conditioning producer and waveform consumer (stateless; no handle) ----------------- */
+
+/* The UpsampleNetwork's mel path: per scale s_i a nearest Stretch2d(s_i) and a Conv2d(1,1,
+ * (1, 2·s_i+1), padding (0, s_i), no bias) whose taps are `upsample.up_layers.{2i+1}.weight`
+ * (fatchord_version.py:64-79), applied to the mel zero-padded by `pad` frames each side. */
+typedef struct {
+    int32_t feat_dims;       /* num_mels (80) */
+    int32_t res_out_dims;    /* MelResNet output channels (128) = 4·aux_dims */
+    int32_t pad;             /* voc_pad (2) */
+    int32_t n_scales;        /* 1..4 (hparams voc_upsample_factors = (5, 5, 11)) */
+    int32_t scales[4];       /* each 1..15 */
+    const float *taps[4];    /* HOST pointers, 2·scales[i]+1 floats each */
+} wrnn_upsample_cfg;
+
+/* Shape of the conditioning wrnn_upsample_pack writes for `B` mel rows of `T` frames:
+ * steps = L = hop·T unbatched (target <= 0), else the fold window target + 2·overlap;
+ * rows = B·num_folds (fold_with_overlap, fatchord_version.py:317-330). */
+int wrnn_cond_shape(const wrnn_upsample_cfg *cfg, int B, int T, int target, int overlap,
+                    int *steps, int *rows);
+
+/* Replaces, in one kernel, everything between MelResNet and the loop's input
+ * (fatchord_version.py:183-205): pad_tensor(pad) → 3× (Stretch2d, Conv2d) → crop indent (:88)
+ * for the mel, resnet_stretch (:83) for `aux`, fold_with_overlap (:293-340, target <= 0:
+ * unbatched) and the cat/transpose into the time-major records wrnn_generate reads.
+ *   mel   [B][feat_dims][T]     the generate() input (device, fp32)
+ *   aux   [B][res_out_dims][T]  MelResNet(pad_tensor(mel)) output (device, fp32)
+ *   cond  [steps][rows][feat_dims + res_out_dims]  (device; row = b·num_folds + fold) */
+int wrnn_upsample_pack(const wrnn_upsample_cfg *cfg, const float *mel, const float *aux, int B, int T,
+                       int target, int overlap, float *cond, void *stream);
+
+/* generate()'s float64 post-processing on the device (fatchord_version.py:243-258):
+ * decode_mu_law (utils/dsp.py:98-103, mu = n_classes) when `mu_law`, xfade_and_unfold
+ * (:342-405) of the `rows` folds when `batched` (else row 0), trim to wave_len, and
+ * output[-fade_len:] *= linspace(1, 0, fade_len) (fade_len = 20·hop_length).
+ *   y     [rows][steps] fp32 loop output (device);  wave [wave_len] float64 (device)
+ * WRNN_EINVAL when fade_len > wave_len (the reference's numpy broadcast error, T < 21). */
+int wrnn_postprocess(const float *y, int rows, int steps, int batched, int overlap, int mu_law,
+                     int n_classes, int wave_len, int fade_len, double *wave, void *stream);
+
+/* Message of the last failed stateless call on this thread. */
+const char *wrnn_cond_last_error(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -261,11 +261,17 @@ def generate(state, dims, mel: np.ndarray, batched: bool, target: int, overlap: 
         m = fold_with_overlap(m, target, overlap)
         a = fold_with_overlap(a, target, overlap)
     out, _ = fatchord_loop(state, dims.mode, m, a, noise)
+    return postprocess(out, batched, overlap, mu_law, dims.n_classes, wave_len, 20 * dims.hop_length)
+
+
+def postprocess(out: np.ndarray, batched: bool, overlap: int, mu_law: bool, n_classes: int, wave_len: int,
+                fade_len: int) -> np.ndarray:
+    """generate()'s float64 tail (fatchord_version.py:243-258) on the loop output [B][L]."""
     out = out.astype(np.float64)                                               # (:243-245)
     if mu_law:
-        out = decode_mu_law(out, dims.n_classes, False)                        # (:247-248)
+        out = decode_mu_law(out, n_classes, False)                             # (:247-248)
     out = xfade_and_unfold(out, overlap) if batched else out[0]                # (:250-253)
-    fade_out = np.linspace(1, 0, 20 * dims.hop_length)                         # (:256-258)
+    fade_out = np.linspace(1, 0, fade_len)                                     # (:256-258)
     out = out[:wave_len]
-    out[-20 * dims.hop_length:] *= fade_out
+    out[-fade_len:] *= fade_out
     return out

@@ -323,7 +323,8 @@ def test_generate_dropin_vs_reference(name):
     ref = fx["output"]
     assert out.dtype == np.float64 and out.shape == ref.shape
     if d.mode == "RAW":
-        # labels are discrete: equal labels ⇒ identical float64 post-processing
-        np.testing.assert_array_equal(out, ref)
+        # labels are discrete and bit-exact; the float64 post-processing runs on the device
+        # (condition.hip), where pow (mu-law) and sqrt (cross-fade) may round 1 ulp apart from libm
+        np.testing.assert_allclose(out, ref, rtol=1e-12, atol=1e-300)
     else:
         assert np.abs(out - ref).max() <= gf.MOL_TOL

@@ -27,20 +27,42 @@ def test_state_dict_keys_match_reference_layout():
 
 
 @pytest.mark.parametrize("batched", [False, True])
-def test_conditioning_matches_oracle(batched):
+def test_upsample_module_matches_oracle(batched):
+    """The torch UpsampleNetwork (training forward / reference API) + fold vs the oracle; the
+    generate() path's HIP kernel is checked against the same oracle in test_gpu_condition.py."""
     d = syn.TINY_MOL
     m, state = _model(d)
+    m.eval()
     mel = syn.make_mel(d.feat_dims, 24, 3)
-    cond, wave_len = m.conditioning(torch.from_numpy(mel)[None], batched, 1500, 200)
+    with torch.no_grad():
+        padded = m.pad_tensor(torch.from_numpy(mel)[None].transpose(1, 2), d.pad).transpose(1, 2)
+        mels, aux = m.upsample(padded)
+        if batched:
+            mels, aux = m.fold_with_overlap(mels, 1500, 200), m.fold_with_overlap(aux, 1500, 200)
     mp = orc.pad_tensor(mel.T[None], d.pad)[0].T
     um, ua = orc.upsample(mp, state, d.upsample_factors, d.res_blocks, d.pad)
     um, ua = um[None], ua[None]
     if batched:
         um, ua = orc.fold_with_overlap(um, 1500, 200), orc.fold_with_overlap(ua, 1500, 200)
-    ref = np.concatenate([um, ua], 2).transpose(1, 0, 2)
-    assert wave_len == (24 - 1) * d.hop_length
-    assert cond.shape == ref.shape
-    assert np.abs(cond.numpy() - ref).max() < 1e-5
+    assert mels.shape == um.shape and aux.shape == ua.shape
+    assert np.abs(mels.numpy() - um).max() < 1e-5 and np.abs(aux.numpy() - ua).max() < 1e-5
+
+
+@pytest.mark.parametrize("T,target,overlap", [(24, 1500, 200), (401, 11000, 550), (4811, 11000, 550),
+                                              (40, 0, 0), (7, 300, 100), (10, 2, 1)])
+def test_cond_shape_matches_fold_formula(T, target, overlap):
+    """wrnn_cond_shape (C-ABI, no GPU needed) reproduces fold_with_overlap's geometry."""
+    from wavernn_amd import condition
+    d = syn.DEFAULT_MOL
+    spec = condition.UpsampleSpec(d.feat_dims, d.res_out_dims, d.pad, d.upsample_factors,
+                                  [np.full(2 * s + 1, 1.0 / (2 * s + 1), np.float32) for s in d.upsample_factors])
+    L = T * d.hop_length
+    steps, rows = spec.shape(2 if target <= 0 else 1, T, target, overlap)
+    if target <= 0:
+        assert (steps, rows) == (L, 2)
+    else:
+        ref = orc.fold_with_overlap(np.zeros((1, L, 1), np.float32), target, overlap)
+        assert (rows, steps) == ref.shape[:2]
 
 
 def test_fold_matches_reference_formula():

@@ -17,7 +17,8 @@ STATUS = {0: "WRNN_OK", -1: "WRNN_EINVAL", -2: "WRNN_EHIP", -3: "WRNN_ENOWEIGHTS
 
 # Every symbol include/wavernn_amd.h declares (tests check the .so exports all of them).
 EXPORTS = ("wrnn_create", "wrnn_set_weights", "wrnn_generate", "wrnn_check", "wrnn_elapsed_ms",
-           "wrnn_query", "wrnn_last_error", "wrnn_destroy")
+           "wrnn_query", "wrnn_last_error", "wrnn_destroy", "wrnn_cond_shape", "wrnn_upsample_pack",
+           "wrnn_postprocess", "wrnn_cond_last_error")
 
 
 class WrnnError(RuntimeError):
@@ -40,6 +41,12 @@ class Info(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in ("grid", "units_rnn", "units_fc", "units_cls", "max_rows",
                                               "lds_bytes", "slab_floats", "num_cus", "rows_grid",
                                               "rows_units_rnn", "sparse_blocks", "split_grid", "last_path")]
+
+
+class UpsampleCfg(ctypes.Structure):
+    _fields_ = [("feat_dims", ctypes.c_int32), ("res_out_dims", ctypes.c_int32), ("pad", ctypes.c_int32),
+                ("n_scales", ctypes.c_int32), ("scales", ctypes.c_int32 * 4),
+                ("taps", ctypes.POINTER(ctypes.c_float) * 4)]
 
 
 _lib = None
@@ -71,8 +78,23 @@ def lib() -> ctypes.CDLL:
     L.wrnn_last_error.restype = ctypes.c_char_p
     L.wrnn_destroy.argtypes = [vp]
     L.wrnn_destroy.restype = None
+    pi = ctypes.POINTER(ctypes.c_int)
+    L.wrnn_cond_shape.argtypes = [ctypes.POINTER(UpsampleCfg), i32, i32, i32, i32, pi, pi]
+    L.wrnn_cond_shape.restype = i32
+    L.wrnn_upsample_pack.argtypes = [ctypes.POINTER(UpsampleCfg), vp, vp, i32, i32, i32, i32, vp, vp]
+    L.wrnn_upsample_pack.restype = i32
+    L.wrnn_postprocess.argtypes = [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp]
+    L.wrnn_postprocess.restype = i32
+    L.wrnn_cond_last_error.argtypes = []
+    L.wrnn_cond_last_error.restype = ctypes.c_char_p
     _lib = L
     return L
+
+
+def check_cond(code: int):
+    """Status of a stateless conditioning / post-processing call."""
+    if code != 0:
+        raise WrnnError(code, (lib().wrnn_cond_last_error() or b"").decode(errors="replace"))
 
 
 def check(handle, code: int):

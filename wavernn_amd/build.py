@@ -9,7 +9,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "_lib", "libwavernn_amd.so")
-SOURCES = [os.path.join(CSRC, f) for f in ("fatchord_loop.hip", "fatchord_split.hip", "fatchord_rows.hip", "deepmind_rows.hip", "capi.cpp")]
+SOURCES = [os.path.join(CSRC, f) for f in ("fatchord_loop.hip", "fatchord_split.hip", "fatchord_rows.hip", "deepmind_rows.hip", "condition.hip", "capi.cpp")]
 HEADERS = [os.path.join(CSRC, f) for f in ("fatchord_loop.h", "fatchord_split.h", "fatchord_rows.h", "deepmind_rows.h", "wrnn_device.h",
                                            "rows_device.h")] + \
     [os.path.join(REPO, "include", "wavernn_amd.h")]

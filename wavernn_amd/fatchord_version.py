@@ -8,8 +8,11 @@ changes is where the sample loop runs: instead of the host-driven per-step loop
 HIP kernel through the C-ABI (`FatchordLoop`).  There is no CPU fallback: the model must
 live on a GPU and the HIP library must be built, otherwise generate() raises.
 
-Pre-processing (pad, UpsampleNetwork, fold) runs as torch ops on the GPU; post-processing
-(mu-law, cross-fade/unfold, fade-out) is the reference's float64 numpy arithmetic.
+Pre-processing: MelResNet as torch modules (MIOpen), then ONE HIP kernel for pad + the
+stretch/box-conv chain + crop + aux stretch + fold + time-major pack (`condition.upsample_pack`).
+Post-processing (mu-law, cross-fade/unfold, trim, fade-out) is one float64 HIP kernel
+(`condition.postprocess`) with the reference's operation order; only the finished waveform
+crosses to the host.
 """
 from __future__ import annotations
 
@@ -22,7 +25,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import dsp
+from . import condition, dsp
 from .loop import LOOP_KEYS, FatchordLoop, noise_width
 
 
@@ -176,22 +179,32 @@ class WaveRNN(nn.Module):
         return self._loop
 
     # ---------------------------------------------------------------------- generate
+    def _upsample_spec(self) -> condition.UpsampleSpec:
+        """Host copy of the box-conv taps, refreshed when those parameters change."""
+        convs = [m.weight for m in self.upsample.up_layers if isinstance(m, nn.Conv2d)]
+        key = tuple((w.data_ptr(), w._version) for w in convs)
+        if getattr(self, "_up_key", None) != key:
+            self._up_spec = condition.UpsampleSpec.from_module(self.upsample, self.feat_dims, self.pad)
+            self._up_key = key
+        return self._up_spec
+
     @torch.no_grad()
     def conditioning(self, mels, batched, target, overlap):
         """pad → upsample → (fold) → time-major [L][B][feat + 4·aux] (fatchord_version.py:183-190).
-        Runs the upsample network in eval mode (BatchNorm running statistics) like generate()."""
+        MelResNet runs as torch modules in eval mode (BatchNorm running statistics) like
+        generate(); everything after it is the `wrnn_upsample_pack` HIP kernel."""
+        device = next(self.parameters()).device
+        if device.type != 'cuda':
+            raise RuntimeError("WaveRNN.generate runs on the MI355X HIP path: move the model to a GPU "
+                               "(model.to('cuda')); there is no CPU fallback")
         was_training = self.training
         self.eval()
         try:
-            device = next(self.parameters()).device
             mels = torch.as_tensor(mels, device=device).to(torch.float32)
             wave_len = (mels.size(-1) - 1) * self.hop_length
-            mels = self.pad_tensor(mels.transpose(1, 2), pad=self.pad, side='both')
-            mels, aux = self.upsample(mels.transpose(1, 2))
-            if batched:
-                mels = self.fold_with_overlap(mels, target, overlap)
-                aux = self.fold_with_overlap(aux, target, overlap)
-            cond = torch.cat([mels, aux], dim=2).transpose(0, 1).contiguous()
+            padded = self.pad_tensor(mels.transpose(1, 2), pad=self.pad, side='both').transpose(1, 2)
+            aux = self.upsample.resnet(padded)
+            cond = condition.upsample_pack(self._upsample_spec(), mels, aux, target if batched else 0, overlap)
         finally:
             self.train(was_training)
         return cond, wave_len
@@ -216,19 +229,12 @@ class WaveRNN(nn.Module):
             if seed is None:
                 seed = int(torch.randint(0, 2 ** 62, (1,)).item())
             out, _ = loop.generate(cond, noise=nz, seed=seed)
-            output = out.cpu().numpy().astype(np.float64)
+            # mu-law, xfade_and_unfold / row 0, trim, fade-out (:243-258) in float64 on the device
+            output = condition.postprocess(out, batched, overlap, mu_law, self.n_classes, wave_len,
+                                           20 * self.hop_length).cpu().numpy()
         self.last_gen_seconds = time.time() - start
         if verbose:
             self.gen_display(seq_len - 1, seq_len, b_size, start)
-        if mu_law:
-            output = dsp.decode_mu_law(output, self.n_classes, False)
-        if batched:
-            output = self.xfade_and_unfold(output, target, overlap)
-        else:
-            output = output[0]
-        fade_out = np.linspace(1, 0, 20 * self.hop_length)
-        output = output[:wave_len]
-        output[-20 * self.hop_length:] *= fade_out
         dsp.save_wav(output, save_path, self.sample_rate)
         self.train()
         return output
@@ -278,7 +284,9 @@ class WaveRNN(nn.Module):
     @staticmethod
     def xfade_and_unfold(y, target, overlap):
         """Equal-power cross-fade of folds and overlap-add back to 1-D float64
-        (fatchord_version.py:342-405; `fade_out` keeps the reference's leading ones)."""
+        (fatchord_version.py:342-405; `fade_out` keeps the reference's leading ones).  Host
+        numpy for callers of the reference API; generate() runs the device kernel
+        (`condition.postprocess`)."""
         num_folds, length = y.shape
         target = length - 2 * overlap
         total_len = num_folds * (target + overlap) + overlap
