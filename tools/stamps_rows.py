@@ -34,6 +34,10 @@ def main(mode="MOL", B=10, L=2000):
     G, S, K = raw[:3].view(np.int32)
     st = raw[3:].reshape(G, S, K).astype(np.int64)[:, 50:S - 1]
     print(f"{mode} B={B} L={L} grid={G}: {ms * 1e3 / L:.2f} us/step incl. terms GEMM (stamped build)")
+    for k, name in ((5, "  fc1: compute wave 0 busy (sum)"), (8, "  fc1: lead loader DMA (sum)")):
+        v = st[:, :, k].ravel() * 10e-3
+        if (v > 0).any():
+            print(f"  {name:34s} median {np.median(v[v > 0]):7.3f} us")
     for a, b, name in SEG:
         m = (st[:, :, a] > 0) & (st[:, :, b] > 0)
         if not m.any():

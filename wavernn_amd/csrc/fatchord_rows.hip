@@ -29,11 +29,17 @@
 
 namespace wrnn {
 
+// cache policy of the stage-tile LDS-DMA: 0 = plain behind an agent acquire, 16 = sc1
+#ifndef WRNN_TILE_CPOL
+#define WRNN_TILE_CPOL 16
+#endif
+constexpr int kTileCpol = WRNN_TILE_CPOL;
+
 // kRF = 512 instantiates the shipped dims (rnn_dims = fc_dims = 512) with compile-time dot
 // lengths; 0 = runtime dims.  SPARSE: block-sparse GRU weights (one 4-unit block-row per gate,
 // U = 4), the GRU matvecs run one engine per activation row over the nonzero blocks.
 template <bool MOL, int kRF, bool SPARSE>
-__global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
+__global__ __launch_bounds__(kRowsThreads) void fatchord_rows_kernel(RowsArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, row = lane >> 4;
     const int w = blockIdx.x;
@@ -55,8 +61,10 @@ __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
     const int Uv = max(0, min(U, R - w * U));
     const int UFv = max(0, min(UF, F - w * UF));
     const int UCv = MOL ? 0 : max(0, min(UC, NC - w * UC));
-    const bool loader = wave == kLoaderWave;
+    const bool loader = wave >= kRowsLead;             // waves 8-11: tile DMA
+    const bool lead = wave == kRowsLead;               // wave 8: flag polls, terms, draws, samplers
     const bool compute = !loader;
+    int *go = abort_flag + 1;                          // LDS: wave 8 → other loaders, "flags seen"
     const int eng = wave * 4 + row;                    // dot engine of this lane (compute waves)
     const size_t hop_sz = (size_t)2 * B * KA;
     unsigned *dbgw = a.dbg ? a.dbg + (size_t)w * a.dbg_steps * kStamps : nullptr;
@@ -71,11 +79,20 @@ __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
         if (tid == 0) __hip_atomic_store(flagp(hop) + w * kFlagStride, (unsigned)t + 1u, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT);
     };
-    // LDS-DMA (sc1) of n floats (contiguous rows) from src into dst, issued by the loader wave
+    // LDS-DMA (sc1) of n floats (contiguous rows) from src into dst, issued by one wave
     auto dma = [&](float *dst, const float *src, int n) {
         for (int c = 0; c < n; c += 256)
             if (c + lane * 4 < n)
                 __builtin_amdgcn_global_load_lds(WRNN_GPTR(src + c + lane * 4), WRNN_LPTR(dst + c), 16, 0, 16);
+    };
+    // the same split over the four loader waves (1 KiB pieces, round robin).  Plain (L2-cached)
+    // loads behind the lead wave's agent-scope acquire (MI355X_MICROARCH.md "Valid forms",
+    // consumer: one relaxed poll → one agent acquire → vmcnt(0) → plain loads): the 32 CUs of an
+    // XCD then share one fetch of each activation line instead of each pulling it past L2.
+    auto dma_part = [&](float *dst, const float *src, int n) {
+        for (int c = (wave - kRowsLead) * 256; c < n; c += kRowsLoaders * 256)
+            if (c + lane * 4 < n)
+                __builtin_amdgcn_global_load_lds(WRNN_GPTR(src + c + lane * 4), WRNN_LPTR(dst + c), 16, 0, kTileCpol);
     };
     // draws of step t for this workgroup's sampled rows → nz slot (t & 1); MoL turned into sampler terms
     auto load_noise = [&](int t, int id, int nl) {
@@ -102,14 +119,17 @@ __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
     {
         const float4 *src = reinterpret_cast<const float4 *>(a.slab + (size_t)w * s.total);
         float4 *dst = reinterpret_cast<float4 *>(smem + ll.slab);
-        for (int i = tid; i < slab_lds / 4; i += kThreads) dst[i] = src[i];
+        for (int i = tid; i < slab_lds / 4; i += kRowsThreads) dst[i] = src[i];
         const float *cs = a.state + (size_t)w * B * SW;
-        for (int i = tid; i < B * SW; i += kThreads) st[i] = a.t0 > 0 ? cs[i] : 0.0f;
+        for (int i = tid; i < B * SW; i += kRowsThreads) st[i] = a.t0 > 0 ? cs[i] : 0.0f;
         const float *cx = a.state + (size_t)G * B * SW;
-        for (int i = tid; i < B; i += kThreads) xs[i] = a.t0 > 0 ? cx[i] : 0.0f;   // x = 0 (:196)
-        if (tid == 0) *abort_flag = 0;
-        load_terms(0, tid, kThreads);
-        load_noise(a.t0, tid, kThreads);
+        for (int i = tid; i < B; i += kRowsThreads) xs[i] = a.t0 > 0 ? cx[i] : 0.0f;   // x = 0 (:196)
+        if (tid == 0) {
+            *abort_flag = 0;
+            *go = -1;
+        }
+        load_terms(0, tid, kRowsThreads);
+        load_noise(a.t0, tid, kRowsThreads);
     }
     __syncthreads();
 
@@ -126,29 +146,46 @@ __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
         if (dbgw && tid == 0 && t_cur - a.t0 < a.dbg_steps)                                        \
             dbgw[(size_t)(t_cur - a.t0) * kStamps + (k)] = (unsigned)__builtin_amdgcn_s_memrealtime(); \
     } while (0)
-    // Stage driver.  The loader wave polls the hop's flags and issues every tile DMA, waiting
-    // only for its own loads; the compute waves run the jobs and store their outputs (sc1), and
-    // drain those stores once, before the stage's signal.  Returns false on abort.
+    // Stage driver.  Wave 8 polls the hop's flags and releases the other loader waves through an
+    // LDS word; the four loader waves split every tile DMA, each waiting only for its own loads;
+    // the compute waves run the jobs and store their outputs (sc1), and drain those stores once,
+    // before the stage's signal.  Returns false on abort.
     auto run_stage = [&](int hop, int K, auto &&jobs) -> bool {
         const float *src = actp(hop, t_cur);
         const int ntiles = (B + TB - 1) / TB;
         if (loader) {
-            wait_flags(flagp(hop), G, (unsigned)t_cur + 1u, a.ctl, a.timeout_ticks, t_cur, hop, abort_flag);
-            if (!*abort_flag) dma(tbuf(0), src, min(TB, B) * K);
+            const int go_val = (t_cur + 1) * kRowsHops + hop;
+            if (lead) {
+                wait_flags(flagp(hop), G, (unsigned)t_cur + 1u, a.ctl, a.timeout_ticks, t_cur, hop, abort_flag);
+                if (kTileCpol == 0) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                __hip_atomic_store(go, go_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {
+                while (__hip_atomic_load(go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != go_val)
+                    __builtin_amdgcn_s_sleep(1);
+            }
+            if (!*reinterpret_cast<volatile int *>(abort_flag)) dma_part(tbuf(0), src, min(TB, B) * K);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         bar();
         if (hop == RH_H2) RSTAMP_T(13);
         if (*abort_flag) return false;
+        unsigned long long busy = 0;                   // diagnostics: summed job / DMA time of the fc1 stage
         for (int k = 0; k < ntiles; ++k) {
             const int tb0 = k * TB, nb = min(TB, B - tb0);
+            const unsigned long long c0 = dbgw ? __builtin_amdgcn_s_memrealtime() : 0;
             if (loader && k + 1 < ntiles) {
-                dma(tbuf(k + 1), src + (size_t)(tb0 + TB) * K, min(TB, B - tb0 - TB) * K);
+                dma_part(tbuf(k + 1), src + (size_t)(tb0 + TB) * K, min(TB, B - tb0 - TB) * K);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
             if (compute) jobs(tbuf(k), tb0, nb);
+            if (dbgw) busy += __builtin_amdgcn_s_memrealtime() - c0;
             bar();
         }
+        if (dbgw && hop == RH_H2 && t_cur - a.t0 < a.dbg_steps && lane == 0 && (wave == 0 || lead))
+            dbgw[(size_t)(t_cur - a.t0) * kStamps + (lead ? 8 : 5)] = (unsigned)busy;
         if (hop == RH_H2) RSTAMP_T(14);
         if (compute) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         bar();
@@ -177,7 +214,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
         // ---- GRU1 (:208-210), own units, every row
         if (compute) {
             float *h1o = actp(RH_H1, t);
-            for (int i = tid; i < B * Uv; i += kCompute) {
+            for (int i = tid; i < B * Uv; i += kRowsCompute) {
                 const int b = i / Uv, u = i - b * Uv, j = w * U + u;
                 const float x = xs[b];
                 const float *Tb = T + b * NT;
@@ -209,7 +246,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
                 // block) dense, (row) sparse
                 const int nbb = (nb + kNX - 1) / kNX, n1 = SPARSE ? nb : Uv * nbb, nj1 = round4(n1);
                 const int nj2 = 2 * nj1, nj3 = nj2 + nUF2 * nbb;
-                for (int jb = eng; jb < nj3; jb += kDotEngines) {
+                for (int jb = eng; jb < nj3; jb += kRowsEngines) {
                     if (jb < nj2) {
                         const bool crit = jb < nj1;
                         const int jj = crit ? jb : jb - nj1;
@@ -276,7 +313,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
                 // [fc1 rows | GH2 of the next step]
                 const int nbb = (nb + kNX - 1) / kNX, n1 = nUF2 * nbb, nj1 = round4(n1);
                 const int nj2 = nj1 + (SPARSE ? nb : Uv * nbb);
-                for (int jb = eng; jb < nj2; jb += kDotEngines) {
+                for (int jb = eng; jb < nj2; jb += kRowsEngines) {
                     if (jb < nj1) {
                         if (jb >= n1) continue;
                         const int r0 = 2 * (jb % nUF2), bb = jb / nUF2;
@@ -327,7 +364,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
             float *f2o = actp(RH_F2, t);
             const bool ok = run_stage(RH_F1, F, [&](const float *tl_, int tb0, int nb) {
                 const int nbb = (nb + kNX - 1) / kNX, nj = nUF2 * nbb;
-                for (int jb = eng; jb < nj; jb += kDotEngines) {
+                for (int jb = eng; jb < nj; jb += kRowsEngines) {
                     const int r0 = 2 * (jb % nUF2), bb = jb / nUF2;
                     const int nx = min(kNX, nb - bb * kNX), b = tb0 + bb * kNX + li;
                     float acc[2];
@@ -353,7 +390,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
             float *lgo = actp(RH_LG, t);
             const bool ok = run_stage(RH_F2, F, [&](const float *tl_, int tb0, int nb) {
                 const int nbb = (nb + kNX - 1) / kNX, nj = nUC2 * nbb;
-                for (int jb = eng; jb < nj; jb += kDotEngines) {
+                for (int jb = eng; jb < nj; jb += kRowsEngines) {
                     const int r0 = 2 * (jb % nUC2), bb = jb / nUC2;
                     const int nx = min(kNX, nb - bb * kNX), b = tb0 + bb * kNX + li;
                     float acc[2];
@@ -374,7 +411,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
             const int hop = MOL ? RH_F2 : RH_LG;
             const int K = MOL ? F : NC;
             const float *src = actp(hop, t);
-            if (loader) {
+            if (lead) {
                 wait_flags(flagp(hop), G, want, a.ctl, a.timeout_ticks, t, hop, abort_flag);
                 if (!*abort_flag)
                     for (int sr = 0; sr < NS && w + sr * G < B; ++sr)
@@ -387,16 +424,16 @@ __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
             if (MOL) {   // the 30 head rows (replicated in every workgroup) against f2 of each sampled row
                 if (compute)
                     for (int sr = 0; sr < NS && w + sr * G < B; ++sr)
-                        for (int c0 = eng; c0 < NC; c0 += 2 * kDotEngines) {
-                            const int ca = c0, cb = min(c0 + kDotEngines, NC - 1);
+                        for (int c0 = eng; c0 < NC; c0 += 2 * kRowsEngines) {
+                            const int ca = c0, cb = min(c0 + kRowsEngines, NC - 1);
                             const float2 v = row_dot2(head + ca * F, head + cb * F, tile + sr * ll.KT, F / 4, li);
                             if (li == 0) lgs[sr * ll.ncp + ca] = v.x + head[s.b3 - s.w3 + ca];
-                            if (li == 0 && c0 + kDotEngines < NC) lgs[sr * ll.ncp + cb] = v.y + head[s.b3 - s.w3 + cb];
+                            if (li == 0 && c0 + kRowsEngines < NC) lgs[sr * ll.ncp + cb] = v.y + head[s.b3 - s.w3 + cb];
                         }
                 bar();
             }
             if (compute)
-                for (int sr = wave; sr < NS; sr += kWaves) {
+                for (int sr = wave; sr < NS; sr += kRowsComputeWaves) {
                     const int b = w + sr * G;
                     if (b >= B) break;
                     const float *u = nzs + (t & 1) * NS * ll.nkp + sr * ll.nkp;
@@ -419,7 +456,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
         }
 
         // loader: terms and draws of the next step, while wave 0 collects x
-        if (loader && tl + 1 < a.Lc) {
+        if (lead && tl + 1 < a.Lc) {
             load_terms(tl + 1, lane, 64);
             load_noise(t + 1, lane, 64);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -439,9 +476,9 @@ __global__ __launch_bounds__(kThreads) void fatchord_rows_kernel(RowsArgs a) {
     // carried state for the next launch of this generate()
     {
         float *cs = a.state + (size_t)w * B * SW;
-        for (int i = tid; i < B * SW; i += kThreads) cs[i] = st[i];
+        for (int i = tid; i < B * SW; i += kRowsThreads) cs[i] = st[i];
         if (w == 0)
-            for (int i = tid; i < B; i += kThreads) a.state[(size_t)G * B * SW + i] = xs[i];
+            for (int i = tid; i < B; i += kRowsThreads) a.state[(size_t)G * B * SW + i] = xs[i];
     }
 }
 
@@ -485,7 +522,7 @@ static const void *pick_rows_kernel(const RowsArgs &a) {
 hipError_t launch_rows(const RowsArgs &a, size_t lds_bytes, hipStream_t st) {
     RowsArgs args = a;
     void *params[] = {&args};
-    return hipLaunchKernel(pick_rows_kernel(a), dim3(a.G), dim3(kThreads), params, lds_bytes, st);
+    return hipLaunchKernel(pick_rows_kernel(a), dim3(a.G), dim3(kRowsThreads), params, lds_bytes, st);
 }
 
 hipError_t prepare_rows_kernel(int max_lds_bytes) {
@@ -500,7 +537,7 @@ hipError_t rows_occupancy(int *blocks_per_cu, size_t lds_bytes) {
     int best = 1 << 30;
     for (const void *k : {WRNN_ROWS_KERNELS}) {
         int n = 0;
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kThreads, lds_bytes);
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kRowsThreads, lds_bytes);
         if (e != hipSuccess) return e;
         best = n < best ? n : best;
     }

@@ -7,6 +7,9 @@
 
 namespace wrnn {
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+
 // ------------------------------------------------------------------ wave-level helpers
 #define WRNN_DPP(v, ctrl) \
     __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, (v)), (ctrl), 0xF, 0xF, false))
@@ -290,20 +293,23 @@ __device__ __forceinline__ float row_reduce_scatter4(const float (&p)[4], int la
 template <int NW, int KI = 0>
 __device__ __forceinline__ void bdot4(const float *__restrict__ W, int ws, const float *__restrict__ X, int xs, int nx,
                                       int K4, int li, float (&out)[NW]) {
+    // packed fp32 FMAs (v_pk_fma_f32: two lanes of work per instruction, the fp32 vector peak):
+    // each (weight row, activation row) pair keeps an even-k and an odd-k partial sum, added at
+    // the end — the float4 halves .xy / .zw are already aligned register pairs, so no moves
     constexpr int NX = 4;
-    const float4 *w4[NW];
-    const float4 *x4[NX];
+    const f4v *w4[NW];
+    const f4v *x4[NX];
 #pragma unroll
-    for (int i = 0; i < NW; ++i) w4[i] = reinterpret_cast<const float4 *>(W + i * ws) + li;
+    for (int i = 0; i < NW; ++i) w4[i] = reinterpret_cast<const f4v *>(W + i * ws) + li;
 #pragma unroll
-    for (int j = 0; j < NX; ++j) x4[j] = reinterpret_cast<const float4 *>(X + (j < nx ? j : 0) * xs) + li;
-    float acc[NW][NX];
+    for (int j = 0; j < NX; ++j) x4[j] = reinterpret_cast<const f4v *>(X + (j < nx ? j : 0) * xs) + li;
+    f2v acc[NW][NX];
 #pragma unroll
     for (int i = 0; i < NW; ++i)
 #pragma unroll
-        for (int j = 0; j < NX; ++j) acc[i][j] = 0.0f;
+        for (int j = 0; j < NX; ++j) acc[i][j] = f2v{0.0f, 0.0f};
     auto step = [&](int k) {
-        float4 wv[NW], xv[NX];
+        f4v wv[NW], xv[NX];
 #pragma unroll
         for (int i = 0; i < NW; ++i) wv[i] = w4[i][16 * k];
 #pragma unroll
@@ -312,12 +318,8 @@ __device__ __forceinline__ void bdot4(const float *__restrict__ W, int ws, const
         for (int i = 0; i < NW; ++i)
 #pragma unroll
             for (int j = 0; j < NX; ++j) {
-                float a = acc[i][j];
-                a = fmaf(wv[i].x, xv[j].x, a);
-                a = fmaf(wv[i].y, xv[j].y, a);
-                a = fmaf(wv[i].z, xv[j].z, a);
-                a = fmaf(wv[i].w, xv[j].w, a);
-                acc[i][j] = a;
+                acc[i][j] = __builtin_elementwise_fma(wv[i].xy, xv[j].xy, acc[i][j]);
+                acc[i][j] = __builtin_elementwise_fma(wv[i].zw, xv[j].zw, acc[i][j]);
             }
     };
     if (KI > 0) {
@@ -327,7 +329,12 @@ __device__ __forceinline__ void bdot4(const float *__restrict__ W, int ws, const
         for (int k = 0; 16 * k + li < K4; ++k) step(k);
     }
 #pragma unroll
-    for (int i = 0; i < NW; ++i) out[i] = row_reduce_scatter4(acc[i], li);
+    for (int i = 0; i < NW; ++i) {
+        float p[NX];
+#pragma unroll
+        for (int j = 0; j < NX; ++j) p[j] = acc[i][j].x + acc[i][j].y;
+        out[i] = row_reduce_scatter4(p, li);
+    }
 }
 
 // Block-sparse gate rows of one 4-unit block-row: out[g] (lane li) = Σ_k blk[g][k] · x[4·col[g][k] …]
