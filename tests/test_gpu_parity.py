@@ -144,6 +144,51 @@ def test_rows_many_rows_tiled():
 
 
 @pytest.mark.parametrize("mode", ["MOL", "RAW"])
+@pytest.mark.parametrize("B", [2, 5, 40])
+def test_rows_two_groups_vs_oracle(mode, B, monkeypatch):
+    """Two row groups in one launch (G/2 workgroups each, twice the units per workgroup; the
+    large-B layout): oracle parity, also for uneven and tiny groups."""
+    from oracle import oracle
+    monkeypatch.setenv("WRNN_PATH", "rows")
+    monkeypatch.setenv("WRNN_ROW_GROUPS", "2")
+    d = syn.DEFAULT_MOL if mode == "MOL" else syn.DEFAULT_RAW
+    L = 300
+    state = syn.make_fatchord_state(d, 91)
+    mels, aux = syn.make_conditioning(B, L, d.feat_dims, d.res_out_dims, 92)
+    noise = syn.make_noise(mode, B, L, d.n_classes, 93)
+    ref, ref_lab = oracle.fatchord_loop(state, mode, mels, aux, noise)
+    loop = _loop(d)
+    loop.set_weights(state)
+    out, lab = loop.generate(_cond(mels, aux), noise=torch.from_numpy(noise).to(DEV), want_labels=True)
+    if mode == "RAW":
+        _report_raw(lab.cpu().numpy(), ref_lab)
+    else:
+        assert np.abs(out.cpu().numpy() - ref).max() <= gf.MOL_TOL
+
+
+@pytest.mark.parametrize("mode", ["MOL", "RAW"])
+def test_row_groups_agree_under_philox(mode, monkeypatch):
+    """One group of G workgroups vs two groups of G/2: same Philox keying by global row, so the
+    same audio (RAW labels equal, MoL within tolerance)."""
+    monkeypatch.setenv("WRNN_PATH", "rows")
+    d = syn.DEFAULT_MOL if mode == "MOL" else syn.DEFAULT_RAW
+    B, L = 30, 400
+    state = syn.make_fatchord_state(d, 95)
+    mels, aux = syn.make_conditioning(B, L, d.feat_dims, d.res_out_dims, 96)
+    cond = _cond(mels, aux)
+    res = {}
+    for g in ("1", "2"):
+        monkeypatch.setenv("WRNN_ROW_GROUPS", g)
+        loop = _loop(d)
+        loop.set_weights(state)
+        res[g] = loop.generate(cond, seed=5, want_labels=(mode == "RAW"))
+    if mode == "RAW":
+        assert torch.equal(res["1"][1], res["2"][1])
+    else:
+        assert (res["1"][0] - res["2"][0]).abs().max().item() <= 2 * gf.MOL_TOL
+
+
+@pytest.mark.parametrize("mode", ["MOL", "RAW"])
 def test_paths_agree_under_philox(mode, monkeypatch):
     """Both kernels key the in-kernel Philox draws identically (seed, global row, step, k), so
     they generate the same audio (RAW: same labels; MoL: within the fp tolerance of each)."""

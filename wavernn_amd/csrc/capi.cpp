@@ -25,7 +25,7 @@ hipError_t launch_ci_gemm(const float *cond, int CD, int Bt, int b0, int Bc, int
                           const float *bias, int N, int K, float *cI, int ldc, hipStream_t st);
 hipError_t launch_pack_terms_input(const float *cond, int CD, int Bt, int b0, int B, int t0, int Lc, int feat, int A,
                                    int R, int KX, float *X, hipStream_t st);
-hipError_t launch_rows(const RowsArgs &a, size_t lds_bytes, hipStream_t st);
+hipError_t launch_rows(const RowsArgs &a, const RowsGroup *g1, size_t lds_bytes, hipStream_t st);
 hipError_t prepare_rows_kernel(int max_lds_bytes);
 hipError_t rows_occupancy(int *blocks_per_cu, size_t lds_bytes);
 hipError_t launch_dm(const DmArgs &a, size_t lds_bytes, hipStream_t st);
@@ -42,6 +42,14 @@ bool split_has_kernel(int R, int F);
 }  // namespace wrnn
 
 using namespace wrnn;
+
+// One partition of the loop weights over the multi-row kernel's workgroups (see wrnn_ctx).
+struct RowsPart {
+    RowsSlab rs{};
+    int rU = 0, rG = 0, rUF = 0, rUC = 0, NT = 0;
+    bool ok = false;
+    float *d_slab = nullptr, *d_Wt = nullptr;
+};
 
 struct wrnn_ctx {
     wrnn_config cfg{};
@@ -72,8 +80,12 @@ struct wrnn_ctx {
     float *d_rslab = nullptr, *d_Wt = nullptr;      // per-workgroup slabs, terms-GEMM weights [G·NT][KX]
     float *d_X = nullptr, *d_T = nullptr, *d_act = nullptr, *d_state = nullptr;
     size_t X_cap = 0, T_cap = 0, act_cap = 0, state_cap = 0;   // floats
-    unsigned *d_flags = nullptr;
-    unsigned long long *d_xr = nullptr;             // x granules
+    unsigned *d_flags = nullptr;                    // [2 row groups][kRowsHops][kFlagSlots][kFlagStride]
+    unsigned long long *d_xr = nullptr;             // x granules, [2 row groups][kXReps][kXRepStride]
+    // the same weights over G/2 workgroups (twice the units each) for two row groups per launch
+    // (large B: halves the activation rows every workgroup streams per stage); swapped into the
+    // r* fields above while in use
+    RowsPart g2{};
     rocblas_handle blas = nullptr;
     int last_path = 0;                              // 1 = latency, 2 = rows, 3 = deepmind, 4 = split
     // deepmind_version (WRNN_MODE_DM): deepmind_rows.hip
@@ -427,6 +439,50 @@ int rows_tile_for(const wrnn_ctx &h, int B, bool head_lds) {
     return 0;
 }
 
+void swap_part(wrnn_ctx &h, RowsPart &p) {
+    std::swap(h.rs, p.rs);
+    std::swap(h.rU, p.rU);
+    std::swap(h.rG, p.rG);
+    std::swap(h.rUF, p.rUF);
+    std::swap(h.rUC, p.rUC);
+    std::swap(h.NT, p.NT);
+    std::swap(h.rows_ok, p.ok);
+    std::swap(h.d_rslab, p.d_slab);
+    std::swap(h.d_Wt, p.d_Wt);
+}
+
+// Swaps a partition in for a scope
+struct PartScope {
+    wrnn_ctx &h;
+    RowsPart &p;
+    bool on;
+    PartScope(wrnn_ctx &h_, RowsPart &p_, bool on_) : h(h_), p(p_), on(on_) {
+        if (on) swap_part(h, p);
+    }
+    ~PartScope() {
+        if (on) swap_part(h, p);
+    }
+};
+
+// The two-group partition: dense weights over G/2 workgroups (G even)
+void set_group_partition(wrnn_ctx &h) {
+    h.g2 = RowsPart{};
+    if (h.G % 2 || h.G < 8) return;
+    RowsPart flat{};
+    swap_part(h, flat);   // h.r* empty, flat holds the current partition
+    const int R = h.cfg.rnn_dims, F = h.cfg.fc_dims;
+    const bool mol = h.cfg.mode == WRNN_MODE_MOL;
+    h.rG = h.G / 2;
+    h.rU = (R + h.rG - 1) / h.rG;
+    h.rUF = (F + h.rG - 1) / h.rG;
+    h.rUC = mol ? 0 : (h.cfg.n_classes + h.rG - 1) / h.rG;
+    h.NT = rows_terms(h.rU, h.rUF);
+    h.rs = make_rows_slab(h, 0);
+    h.rows_ok = rows_tile_for(h, 16, false) >= 4;
+    swap_part(h, flat);   // h.r* = flat again, `flat` = the group partition
+    h.g2 = flat;
+}
+
 // ------------------------------------------------------------------ deepmind_version packing
 DmSlab make_dm_slab(const wrnn_ctx &h) {
     const int H = h.cfg.rnn_dims, S = H / 2;
@@ -663,15 +719,28 @@ int grow(wrnn_t *h, float *&p, size_t &cap, size_t n) {
     return WRNN_OK;
 }
 
-// B rows through the multi-row kernel: row groups of <= kRowsMax, time chunks sized so the
-// precomputed terms stay within WRNN_TERMS_MB (default 8192 MiB).
+// B rows through the multi-row kernel: row blocks of <= kRowsMax rows per launch, time chunks
+// sized so the precomputed terms stay within WRNN_TERMS_MB (default 8192 MiB).  Blocks of
+// >= kGroupRows rows run as two row groups of half the rows on G/2 workgroups each (the grouped
+// partition, dense weights only; WRNN_ROW_GROUPS=1|2 forces one or the other).  Measured on
+// MI355X (MoL 512, us/step, one group → two): B=2 17.2 → 15.7, B=10 18.3 → 16.9, B=32 26.6 →
+// 19.5, B=115 51.2 → 40.2: half the rows streamed per stage and half the flags per hop.
+constexpr int kGroupRows = 2;
+
 int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed, int64_t row_offset,
                   float *out, int32_t *labels, hipStream_t st) {
     const wrnn_config &c = h->cfg;
+    const char *grp_env = std::getenv("WRNN_ROW_GROUPS");
+    const int grp_force = grp_env ? std::atoi(grp_env) : 0;
+    const bool can_group = h->g2.ok && !h->sparse && grp_force != 1;
+    const bool grouped = can_group && B >= 2 && (grp_force == 2 || std::min(B, kRowsMax) >= kGroupRows);
+    PartScope ps(*h, h->g2, grouped);          // h->r*, rs, NT, d_rslab, d_Wt = the grouped partition
+    const int ng = grouped ? 2 : 1;
     const int R = c.rnn_dims, A = c.aux_dims, N = h->rG * h->NT;
+    const size_t flag_words = (size_t)kRowsHops * kFlagSlots * kFlagStride, xr_words = (size_t)kXReps * kXRepStride;
     if (!h->d_flags) {
-        HIP_TRY(h, hipMalloc(&h->d_flags, (size_t)kRowsHops * kFlagSlots * kFlagStride * 4));
-        HIP_TRY(h, hipMalloc(&h->d_xr, (size_t)kXReps * kXRepStride * 8));
+        HIP_TRY(h, hipMalloc(&h->d_flags, 2 * flag_words * 4));
+        HIP_TRY(h, hipMalloc(&h->d_xr, 2 * xr_words * 8));
     }
     if (!h->blas && rocblas_create_handle(&h->blas) != rocblas_status_success)
         return fail(h, WRNN_EHIP, "rocblas_create_handle failed");
@@ -688,32 +757,38 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
     }
     for (int b0 = 0; b0 < B;) {
         int Bl = std::min(B - b0, kRowsMax);
-        while (Bl > 1 && rows_tile_for(*h, Bl) == 0 && rows_tile_for(*h, Bl, false) == 0) --Bl;
+        auto group_rows = [&](int bl, int g) { const int b_0 = (bl + ng - 1) / ng; return g == 0 ? b_0 : bl - b_0; };
+        while (Bl > 1 && rows_tile_for(*h, group_rows(Bl, 0)) == 0 && rows_tile_for(*h, group_rows(Bl, 0), false) == 0) --Bl;
+        const int Bg = group_rows(Bl, 0);          // rows of group 0 (>= those of group 1)
         // the MoL head stays in LDS while all rows fit one tile next to it; beyond that, larger
         // tiles are worth more than an LDS-resident head (the samplers then read it from L2)
         const bool mol = c.mode == WRNN_MODE_MOL;
-        const int tb_in = rows_tile_for(*h, Bl);
-        const bool head_lds = !mol || tb_in >= std::min(Bl, 16) || rows_tile_for(*h, Bl, false) == 0;
-        const int TB = head_lds ? tb_in : rows_tile_for(*h, Bl, false);
+        const int tb_in = rows_tile_for(*h, Bg);
+        const bool head_lds = !mol || tb_in >= std::min(Bg, 16) || rows_tile_for(*h, Bg, false) == 0;
+        const int TB = head_lds ? tb_in : rows_tile_for(*h, Bg, false);
         if (TB == 0) return fail(h, WRNN_EUNSUPPORTED, "rows kernel: one row of state does not fit LDS");
         const int SW = rows_state_width(h->rU, h->rUF);
         const int Lc_max = (int)std::max(1.0, std::min((double)L, budget / ((double)Bl * (N + h->KX))));
-        if (grow(h, h->d_X, h->X_cap, (size_t)Lc_max * Bl * h->KX) ||
-            grow(h, h->d_T, h->T_cap, (size_t)Lc_max * Bl * N) ||
-            grow(h, h->d_act, h->act_cap, (size_t)kRowsHops * 2 * Bl * h->KA) ||
-            grow(h, h->d_state, h->state_cap, (size_t)h->rG * Bl * SW + Bl))
+        const size_t T_grp = (size_t)Lc_max * Bg * N, act_grp = (size_t)kRowsHops * 2 * Bg * h->KA;
+        const size_t state_grp = (size_t)h->rG * Bg * SW + Bg;
+        if (grow(h, h->d_X, h->X_cap, (size_t)Lc_max * Bg * h->KX) || grow(h, h->d_T, h->T_cap, ng * T_grp) ||
+            grow(h, h->d_act, h->act_cap, ng * act_grp) || grow(h, h->d_state, h->state_cap, ng * state_grp))
             return WRNN_EHIP;
-        HIP_TRY(h, hipMemsetAsync(h->d_flags, 0, (size_t)kRowsHops * kFlagSlots * kFlagStride * 4, st));
-        HIP_TRY(h, hipMemsetAsync(h->d_xr, 0, (size_t)kXReps * kXRepStride * 8, st));
+        HIP_TRY(h, hipMemsetAsync(h->d_flags, 0, ng * flag_words * 4, st));
+        HIP_TRY(h, hipMemsetAsync(h->d_xr, 0, ng * xr_words * 8, st));
         for (int t0 = 0; t0 < L; t0 += Lc_max) {
             const int Lc = std::min(Lc_max, L - t0);
-            // conditioning terms of steps [t0, t0 + Lc): cI, then one fp32 GEMM for every workgroup's terms
-            HIP_TRY(h, launch_ci_gemm(cond, h->CD, B, b0, Bl, t0, Lc, h->d_IW, 1 + c.feat_dims + A, h->d_Ib, R,
-                                      c.feat_dims + A, h->d_X, h->KX, st));
-            HIP_TRY(h, launch_pack_terms_input(cond, h->CD, B, b0, Bl, t0, Lc, c.feat_dims, A, R, h->KX, h->d_X, st));
-            if (rocblas_sgemm(h->blas, rocblas_operation_transpose, rocblas_operation_none, N, Lc * Bl, h->KX, &one,
-                              h->d_Wt, h->KX, h->d_X, h->KX, &zero, h->d_T, N) != rocblas_status_success)
-                return fail(h, WRNN_EHIP, "rocblas_sgemm (conditioning terms) failed");
+            // conditioning terms of steps [t0, t0 + Lc), per group: cI, then one fp32 GEMM for
+            // every workgroup's terms
+            for (int g = 0; g < ng; ++g) {
+                const int bg0 = b0 + (g ? Bg : 0), nb = group_rows(Bl, g);
+                HIP_TRY(h, launch_ci_gemm(cond, h->CD, B, bg0, nb, t0, Lc, h->d_IW, 1 + c.feat_dims + A, h->d_Ib, R,
+                                          c.feat_dims + A, h->d_X, h->KX, st));
+                HIP_TRY(h, launch_pack_terms_input(cond, h->CD, B, bg0, nb, t0, Lc, c.feat_dims, A, R, h->KX, h->d_X, st));
+                if (rocblas_sgemm(h->blas, rocblas_operation_transpose, rocblas_operation_none, N, Lc * nb, h->KX, &one,
+                                  h->d_Wt, h->KX, h->d_X, h->KX, &zero, h->d_T + g * T_grp, N) != rocblas_status_success)
+                    return fail(h, WRNN_EHIP, "rocblas_sgemm (conditioning terms) failed");
+            }
             RowsArgs a{};
             a.slab = h->d_rslab;
             a.terms = h->d_T;
@@ -731,7 +806,7 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
             a.L = L;
             a.t0 = t0;
             a.Lc = Lc;
-            a.B = Bl;
+            a.B = Bg;
             a.Bt = B;
             a.b0 = b0;
             a.R = R;
@@ -751,7 +826,19 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
             a.dbg = (b0 == 0 && t0 == 0) ? d_dbg : nullptr;
             a.dbg_steps = std::min(dbg_steps, Lc);
             a.head_lds = head_lds ? 1 : 0;
-            HIP_TRY(h, launch_rows(a, rows_lds_bytes(*h, Bl, TB, head_lds), st));
+            RowsGroup g1{};
+            if (grouped) {
+                g1.terms = h->d_T + T_grp;
+                g1.act = h->d_act + act_grp;
+                g1.flags = h->d_flags + flag_words;
+                g1.xg = h->d_xr + xr_words;
+                g1.state = h->d_state + state_grp;
+                g1.row0 = row_offset + b0 + Bg;
+                g1.B = group_rows(Bl, 1);
+                g1.b0 = b0 + Bg;
+                g1.dbg = nullptr;
+            }
+            HIP_TRY(h, launch_rows(a, grouped ? &g1 : nullptr, rows_lds_bytes(*h, Bg, TB, head_lds), st));
         }
         b0 += Bl;
     }
@@ -1061,6 +1148,12 @@ int wrnn_create(const wrnn_config *cfg, int device, wrnn_t **out) {
         HIP_TRY(h, rows_occupancy(&per_cu, rows_lds_bytes(*h, 1, 1)));
         if (per_cu * h->num_cus < h->rG) h->rows_ok = false;
     }
+    set_group_partition(*h);
+    if (h->g2.ok) {
+        PartScope ps(*h, h->g2, true);
+        HIP_TRY(h, rows_occupancy(&per_cu, rows_lds_bytes(*h, 1, 1)));
+        if (per_cu * h->num_cus < 2 * h->rG) h->rows_ok = false;
+    }
     // one MoL row: the role-split kernel (compile-time dims) when its grid and LDS fit; an
     // explicit grid request keeps the uniform kernels
     if (mol && c.grid <= 0 && split_has_kernel(R, F) && R % kSplitUnits == 0 && F % kSplitFcRows == 0) {
@@ -1152,6 +1245,21 @@ int wrnn_set_weights(wrnn_t *h, const wrnn_tensor *tensors, int n) {
         std::vector<float> Wt((size_t)h->rG * h->NT * h->KX);
         pack_terms_weights(*h, Wt.data());
         if (h->d_Wt) HIP_TRY(h, hipFree(h->d_Wt));
+        HIP_TRY(h, hipMalloc(&h->d_Wt, Wt.size() * 4));
+        HIP_TRY(h, hipMemcpy(h->d_Wt, Wt.data(), Wt.size() * 4, hipMemcpyHostToDevice));
+    }
+    if (h->g2.ok && !h->sparse) {
+        PartScope ps(*h, h->g2, true);
+        std::vector<float> rslab((size_t)h->rG * h->rs.total);
+        for (int w = 0; w < h->rG; ++w) pack_rows_slab(*h, w, rslab.data() + (size_t)w * h->rs.total);
+        if (h->d_rslab) HIP_TRY(h, hipFree(h->d_rslab));
+        h->d_rslab = nullptr;
+        HIP_TRY(h, hipMalloc(&h->d_rslab, rslab.size() * 4));
+        HIP_TRY(h, hipMemcpy(h->d_rslab, rslab.data(), rslab.size() * 4, hipMemcpyHostToDevice));
+        std::vector<float> Wt((size_t)h->rG * h->NT * h->KX);
+        pack_terms_weights(*h, Wt.data());
+        if (h->d_Wt) HIP_TRY(h, hipFree(h->d_Wt));
+        h->d_Wt = nullptr;
         HIP_TRY(h, hipMalloc(&h->d_Wt, Wt.size() * 4));
         HIP_TRY(h, hipMemcpy(h->d_Wt, Wt.data(), Wt.size() * 4, hipMemcpyHostToDevice));
     }
@@ -1279,7 +1387,7 @@ void wrnn_destroy(wrnn_t *h) {
                     (void *)h->d_ctl, (void *)h->d_rslab, (void *)h->d_Wt, (void *)h->d_X, (void *)h->d_T,
                     (void *)h->d_act, (void *)h->d_state, (void *)h->d_flags, (void *)h->d_xr, (void *)h->d_dmslab,
                     (void *)h->d_dmflags, (void *)h->d_dmxg, (void *)h->d_sgslab, (void *)h->d_sfslab,
-                    (void *)h->d_sWt})
+                    (void *)h->d_sWt, (void *)h->g2.d_slab, (void *)h->g2.d_Wt})
         if (p) (void)hipFree(p);
     if (h->blas) (void)rocblas_destroy_handle(h->blas);
     delete h;

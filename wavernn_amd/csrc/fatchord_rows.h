@@ -78,6 +78,18 @@ struct RowsArgs {
     int head_lds;                 // MoL: 1 = head in LDS, 0 = samplers read it from HBM (workgroup 0's slab)
 };
 
+// The per-group fields of a second row group sharing the launch (fatchord_rows.hip)
+struct RowsGroup {
+    const float *terms;
+    float *act;
+    unsigned *flags;
+    unsigned long long *xg;
+    float *state;
+    long long row0;
+    int B, b0;
+    unsigned *dbg;
+};
+
 struct RowsLds {
     int slab, tile, st, x, ring, lg, nz, flag, total;
     int SW, KT, NS, ncp, nkp;

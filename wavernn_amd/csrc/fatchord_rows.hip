@@ -38,11 +38,28 @@ constexpr int kTileCpol = WRNN_TILE_CPOL;
 // kRF = 512 instantiates the shipped dims (rnn_dims = fc_dims = 512) with compile-time dot
 // lengths; 0 = runtime dims.  SPARSE: block-sparse GRU weights (one 4-unit block-row per gate,
 // U = 4), the GRU matvecs run one engine per activation row over the nonzero blocks.
+//
+// Row groups: workgroups [0, G0) run argument set a0, [G0, 2·G0) set a1 — two independent
+// instances of the loop (own rows, buffers, flags) in one launch.  With B large the activation
+// broadcast (every workgroup DMAs every row of every stage) is what limits a stage; two groups of
+// G/2 workgroups, each holding twice the weight rows, halve the rows each workgroup streams.
 template <bool MOL, int kRF, bool SPARSE>
-__global__ __launch_bounds__(kRowsThreads) void fatchord_rows_kernel(RowsArgs a) {
+__global__ __launch_bounds__(kRowsThreads) void fatchord_rows_kernel(RowsArgs a, RowsGroup g1, int G0) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, row = lane >> 4;
-    const int w = blockIdx.x;
+    const bool grp1 = (int)blockIdx.x >= G0;
+    if (grp1) {   // field by field (uniform selects; a dynamically chosen struct would go to scratch)
+        a.terms = g1.terms;
+        a.act = g1.act;
+        a.flags = g1.flags;
+        a.xg = g1.xg;
+        a.state = g1.state;
+        a.row0 = g1.row0;
+        a.B = g1.B;
+        a.b0 = g1.b0;
+        a.dbg = g1.dbg;
+    }
+    const int w = (int)blockIdx.x - (grp1 ? G0 : 0);
     const int R = kRF ? kRF : a.R, F = kRF ? kRF : a.F, NC = a.NC, NK = a.NK, U = a.U, UF = a.UF, UC = a.UC, G = a.G, B = a.B;
     const int NT = a.NT, TB = a.TB, KA = a.KA;
     const int slab_lds = (MOL && !a.head_lds) ? a.s.body : a.s.total;   // floats resident in LDS
@@ -519,10 +536,13 @@ static const void *pick_rows_kernel(const RowsArgs &a) {
     return d512 ? (const void *)fatchord_rows_kernel<false, 512, false> : (const void *)fatchord_rows_kernel<false, 0, false>;
 }
 
-hipError_t launch_rows(const RowsArgs &a, size_t lds_bytes, hipStream_t st) {
+// one row group (g1 == nullptr) or two (workgroups [G, 2G) run group 1) in one launch
+hipError_t launch_rows(const RowsArgs &a, const RowsGroup *g1, size_t lds_bytes, hipStream_t st) {
     RowsArgs args = a;
-    void *params[] = {&args};
-    return hipLaunchKernel(pick_rows_kernel(a), dim3(a.G), dim3(kRowsThreads), params, lds_bytes, st);
+    RowsGroup grp = g1 ? *g1 : RowsGroup{};
+    int G0 = a.G;
+    void *params[] = {&args, &grp, &G0};
+    return hipLaunchKernel(pick_rows_kernel(a), dim3(g1 ? 2 * a.G : a.G), dim3(kRowsThreads), params, lds_bytes, st);
 }
 
 hipError_t prepare_rows_kernel(int max_lds_bytes) {
