@@ -913,7 +913,8 @@ int generate_split(wrnn_t *h, const float *cond, int B, int L, const float *nois
     const int Lc_max = (int)std::max(1.0, std::min((double)L, budget / (double)(N + h->KX) - 1.0));
     const char *rep_env = std::getenv("WRNN_REPLICAS");
     const int reps = std::max(1, std::min(32, rep_env ? std::atoi(rep_env) : 8));
-    const long long vec_max = std::max<long long>({(long long)kTermsPerUnit * R, (long long)R, (long long)c.fc_dims});
+    const long long vec_max = std::max<long long>({(long long)kTermsPerUnit * R, (long long)R, (long long)c.fc_dims,
+                                                   (long long)(R / kSplitUnits) * kYLine});
     const long long rep_stride = (((vec_max + kOverRead) * 8 + 65535) / 65536) * 65536 / 8;
     const size_t need_xg = (size_t)kSplitHops * reps * rep_stride;
     HIP_TRY(h, ensure(h->d_xg, h->xg_cap, need_xg));

@@ -12,6 +12,7 @@ constexpr int kSplitFcRows = 16;     // fc1 and fc2 rows per FC workgroup (one p
 constexpr int kSplitTerms = 32;      // conditioning terms per workgroup per step (terms-GEMM columns)
 constexpr int kSplitRing = 4;        // steps of terms / sampler noise held in LDS
 constexpr int kSplitNoise = 12;      // 11 MoL sampler terms, padded
+constexpr int kYLine = 16;           // granules (one 128-B line) per GRU workgroup in the y vector
 
 // Hand-off vectors (granules {tag = step + 1, value}).  H2 and the GRU1 terms are double-
 // buffered by step parity; Y, F1, F2 are not (the step's dependency chain orders their reuse).

@@ -8,12 +8,12 @@
 //     GRU workgroup (local gate math on gathered terms, as in fatchord_loop.hip), GRU2 for the
 //     own units; each publishes y_j = x_I,j + h1_j + h2_j (fc1's input, :212-216) and h2_j.
 //   FC workgroups (Gf = F/16): 16 rows of fc1 and of fc2, one per 16-lane engine.
-//   Every workgroup gathers f2 and runs fc3 + the MoL sampler redundantly (bit-identical), so
-//     the sample needs no hand-off of its own.
+//   Every GRU workgroup gathers f2 and runs fc3 + the MoL sampler redundantly (bit-identical),
+//     so the sample needs no hand-off of its own; the FC workgroups need no x.
 //
 // Critical path per step:
 //   x_{t-1} → GRU1 (all units) → W_ih2[:, :R]·h1 → GRU2 gates → [hop Y: Gg → Gf]
-//   → W1[:, :R]·y → [hop F1: Gf → Gf] → W2[:, :F]·f1 → [hop F2: Gf → all] → fc3 → sample → x_t
+//   → W1[:, :R]·y → [hop F1: Gf → Gf] → W2[:, :F]·f1 → [hop F2: Gf → Gg] → fc3 → sample → x_t
 // Off the critical path, while fc1/fc2 run in the FC workgroups, the GRU workgroups compute
 // GH1 = W_hh1·h1_t → publish step t+1's GRU1 terms, gather h2_t → GH2 = W_hh2·h2_t, and
 // gather step t+1's terms of all units.  Everything that depends only on the conditioning
@@ -30,6 +30,15 @@
 #include "wrnn_device.h"
 
 namespace wrnn {
+
+#ifndef WRNN_OFF_SLEEP
+#define WRNN_OFF_SLEEP 2
+#endif
+constexpr int kOffSleep = WRNN_OFF_SLEEP;   // backoff (×64 cycles) of the off-critical polls
+#ifndef WRNN_DRAIN_PUB
+#define WRNN_DRAIN_PUB 1
+#endif
+constexpr bool kDrainPub = WRNN_DRAIN_PUB;
 
 #define SSTAMP(k)                                                                                          \
     do {                                                                                                   \
@@ -95,10 +104,11 @@ __global__ __launch_bounds__(kThreads) void fatchord_split_kernel(SplitArgs a) {
                     (uint32_t)t + 1u, v);
         }
     };
-    auto gather_terms = [&](int t) {
-        gather_chunked<NG_R, kPollThreads>(XG(SH_S0 + (t & 1)) + poll_off, RT, RT, (uint32_t)t + 1u, a.ctl,
-                                           a.timeout_ticks, t, SH_S0 + (t & 1), abort_flag, lane,
-                                           [&](int, int j, float v) { sg[j] = v; });
+    auto store_sg = [&](int, int j, float v) { sg[j] = v; };
+    auto gather_terms = [&](int t) {   // off the critical path: polls back off (kOffSleep)
+        gather_chunked<NG_R, kPollThreads, decltype(store_sg), kOffSleep>(
+            XG(SH_S0 + (t & 1)) + poll_off, RT, RT, (uint32_t)t + 1u, a.ctl, a.timeout_ticks, t, SH_S0 + (t & 1),
+            abort_flag, lane, store_sg);
     };
 
     // ---- prologue: slab → LDS, state (zero, or carried from the previous time chunk), the
@@ -184,7 +194,9 @@ __global__ __launch_bounds__(kThreads) void fatchord_split_kernel(SplitArgs a) {
                 const float hn = gru_gate_math(gi[0], gi[1], gi[2], gh[0], gh[1], gh[2], h2own[u]);
                 // y = (x_I + h1) + h2 (:212, :216), x_I = cI + W_I[:, 0]·x
                 const float y = (fmaf(S[a.gs.wi0 + u], x, tr[ST_CI + u]) + va[j]) + hn;
-                if (lane < a.reps) publish(XG(SH_Y) + (size_t)lane * a.rep_stride + j, tag, y);
+                // y: one 128-B line per GRU workgroup (kYLine granules), so no two workgroups'
+                // sc1 stores share a line (4 producers per line cost the hop ~0.5 us)
+                if (lane < a.reps) publish(XG(SH_Y) + (size_t)lane * a.rep_stride + g * kYLine + u, tag, y);
                 else if (lane < 2 * a.reps)
                     publish(XG(SH_H2A + (t & 1)) + (size_t)(lane - a.reps) * a.rep_stride + j, tag, hn);
                 if (lane == 0) h2own[u] = hn;
@@ -192,7 +204,9 @@ __global__ __launch_bounds__(kThreads) void fatchord_split_kernel(SplitArgs a) {
             }
 
             // ---- C: while fc1/fc2 run elsewhere: f2 (wave 0), step t+1's GRU1 terms (wave 1
-            // publishes, wave 3 gathers), h2 → GH2 (wave 2)
+            // publishes, wave 3 gathers), h2 → GH2 (wave 2).  The polling waves first let their y/h2
+            // stores leave the CU (vmcnt(0)): polls queued behind them slow the critical y hop
+            if (kDrainPub && wave != 1 && !loader) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (wave == 0) {
                 gather<NG_F, kPollThreads>(XG(SH_F2) + poll_off, 0, F, F, tag, a.ctl, a.timeout_ticks, t, SH_F2,
                                            abort_flag, lane, [&](int, int k, float v) { f2[k] = v; });
@@ -209,9 +223,10 @@ __global__ __launch_bounds__(kThreads) void fatchord_split_kernel(SplitArgs a) {
                 }
             } else if (wave == 2) {
                 if (more) {
-                    gather<NG_R, kPollThreads>(XG(SH_H2A + (t & 1)) + poll_off, 0, R, R, tag, a.ctl, a.timeout_ticks,
-                                               t, SH_H2A + (t & 1), abort_flag, lane,
-                                               [&](int, int k, float v) { vb[k] = v; });
+                    auto store_h2 = [&](int, int k, float v) { vb[k] = v; };
+                    gather<NG_R, kPollThreads, decltype(store_h2), kOffSleep>(
+                        XG(SH_H2A + (t & 1)) + poll_off, 0, R, R, tag, a.ctl, a.timeout_ticks, t, SH_H2A + (t & 1),
+                        abort_flag, lane, store_h2);
                     const float3 v = row_dot3(S + a.gs.whh2 + (row * 3 + 0) * R, S + a.gs.whh2 + (row * 3 + 1) * R,
                                               S + a.gs.whh2 + (row * 3 + 2) * R, vb, R / 4, li);
                     float *o = gh2 + ((t + 1) & 1) * 12 + row * 3;
@@ -230,10 +245,13 @@ __global__ __launch_bounds__(kThreads) void fatchord_split_kernel(SplitArgs a) {
             SSTAMP(3);
             if (*abort_flag) return;
         } else {
-            // ---- A': y (hop Y)
+            // ---- A': y (hop Y); the gathering wave first lets its f2 stores leave the CU
+            if (kDrainPub && wave == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (wave == 0)
-                gather<NG_R, kPollThreads>(XG(SH_Y) + poll_off, 0, R, R, tag, a.ctl, a.timeout_ticks, t, SH_Y,
-                                           abort_flag, lane, [&](int, int k, float v) { va[k] = v; });
+                gather_mapped<NG_R, kPollThreads>(XG(SH_Y) + poll_off, R, tag, a.ctl, a.timeout_ticks, t, SH_Y,
+                                                  abort_flag, lane,
+                                                  [](int i) { return (i / kSplitUnits) * kYLine + i % kSplitUnits; },
+                                                  [&](int k, float v) { va[k] = v; });
             bar();
             SSTAMP(1);
             if (*abort_flag) return;
@@ -246,6 +264,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_split_kernel(SplitArgs a) {
                     publish(XG(SH_F1) + (size_t)li * a.rep_stride + g * kSplitFcRows + e, tag, v > 0.0f ? v : 0.0f);
                 if (dbg_on && tid == 0) stamp[(t & 1) * kStamps + 6] = (unsigned)__builtin_amdgcn_s_memrealtime();
             }
+            if (kDrainPub && wave == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // f1 stores out first
             if (wave == 0)
                 gather<NG_F, kPollThreads>(XG(SH_F1) + poll_off, 0, F, F, tag, a.ctl, a.timeout_ticks, t, SH_F1,
                                            abort_flag, lane, [&](int, int k, float v) { vb[k] = v; });
@@ -259,13 +278,12 @@ __global__ __launch_bounds__(kThreads) void fatchord_split_kernel(SplitArgs a) {
                     publish(XG(SH_F2) + (size_t)li * a.rep_stride + g * kSplitFcRows + e, tag, v > 0.0f ? v : 0.0f);
                 if (dbg_on && tid == 0) stamp[(t & 1) * kStamps + 7] = (unsigned)__builtin_amdgcn_s_memrealtime();
             }
-            if (wave == 0)
-                gather<NG_F, kPollThreads>(XG(SH_F2) + poll_off, 0, F, F, tag, a.ctl, a.timeout_ticks, t, SH_F2,
-                                           abort_flag, lane, [&](int, int k, float v) { f2[k] = v; });
+            // the FC workgroups need neither f2 nor x: they go straight to the next step's y
             if (loader) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             bar();
             SSTAMP(3);
             if (*abort_flag) return;
+            continue;
         }
 
         // ---- D: fc3 (:223), 30 rows over the 16 engines: rows e and e + 16

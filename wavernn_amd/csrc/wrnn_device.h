@@ -146,7 +146,9 @@ __device__ __noinline__ void record_abort(int *ctl, int code, int step, int hop,
 // with a runtime condition makes hipcc branch around it and wait vmcnt(0) per load, i.e. NG
 // serialized memory round trips per pass (measured: 2-4x slower hops).
 // On timeout, or when another workgroup has aborted, sets *lds_abort.
-template <int NG, int NL, typename Store>
+// kSleep > 0 backs off 64·kSleep cycles between unsuccessful polls: for off-critical vectors,
+// whose polling traffic would otherwise compete with a critical hand-off in flight.
+template <int NG, int NL, typename Store, int kSleep = 0>
 __device__ __forceinline__ void gather(const unsigned long long *g, int base, int n, int N, uint32_t tag, int *ctl,
                                        long long timeout, int step, int hop, int *lds_abort, int lid, Store store,
                                        unsigned *dbg_slot = nullptr) {
@@ -173,6 +175,7 @@ __device__ __forceinline__ void gather(const unsigned long long *g, int base, in
             }
             break;
         }
+        if (kSleep) __builtin_amdgcn_s_sleep(kSleep);
         if ((++spins & 63u) == 0) {
             const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - t0) > timeout;
             const bool other = __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
@@ -186,13 +189,50 @@ __device__ __forceinline__ void gather(const unsigned long long *g, int base, in
     if (dbg_slot && lid == 0) dbg_slot[0] = spins + 1;
 }
 
+// gather() over a strided layout: value i sits at granule map(i) (e.g. one 128-B line per
+// producer workgroup, so that no two producers' sc1 stores share a line)
+template <int NG, int NL, typename Map, typename Store>
+__device__ __forceinline__ void gather_mapped(const unsigned long long *g, int n, uint32_t tag, int *ctl, long long timeout,
+                                              int step, int hop, int *lds_abort, int lid, Map map, Store store) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned spins = 0;
+    for (;;) {
+        unsigned long long v[NG];
+#pragma unroll
+        for (int k = 0; k < NG; ++k) {
+            const int i = lid + k * NL;
+            v[k] = __hip_atomic_load(g + map(i < n ? i : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        bool ok = true;
+#pragma unroll
+        for (int k = 0; k < NG; ++k) ok &= (lid + k * NL >= n) | ((uint32_t)(v[k] >> 32) == tag);
+        if (ok) {
+#pragma unroll
+            for (int k = 0; k < NG; ++k) {
+                const int i = lid + k * NL;
+                if (i < n) store(i, __uint_as_float((uint32_t)v[k]));
+            }
+            break;
+        }
+        if ((++spins & 63u) == 0) {
+            const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - t0) > timeout;
+            const bool other = __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+            if (late || other) {
+                if (late) record_abort(ctl, -4, step, hop, blockIdx.x);
+                *lds_abort = 1;
+                break;
+            }
+        }
+    }
+}
+
 // A long, off-critical-path vector gathered in chunks of NG·NL granules (bounded registers).
-template <int NG, int NL, typename Store>
+template <int NG, int NL, typename Store, int kSleep = 0>
 __device__ __forceinline__ void gather_chunked(const unsigned long long *g, int n, int N, uint32_t tag, int *ctl,
                                                long long timeout, int step, int hop, int *lds_abort, int lid,
                                                Store store) {
     for (int c0 = 0; c0 < n; c0 += NG * NL) {
-        gather<NG, NL>(g, c0, n, N, tag, ctl, timeout, step, hop, lds_abort, lid, store);
+        gather<NG, NL, Store, kSleep>(g, c0, n, N, tag, ctl, timeout, step, hop, lds_abort, lid, store);
         if (*reinterpret_cast<volatile int *>(lds_abort)) return;
     }
 }
