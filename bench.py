@@ -29,7 +29,7 @@ sys.path.insert(0, REPO)
 from wavernn_amd import synthetic as syn  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
-PMC_PROFILE = os.environ.get("WRNN_PMC_PROFILE", os.path.join(REPO, "profiles", "r01_v7_pmc_traffic.json"))
+PMC_PROFILE = os.environ.get("WRNN_PMC_PROFILE", os.path.join(REPO, "profiles", "r01_v8_pmc_traffic.json"))
 
 
 def pmc_traffic_bytes(mode: str, batched: bool, seconds: float):
