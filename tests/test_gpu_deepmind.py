@@ -68,3 +68,18 @@ def test_dm_philox_row_keyed():
     assert torch.equal(r2[0], a[2])
     u = a.cpu().numpy() + 2 ** 15
     assert (u >= 0).all() and (u < 2 ** 16).all() and len(np.unique(u // 256)) > 100
+
+
+def test_dm_row_groups_agree(monkeypatch):
+    """One group of G workgroups vs two groups of G/2 (twice the units each): the coarse/fine
+    labels are bit-exact across partitions (Philox keyed by global row)."""
+    from wavernn_amd.loop import DeepmindLoop
+    d = syn.DEFAULT_DM
+    res = {}
+    for g in ("1", "2"):
+        monkeypatch.setenv("WRNN_ROW_GROUPS", g)
+        loop = DeepmindLoop(d.hidden_size, d.quantisation)
+        loop.set_weights(syn.make_deepmind_state(d, 17))
+        res[g] = loop.generate(9, 300, seed=5)[1]
+        loop.close()
+    assert torch.equal(res["1"], res["2"])

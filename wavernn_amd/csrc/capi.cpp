@@ -28,7 +28,7 @@ hipError_t launch_pack_terms_input(const float *cond, int CD, int Bt, int b0, in
 hipError_t launch_rows(const RowsArgs &a, const RowsGroup *g1, size_t lds_bytes, hipStream_t st);
 hipError_t prepare_rows_kernel(int max_lds_bytes);
 hipError_t rows_occupancy(int *blocks_per_cu, size_t lds_bytes);
-hipError_t launch_dm(const DmArgs &a, size_t lds_bytes, hipStream_t st);
+hipError_t launch_dm(const DmArgs &a, const DmGroup *g1, size_t lds_bytes, hipStream_t st);
 hipError_t prepare_dm_kernel(int max_lds_bytes);
 hipError_t dm_occupancy(int *blocks_per_cu, size_t lds_bytes);
 hipError_t launch_loop(const LoopArgs &a, size_t lds_bytes, hipStream_t st);
@@ -49,6 +49,14 @@ struct RowsPart {
     int rU = 0, rG = 0, rUF = 0, rUC = 0, NT = 0;
     bool ok = false;
     float *d_slab = nullptr, *d_Wt = nullptr;
+};
+
+// The deepmind partition (units per workgroup, grid) and its packed slab (see wrnn_ctx::dm2)
+struct DmPart {
+    DmSlab ds{};
+    int dmU = 0, dmUO = 0, dmUO2 = 0, G = 0;
+    bool ok = false;
+    float *d_slab = nullptr;
 };
 
 struct wrnn_ctx {
@@ -93,6 +101,7 @@ struct wrnn_ctx {
     int dmU = 0, dmUO = 0, dmUO2 = 0;
     bool dm = false;
     float *d_dmslab = nullptr;
+    DmPart dm2{};                                   // G/2 workgroups, twice the units: two row groups per launch
     unsigned *d_dmflags = nullptr;
     unsigned long long *d_dmxg = nullptr;
     size_t dmflags_cap = 0, dmxg_cap = 0;
@@ -558,6 +567,27 @@ int dm_tile_for(const wrnn_ctx &h, int B) {
     return 0;
 }
 
+void swap_dm(wrnn_ctx &h, DmPart &p) {
+    std::swap(h.ds, p.ds);
+    std::swap(h.dmU, p.dmU);
+    std::swap(h.dmUO, p.dmUO);
+    std::swap(h.dmUO2, p.dmUO2);
+    std::swap(h.G, p.G);
+    std::swap(h.d_dmslab, p.d_slab);
+}
+
+struct DmScope {
+    wrnn_ctx &h;
+    DmPart &p;
+    bool on;
+    DmScope(wrnn_ctx &h_, DmPart &p_, bool on_) : h(h_), p(p_), on(on_) {
+        if (on) swap_dm(h, p);
+    }
+    ~DmScope() {
+        if (on) swap_dm(h, p);
+    }
+};
+
 size_t lds_bytes_for(const wrnn_ctx &h, int Bc) {
     return (size_t)lds_layout(h.s.total, Bc, h.cfg.rnn_dims, h.cfg.fc_dims, h.cfg.aux_dims, h.cfg.n_classes, h.NK,
                               h.U, h.UF)
@@ -849,20 +879,28 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
 // deepmind_version: B rows (utterances) in row groups of <= kRowsMax, one launch each
 int generate_dm(wrnn_t *h, int B, int L, const float *noise, uint64_t seed, int64_t row_offset, float *out,
                 int32_t *labels, hipStream_t st) {
+    // two row groups per launch (G/2 workgroups each) unless WRNN_ROW_GROUPS=1 or one row
+    const char *grp_env = std::getenv("WRNN_ROW_GROUPS");
+    const bool grouped = h->dm2.ok && B >= 2 && !(grp_env && std::atoi(grp_env) == 1);
+    DmScope sc(*h, h->dm2, grouped);
+    const int ng = grouped ? 2 : 1;
     const int S = h->cfg.rnn_dims / 2, Q = h->cfg.n_classes;
+    const size_t flag_words = (size_t)kDmHops * kFlagSlots * kFlagStride, xg_words = (size_t)2 * kXReps * kXRepStride;
     for (int b0 = 0; b0 < B;) {
         int Bl = std::min(B - b0, kRowsMax);
-        while (Bl > 1 && dm_tile_for(*h, Bl) == 0) --Bl;
-        const int TB = dm_tile_for(*h, Bl);
+        auto group_rows = [&](int bl, int g) { const int b_0 = (bl + ng - 1) / ng; return g == 0 ? b_0 : bl - b_0; };
+        while (Bl > 1 && dm_tile_for(*h, group_rows(Bl, 0)) == 0) --Bl;
+        const int Bg = group_rows(Bl, 0);
+        const int TB = dm_tile_for(*h, Bg);
         if (TB == 0) return fail(h, WRNN_EUNSUPPORTED, "DM: one row of state does not fit LDS");
         const int SW = dm_state_width(h->dmU);
-        if (grow(h, h->d_act, h->act_cap, (size_t)kDmHops * 2 * Bl * h->KA) ||
-            grow(h, h->d_state, h->state_cap, (size_t)h->G * Bl * SW + 2 * Bl))
+        const size_t act_grp = (size_t)kDmHops * 2 * Bg * h->KA, state_grp = (size_t)h->G * Bg * SW + 2 * Bg;
+        if (grow(h, h->d_act, h->act_cap, ng * act_grp) || grow(h, h->d_state, h->state_cap, ng * state_grp))
             return WRNN_EHIP;
-        HIP_TRY(h, ensure(h->d_dmflags, h->dmflags_cap, (size_t)kDmHops * kFlagSlots * kFlagStride));
-        HIP_TRY(h, ensure(h->d_dmxg, h->dmxg_cap, (size_t)2 * kXReps * kXRepStride));
-        HIP_TRY(h, hipMemsetAsync(h->d_dmflags, 0, (size_t)kDmHops * kFlagSlots * kFlagStride * 4, st));
-        HIP_TRY(h, hipMemsetAsync(h->d_dmxg, 0, (size_t)2 * kXReps * kXRepStride * 8, st));
+        HIP_TRY(h, ensure(h->d_dmflags, h->dmflags_cap, 2 * flag_words));
+        HIP_TRY(h, ensure(h->d_dmxg, h->dmxg_cap, 2 * xg_words));
+        HIP_TRY(h, hipMemsetAsync(h->d_dmflags, 0, ng * flag_words * 4, st));
+        HIP_TRY(h, hipMemsetAsync(h->d_dmxg, 0, ng * xg_words * 8, st));
         DmArgs a{};
         a.slab = h->d_dmslab;
         a.noise = noise;
@@ -879,7 +917,7 @@ int generate_dm(wrnn_t *h, int B, int L, const float *noise, uint64_t seed, int6
         a.L = L;
         a.t0 = 0;
         a.Lc = L;
-        a.B = Bl;
+        a.B = Bg;
         a.Bt = B;
         a.b0 = b0;
         a.H = 2 * S;
@@ -892,7 +930,17 @@ int generate_dm(wrnn_t *h, int B, int L, const float *noise, uint64_t seed, int6
         a.TB = TB;
         a.KA = h->KA;
         a.s = h->ds;
-        HIP_TRY(h, launch_dm(a, dm_lds_bytes(*h, Bl, TB), st));
+        DmGroup g1{};
+        if (grouped) {
+            g1.act = h->d_act + act_grp;
+            g1.flags = h->d_dmflags + flag_words;
+            g1.xg = h->d_dmxg + xg_words;
+            g1.state = h->d_state + state_grp;
+            g1.row0 = row_offset + b0 + Bg;
+            g1.B = group_rows(Bl, 1);
+            g1.b0 = b0 + Bg;
+        }
+        HIP_TRY(h, launch_dm(a, grouped ? &g1 : nullptr, dm_lds_bytes(*h, Bg, TB), st));
         b0 += Bl;
     }
     return WRNN_OK;
@@ -1099,6 +1147,26 @@ int wrnn_create(const wrnn_config *cfg, int device, wrnn_t **out) {
         HIP_TRY(h, dm_occupancy(&per_cu, dm_lds_bytes(*h, 1, 1)));
         if (per_cu * h->num_cus < h->G)
             return fail(h, WRNN_EUNSUPPORTED, "DM persistent grid is not co-resident");
+        // two row groups of G/2 workgroups (twice the units each), as the fatchord rows kernel
+        if (h->G % 2 == 0 && h->G >= 8) {
+            DmPart p{};
+            p.G = h->G / 2;
+            p.dmU = (S + p.G - 1) / p.G;
+            p.G = (S + p.dmU - 1) / p.dmU;
+            p.dmUO = (S + p.G - 1) / p.G;
+            p.dmUO2 = (Q + p.G - 1) / p.G;
+            h->dm2 = p;
+            bool ok = false;
+            {
+                DmScope sc(*h, h->dm2, true);
+                h->ds = make_dm_slab(*h);
+                if (dm_tile_for(*h, 2) > 0) {
+                    HIP_TRY(h, dm_occupancy(&per_cu, dm_lds_bytes(*h, 1, 1)));
+                    ok = per_cu * h->num_cus >= 2 * h->G;
+                }
+            }
+            h->dm2.ok = ok;
+        }
         h->timeout_ticks = (long long)(c.timeout_ms > 0 ? c.timeout_ms : 2000) * 100000LL;
         HIP_TRY(h, hipMalloc(&h->d_ctl, kCtlWords * sizeof(int)));
         HIP_TRY(h, hipMemset(h->d_ctl, 0, kCtlWords * sizeof(int)));
@@ -1197,11 +1265,15 @@ int wrnn_set_weights(wrnn_t *h, const wrnn_tensor *tensors, int n) {
     for (const auto &q : need)
         if (!h->w.count(q.name)) { h->ready = false; return WRNN_OK; }   // partial load so far
     if (h->dm) {
-        std::vector<float> slab((size_t)h->G * h->ds.total);
-        for (int w = 0; w < h->G; ++w) pack_dm_slab(*h, w, slab.data() + (size_t)w * h->ds.total);
-        if (h->d_dmslab) HIP_TRY(h, hipFree(h->d_dmslab));
-        HIP_TRY(h, hipMalloc(&h->d_dmslab, slab.size() * 4));
-        HIP_TRY(h, hipMemcpy(h->d_dmslab, slab.data(), slab.size() * 4, hipMemcpyHostToDevice));
+        for (int grouped = 0; grouped < (h->dm2.ok ? 2 : 1); ++grouped) {
+            DmScope sc(*h, h->dm2, grouped == 1);
+            std::vector<float> slab((size_t)h->G * h->ds.total);
+            for (int w = 0; w < h->G; ++w) pack_dm_slab(*h, w, slab.data() + (size_t)w * h->ds.total);
+            if (h->d_dmslab) HIP_TRY(h, hipFree(h->d_dmslab));
+            h->d_dmslab = nullptr;
+            HIP_TRY(h, hipMalloc(&h->d_dmslab, slab.size() * 4));
+            HIP_TRY(h, hipMemcpy(h->d_dmslab, slab.data(), slab.size() * 4, hipMemcpyHostToDevice));
+        }
         h->ready = true;
         return WRNN_OK;
     }
@@ -1388,7 +1460,7 @@ void wrnn_destroy(wrnn_t *h) {
                     (void *)h->d_ctl, (void *)h->d_rslab, (void *)h->d_Wt, (void *)h->d_X, (void *)h->d_T,
                     (void *)h->d_act, (void *)h->d_state, (void *)h->d_flags, (void *)h->d_xr, (void *)h->d_dmslab,
                     (void *)h->d_dmflags, (void *)h->d_dmxg, (void *)h->d_sgslab, (void *)h->d_sfslab,
-                    (void *)h->d_sWt, (void *)h->g2.d_slab, (void *)h->g2.d_Wt})
+                    (void *)h->d_sWt, (void *)h->g2.d_slab, (void *)h->g2.d_Wt, (void *)h->dm2.d_slab})
         if (p) (void)hipFree(p);
     if (h->blas) (void)rocblas_destroy_handle(h->blas);
     delete h;

@@ -41,6 +41,16 @@ struct DmArgs {
     DmSlab s;
 };
 
+// The per-group fields of a second row group sharing the launch (as RowsGroup, fatchord_rows.h)
+struct DmGroup {
+    float *act;
+    unsigned *flags;
+    unsigned long long *xg;
+    float *state;
+    long long row0;
+    int B, b0;
+};
+
 // Per-row state of a workgroup's own units: hc U | hf U | Rh[2 parities][2 halves of h][6][U]
 __host__ __device__ inline int dm_state_width(int U) { return round4(2 * U + 24 * U); }
 

@@ -25,11 +25,23 @@
 namespace wrnn {
 
 // kS = 448 instantiates the shipped dims (hidden 896) with compile-time dot lengths.
+// Row groups as in fatchord_rows.hip: workgroups [G0, 2·G0) run a second, independent instance
+// over the rows of g1 (half the flags per hop, half the rows streamed per stage).
 template <int kS>
-__global__ __launch_bounds__(kThreads) void deepmind_rows_kernel(DmArgs a) {
+__global__ __launch_bounds__(kThreads) void deepmind_rows_kernel(DmArgs a, DmGroup g1, int G0) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, row = lane >> 4;
-    const int w = blockIdx.x;
+    const bool grp1 = (int)blockIdx.x >= G0;
+    if (grp1) {
+        a.act = g1.act;
+        a.flags = g1.flags;
+        a.xg = g1.xg;
+        a.state = g1.state;
+        a.row0 = g1.row0;
+        a.B = g1.B;
+        a.b0 = g1.b0;
+    }
+    const int w = (int)blockIdx.x - (grp1 ? G0 : 0);
     const int S = kS ? kS : a.S, H = 2 * S, Q = a.Q, U = a.U, UO = a.UO, UO2 = a.UO2, G = a.G, B = a.B;
     const int TB = a.TB, KA = a.KA;
     const DmLds ll = dm_lds_layout(a.s.total, B, TB, S, Q, U, G);
@@ -290,10 +302,12 @@ static const void *pick_dm_kernel(const DmArgs &a) {
     return a.S == 448 ? (const void *)deepmind_rows_kernel<448> : (const void *)deepmind_rows_kernel<0>;
 }
 
-hipError_t launch_dm(const DmArgs &a, size_t lds_bytes, hipStream_t st) {
+hipError_t launch_dm(const DmArgs &a, const DmGroup *g1, size_t lds_bytes, hipStream_t st) {
     DmArgs args = a;
-    void *params[] = {&args};
-    return hipLaunchKernel(pick_dm_kernel(a), dim3(a.G), dim3(kThreads), params, lds_bytes, st);
+    DmGroup grp = g1 ? *g1 : DmGroup{};
+    int G0 = a.G;
+    void *params[] = {&args, &grp, &G0};
+    return hipLaunchKernel(pick_dm_kernel(a), dim3(g1 ? 2 * a.G : a.G), dim3(kThreads), params, lds_bytes, st);
 }
 
 hipError_t prepare_dm_kernel(int max_lds_bytes) {
