@@ -47,6 +47,7 @@ def main(mode="MOL", B=10, L=2000):
 
 
 if __name__ == "__main__":
-    main("MOL", 10, 2000)
-    main("MOL", 115, 300)
-    main("RAW", 10, 1000)
+    # python tools/stamps_rows.py [MODE B L]...   (default: MOL 115 400, MOL 32 1000, MOL 10 1000)
+    args = sys.argv[1:] or ["MOL", "115", "400", "MOL", "32", "1000", "MOL", "10", "1000"]
+    for i in range(0, len(args), 3):
+        main(args[i], int(args[i + 1]), int(args[i + 2]))
