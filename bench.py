@@ -29,6 +29,8 @@ sys.path.insert(0, REPO)
 from wavernn_amd import synthetic as syn  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
+FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak (dense)
+MOL_MACS_PER_ROW_STEP = 3825152   # loop MACs per row-step, MoL rnn 512
 PMC_PROFILE = os.environ.get("WRNN_PMC_PROFILE", os.path.join(REPO, "profiles", "r01_v8_pmc_traffic.json"))
 
 
@@ -71,9 +73,16 @@ def other_configs(dev) -> dict:
     torch.cuda.synchronize()
     dt = time.perf_counter() - t
     ms = model.loop_handle().elapsed_ms()
+    flops = 2.0 * MOL_MACS_PER_ROW_STEP * 115 * 12100
     res["config3_mol_fold_60s"] = {"samples_per_s": out.shape[0] / dt, "rtf": out.shape[0] / dt / d.sample_rate,
                                    "rows": 115, "loop_steps": 12100, "device_ms": ms, "wall_s": dt,
-                                   "us_per_loop_step": ms * 1e3 / 12100}
+                                   "us_per_loop_step": ms * 1e3 / 12100,
+                                   "roofline": {"bound": "fp32 (vector/mfma)", "achieved": flops / (ms / 1e3) / 1e12,
+                                                "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                                "frac": flops / (ms / 1e3) / 1e12 / FP32_PEAK_TFLOPS,
+                                                "note": "algorithmic FLOP = 2 x 3 825 152 MAC x 115 rows per step "
+                                                        "(SURVEY.md 8(d): AI 57 F/B > ridge); device time of the loop "
+                                                        "launches incl. the terms GEMMs between time chunks"}}
     del model
     # config 4
     d4 = syn.SPARSE896_MOL
