@@ -10,6 +10,10 @@ namespace wrnn {
 // x hand-offs of the sampled labels (tagged granules).
 enum DmHop { DH_HC = 0, DH_O1 = 1, DH_LC = 2, DH_HF = 3, DH_O3 = 4, DH_LF = 5, kDmHops = 6 };
 
+// 8 waves: 0-3 compute (16 dot engines), 4-7 split each tile's LDS-DMA; wave 4 also polls flags
+constexpr int kDmLoaders = 4;
+constexpr int kDmThreads = kCompute + 64 * kDmLoaders;
+
 // Per-workgroup resident weights (floats).  Workgroup w owns coarse units j = w·U + u and the
 // fine units S + j (u < U) — their u/r/e rows of R (3H × H, no bias, deepmind_version.py:16),
 // split in the generate() order [cu | fu | cr | fr | ce | fe] (:116-119) — plus UO rows of each

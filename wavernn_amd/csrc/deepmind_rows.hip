@@ -28,7 +28,7 @@ namespace wrnn {
 // Row groups as in fatchord_rows.hip: workgroups [G0, 2·G0) run a second, independent instance
 // over the rows of g1 (half the flags per hop, half the rows streamed per stage).
 template <int kS>
-__global__ __launch_bounds__(kThreads) void deepmind_rows_kernel(DmArgs a, DmGroup g1, int G0) {
+__global__ __launch_bounds__(kDmThreads) void deepmind_rows_kernel(DmArgs a, DmGroup g1, int G0) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, row = lane >> 4;
     const bool grp1 = (int)blockIdx.x >= G0;
@@ -57,8 +57,10 @@ __global__ __launch_bounds__(kThreads) void deepmind_rows_kernel(DmArgs a, DmGro
     const int Uv = max(0, min(U, S - w * U));
     const int UOv = max(0, min(UO, S - w * UO));
     const int UO2v = max(0, min(UO2, Q - w * UO2));
-    const bool loader = wave == kLoaderWave;
+    const bool loader = wave >= kLoaderWave;           // waves 4-7: tile DMA (split four ways)
+    const bool lead = wave == kLoaderWave;             // wave 4: flag polls, draws, samplers
     const bool compute = !loader;
+    int *go = abort_flag + 1;                          // LDS: wave 4 → the other loaders, "flags seen"
     const int eng = wave * 4 + row;
     const size_t hop_sz = (size_t)2 * B * KA;
     auto actp = [&](int hop, int t) { return a.act + hop * hop_sz + (size_t)(t & 1) * B * KA; };
@@ -70,6 +72,13 @@ __global__ __launch_bounds__(kThreads) void deepmind_rows_kernel(DmArgs a, DmGro
     auto xgp = [&](int which) { return a.xg + (size_t)which * kXReps * kXRepStride; };
     auto dma = [&](float *dst, const float *src, int n) {
         for (int c = 0; c < n; c += 256)
+            if (c + lane * 4 < n)
+                __builtin_amdgcn_global_load_lds(WRNN_GPTR(src + c + lane * 4), WRNN_LPTR(dst + c), 16, 0, 16);
+    };
+    // the same split over the four loader waves (1 KiB pieces, round robin): one wave streams a
+    // fresh tile at only ~15 GB/s (MI355X_MICROARCH.md handoff-payload)
+    auto dma_part = [&](float *dst, const float *src, int n) {
+        for (int c = (wave - kLoaderWave) * 256; c < n; c += kDmLoaders * 256)
             if (c + lane * 4 < n)
                 __builtin_amdgcn_global_load_lds(WRNN_GPTR(src + c + lane * 4), WRNN_LPTR(dst + c), 16, 0, 16);
     };
@@ -89,16 +98,19 @@ __global__ __launch_bounds__(kThreads) void deepmind_rows_kernel(DmArgs a, DmGro
     {
         const float4 *src = reinterpret_cast<const float4 *>(a.slab + (size_t)w * s.total);
         float4 *dst = reinterpret_cast<float4 *>(smem + ll.slab);
-        for (int i = tid; i < s.total / 4; i += kThreads) dst[i] = src[i];
+        for (int i = tid; i < s.total / 4; i += kDmThreads) dst[i] = src[i];
         const float *cs = a.state + (size_t)w * B * SW;
-        for (int i = tid; i < B * SW; i += kThreads) st[i] = a.t0 > 0 ? cs[i] : 0.0f;
+        for (int i = tid; i < B * SW; i += kDmThreads) st[i] = a.t0 > 0 ? cs[i] : 0.0f;
         const float *cx = a.state + (size_t)G * B * SW;
-        for (int i = tid; i < B; i += kThreads) {   // out_coarse = out_fine = 0 initially (:89-90)
+        for (int i = tid; i < B; i += kDmThreads) {   // out_coarse = out_fine = 0 initially (:89-90)
             pcv[i] = a.t0 > 0 ? cx[i] : 0.0f;
             pfv[i] = a.t0 > 0 ? cx[B + i] : 0.0f;
         }
-        if (tid == 0) *abort_flag = 0;
-        load_noise(a.t0, tid, kThreads);
+        if (tid == 0) {
+            *abort_flag = 0;
+            *go = -1;
+        }
+        load_noise(a.t0, tid, kDmThreads);
     }
     __syncthreads();
 
@@ -109,9 +121,16 @@ __global__ __launch_bounds__(kThreads) void deepmind_rows_kernel(DmArgs a, DmGro
     auto run_stage = [&](int hop, int K, auto &&jobs) -> bool {
         const float *src = actp(hop, t_cur);
         const int ntiles = (B + TB - 1) / TB;
-        if (loader) {
-            wait_flags(flagp(hop), G, (unsigned)t_cur + 1u, a.ctl, a.timeout_ticks, t_cur, hop, abort_flag);
-            if (!*abort_flag) dma(tbuf(0), src, min(TB, B) * K);
+        if (loader) {   // wave 4 polls the flags and releases waves 5-7 through an LDS word
+            const int go_val = (t_cur + 1) * kDmHops + hop;
+            if (lead) {
+                wait_flags(flagp(hop), G, (unsigned)t_cur + 1u, a.ctl, a.timeout_ticks, t_cur, hop, abort_flag);
+                __hip_atomic_store(go, go_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {
+                while (__hip_atomic_load(go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != go_val)
+                    __builtin_amdgcn_s_sleep(1);
+            }
+            if (!*reinterpret_cast<volatile int *>(abort_flag)) dma_part(tbuf(0), src, min(TB, B) * K);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         bar();
@@ -119,7 +138,7 @@ __global__ __launch_bounds__(kThreads) void deepmind_rows_kernel(DmArgs a, DmGro
         for (int k = 0; k < ntiles; ++k) {
             const int tb0 = k * TB, nb = min(TB, B - tb0);
             if (loader && k + 1 < ntiles) {
-                dma(tbuf(k + 1), src + (size_t)(tb0 + TB) * K, min(TB, B - tb0 - TB) * K);
+                dma_part(tbuf(k + 1), src + (size_t)(tb0 + TB) * K, min(TB, B - tb0 - TB) * K);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
             if (compute) jobs(tbuf(k), tb0, nb);
@@ -208,7 +227,7 @@ __global__ __launch_bounds__(kThreads) void deepmind_rows_kernel(DmArgs a, DmGro
     auto sample = [&](int hop, int which, int t, bool fine) -> bool {
         if (w >= B) return true;
         const float *src = actp(hop, t);
-        if (loader) {
+        if (lead) {
             wait_flags(flagp(hop), G, (unsigned)t + 1u, a.ctl, a.timeout_ticks, t, hop, abort_flag);
             if (!*abort_flag)
                 for (int sr = 0; sr < NS && w + sr * G < B; ++sr) dma(tile + sr * ll.KT, src + (size_t)(w + sr * G) * Q, Q);
@@ -277,21 +296,21 @@ __global__ __launch_bounds__(kThreads) void deepmind_rows_kernel(DmArgs a, DmGro
         signal(DH_LF, t);
         // ---- sample f_t; collect f_t of every row; previous labels ← (c_t, f_t)
         if (!sample(DH_LF, 1, t, true)) return;
-        if (loader && tl + 1 < a.Lc) {
+        if (lead && tl + 1 < a.Lc) {
             load_noise(t + 1, lane, 64);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         gather_labels(1, t, pfv);
-        for (int i = tid; i < B; i += kThreads) pcv[i] = cnew[i];
+        for (int i = tid; i < B; i += kDmThreads) pcv[i] = cnew[i];
         bar();
         if (*abort_flag) return;
     }
 
     {
         float *cs = a.state + (size_t)w * B * SW;
-        for (int i = tid; i < B * SW; i += kThreads) cs[i] = st[i];
+        for (int i = tid; i < B * SW; i += kDmThreads) cs[i] = st[i];
         if (w == 0)
-            for (int i = tid; i < B; i += kThreads) {
+            for (int i = tid; i < B; i += kDmThreads) {
                 a.state[(size_t)G * B * SW + i] = pcv[i];
                 a.state[(size_t)G * B * SW + B + i] = pfv[i];
             }
@@ -307,7 +326,7 @@ hipError_t launch_dm(const DmArgs &a, const DmGroup *g1, size_t lds_bytes, hipSt
     DmGroup grp = g1 ? *g1 : DmGroup{};
     int G0 = a.G;
     void *params[] = {&args, &grp, &G0};
-    return hipLaunchKernel(pick_dm_kernel(a), dim3(g1 ? 2 * a.G : a.G), dim3(kThreads), params, lds_bytes, st);
+    return hipLaunchKernel(pick_dm_kernel(a), dim3(g1 ? 2 * a.G : a.G), dim3(kDmThreads), params, lds_bytes, st);
 }
 
 hipError_t prepare_dm_kernel(int max_lds_bytes) {
@@ -322,7 +341,7 @@ hipError_t dm_occupancy(int *blocks_per_cu, size_t lds_bytes) {
     int best = 1 << 30;
     for (const void *k : {(const void *)deepmind_rows_kernel<448>, (const void *)deepmind_rows_kernel<0>}) {
         int n = 0;
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kThreads, lds_bytes);
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kDmThreads, lds_bytes);
         if (e != hipSuccess) return e;
         best = n < best ? n : best;
     }
