@@ -12,10 +12,10 @@ import torch
 from wavernn_amd import synthetic as syn
 from wavernn_amd.loop import FatchordLoop
 
-GRU = [(0, "start"), (1, "GRU1 done"), (2, "Y published (GRU2 done)"), (3, "phase C done (F2 gathered)"),
-       (4, "fc3 done"), (5, "sample done")]
-FC = [(0, "start"), (1, "Y gathered"), (6, "f1 published"), (2, "F1 gathered"), (7, "f2 published"),
-      (3, "F2 gathered"), (4, "fc3 done"), (5, "sample done")]
+GRU = [(0, "start"), (1, "GRU1 done"), (2, "Y published (GRU2 done)"), (4, "F2 partial logits gathered"),
+       (5, "sample done"), (3, "phase C done")]
+FC = [(0, "start"), (1, "Y gathered"), (6, "f1 published"), (2, "F1 gathered"), (3, "fc2 done"),
+      (7, "partial logits published")]
 
 
 def main(L=3000):

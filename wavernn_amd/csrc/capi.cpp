@@ -595,15 +595,14 @@ size_t lds_bytes_for(const wrnn_ctx &h, int Bc) {
 }
 
 // ------------------------------------------------------------- batch-1 role-split kernel
-// GRU workgroup g owns units 4g..4g+3 (rows u·3 + gate), FC workgroup f owns fc rows 16f..16f+15;
-// the MoL head is first in both slabs (same LDS address in every workgroup).
+// GRU workgroup g owns units 4g..4g+3 (rows u·3 + gate), FC workgroup f owns fc rows 16f..16f+15
+// and the fc3 columns of those rows (fatchord_split.h, slabs).
 void make_split_slabs(wrnn_ctx &h) {
     const int R = h.cfg.rnn_dims, F = h.cfg.fc_dims, NC = h.cfg.n_classes;
     constexpr int U = kSplitUnits, NF = kSplitFcRows;
     int o = 0;
     auto take = [&](int n) { int at = o; o += round4(n); return at; };
     SplitGruSlab &g = h.sgs;
-    g.w3 = take(NC * F);
     g.b3 = take(NC);
     g.wih2 = take(3 * U * R);
     g.whh1 = take(3 * U * R);
@@ -618,8 +617,7 @@ void make_split_slabs(wrnn_ctx &h) {
     g.total = o;
     o = 0;
     SplitFcSlab &f = h.sfs;
-    f.w3 = take(NC * F);
-    f.b3 = take(NC);
+    f.w3p = take(NF * kSplitLogitLine);
     f.w1 = take(NF * R);
     f.w2 = take(NF * F);
     f.total = o;
@@ -644,7 +642,6 @@ void pack_split_slabs(const wrnn_ctx &h, std::vector<float> &gs, std::vector<flo
     for (int r = 0; r < 3 * R; ++r) q1a[r] = xcol_dot(W("rnn1.weight_ih_l0") + (size_t)r * R, IW, nin, R);
     for (int w = 0; w < h.sGg; ++w) {
         float *out = gs.data() + (size_t)w * sg.total;
-        std::memcpy(out + sg.w3, W("fc3.weight"), (size_t)NC * F * 4);
         std::memcpy(out + sg.b3, W("fc3.bias"), (size_t)NC * 4);
         std::memcpy(out + sg.q1a, q1a.data(), (size_t)3 * R * 4);
         for (int u = 0; u < U; ++u) {
@@ -666,10 +663,9 @@ void pack_split_slabs(const wrnn_ctx &h, std::vector<float> &gs, std::vector<flo
     }
     for (int w = 0; w < h.sGf; ++w) {
         float *out = fs.data() + (size_t)w * sf.total;
-        std::memcpy(out + sf.w3, W("fc3.weight"), (size_t)NC * F * 4);
-        std::memcpy(out + sf.b3, W("fc3.bias"), (size_t)NC * 4);
         for (int e = 0; e < NF; ++e) {
             const int r = w * NF + e;
+            for (int j = 0; j < NC; ++j) out[sf.w3p + e * kSplitLogitLine + j] = W("fc3.weight")[(size_t)j * F + r];
             std::memcpy(out + sf.w1 + (size_t)e * R, W("fc1.weight") + (size_t)r * (R + A), R * 4);
             std::memcpy(out + sf.w2 + (size_t)e * F, W("fc2.weight") + (size_t)r * (F + A), F * 4);
         }
@@ -963,7 +959,8 @@ int generate_split(wrnn_t *h, const float *cond, int B, int L, const float *nois
     // 4 replicas of every hand-off vector: 6.31 us/step vs 6.36 at 8, 6.45 at 2, 7.05 at 16 (MI355X, v8)
     const int reps = std::max(1, std::min(32, rep_env ? std::atoi(rep_env) : 4));
     const long long vec_max = std::max<long long>({(long long)kTermsPerUnit * R, (long long)R, (long long)c.fc_dims,
-                                                   (long long)(R / kSplitUnits) * kYLine});
+                                                   (long long)(R / kSplitUnits) * kYLine,
+                                                   (long long)h->sGf * kSplitLogitLine});
     const long long rep_stride = (((vec_max + kOverRead) * 8 + 65535) / 65536) * 65536 / 8;
     const size_t need_xg = (size_t)kSplitHops * reps * rep_stride;
     HIP_TRY(h, ensure(h->d_xg, h->xg_cap, need_xg));

@@ -24,14 +24,16 @@ enum SplitHop { SH_Y = 0, SH_F1 = 1, SH_F2 = 2, SH_H2A = 3, SH_H2B = 4, SH_S0 = 
 //   FC workgroup:  [0,16) V1c = W1[:, R:]·a3 + b1,  [16,32) V2 = W2[:, F:]·a4 + b2
 enum SplitTerm { ST_P1 = 0, ST_P2 = 12, ST_CI = 24, ST_V1 = 0, ST_V2 = 16 };
 
-// Slabs (floats).  The MoL head (fc3) sits at offset 0 in both, so the shared fc3 / sampler
-// code reads it at the same LDS address in every workgroup.
+// Slabs (floats).  fc3 is split by its input columns: FC workgroup f holds W3[:, 16f..16f+15]
+// (w3p[e·32 + j] = W3[j][16f + e]) and publishes the 30 partial logits of its 16 f2 rows; the
+// GRU workgroups keep only b3 for the sum.
 struct SplitGruSlab {
-    int w3, b3, wih2, whh1, whh2, q1a, q2, wi0, bih1, bhh1, bih2, bhh2, total;
+    int b3, wih2, whh1, whh2, q1a, q2, wi0, bih1, bhh1, bih2, bhh2, total;
 };
 struct SplitFcSlab {
-    int w3, b3, w1, w2, total;
+    int w3p, w1, w2, total;
 };
+constexpr int kSplitLogitLine = 32;   // granules per FC workgroup in the partial-logit vector
 
 // Per-workgroup state carried between time chunks (floats):
 // [h1 R | h2 R | GRU1 terms 4R | gh2 24 | h2own 4 | x | pad]
@@ -59,7 +61,7 @@ struct SplitArgs {
 };
 
 struct SplitLds {
-    int slab, va, vb, f2, lg, sg, ring, nz, gh2, gh1, h2own, xprev, flag, stamp, total;
+    int slab, va, vb, f2, sg, ring, nz, gh2, gh1, h2own, xprev, flag, stamp, total;
 };
 
 __host__ __device__ inline SplitLds split_lds_layout(int slab_total, int R, int F) {
@@ -68,15 +70,14 @@ __host__ __device__ inline SplitLds split_lds_layout(int slab_total, int R, int 
     l.slab = o;  o += round4(slab_total);
     l.va = o;    o += round4(R > F ? R : F);     // GRU: h1          FC: y = x_I + h1 + h2
     l.vb = o;    o += round4(R > F ? R : F);     // GRU: h2 (all)    FC: f1
-    l.f2 = o;    o += round4(F);
-    l.lg = o;    o += 32;
+    l.f2 = o;    o += 32;                         // FC: its own 16 f2 rows
     l.sg = o;    o += kTermsPerUnit * R;          // GRU1 terms of all units for the coming step
     l.ring = o;  o += kSplitRing * kSplitTerms;
     l.nz = o;    o += kSplitRing * kSplitNoise;
     l.gh2 = o;   o += 2 * 12;                     // W_hh2·h2 of own units, by step parity
     l.gh1 = o;   o += 12;
     l.h2own = o; o += 4;
-    l.xprev = o; o += 4;
+    l.xprev = o; o += 4;                          // x_t, by step parity
     l.flag = o;  o += 4;
     l.stamp = o; o += 2 * kStamps;
     l.total = o;

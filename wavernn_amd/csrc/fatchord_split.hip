@@ -7,19 +7,22 @@
 //   GRU workgroups (Gg = R/4): 4 hidden units of both GRUs.  GRU1 runs for ALL units in every
 //     GRU workgroup (local gate math on gathered terms, as in fatchord_loop.hip), GRU2 for the
 //     own units; each publishes y_j = x_I,j + h1_j + h2_j (fc1's input, :212-216) and h2_j.
-//   FC workgroups (Gf = F/16): 16 rows of fc1 and of fc2, one per 16-lane engine.
-//   Every GRU workgroup gathers f2 and runs fc3 + the MoL sampler redundantly (bit-identical),
-//     so the sample needs no hand-off of its own; the FC workgroups need no x.
+//   FC workgroups (Gf = F/16): 16 rows of fc1 and of fc2, one per 16-lane engine, and the fc3
+//     columns of its f2 rows: it publishes 30 partial logits W3[:, own rows]·f2[own rows].
+//   Every GRU workgroup gathers the partial logits, sums them and runs the MoL sampler
+//     redundantly (bit-identical), so the sample needs no hand-off of its own; the FC
+//     workgroups need no x.
 //
 // Critical path per step:
 //   x_{t-1} → GRU1 (all units) → W_ih2[:, :R]·h1 → GRU2 gates → [hop Y: Gg → Gf]
-//   → W1[:, :R]·y → [hop F1: Gf → Gf] → W2[:, :F]·f1 → [hop F2: Gf → Gg] → fc3 → sample → x_t
+//   → W1[:, :R]·y → [hop F1: Gf → Gf] → W2[:, :F]·f1 → fc3 partials → [hop F2: Gf → Gg]
+//   → Σ partials + b3 → sample → x_t
 // Off the critical path, while fc1/fc2 run in the FC workgroups, the GRU workgroups compute
 // GH1 = W_hh1·h1_t → publish step t+1's GRU1 terms, gather h2_t → GH2 = W_hh2·h2_t, and
 // gather step t+1's terms of all units.  Everything that depends only on the conditioning
 // (P1 = W_ih1·cI, P2 = W_ih2·[cI; a2], V1c = W1[:, R:]·a3 + b1, V2 = W2[:, F:]·a4 + b2, and
 // cI itself) comes from one fp32 GEMM before the launch (capi.cpp) and is streamed into an LDS
-// ring by the loader wave, so the LDS holds only the loop matrices and the MoL head.
+// ring by the loader wave, so the LDS holds only the loop matrices (and, FC, 16 fc3 columns).
 //
 // Arithmetic is fp32; the sums are re-associated like fatchord_loop.hip's (tolerance-checked
 // against the oracle).  Every wait is bounded; a timeout sets the abort word.
@@ -57,7 +60,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_split_kernel(SplitArgs a) {
     const int g = gru ? w : w - a.Gg;                 // index within the role
     const SplitLds ll = split_lds_layout(a.gs.total > a.fs.total ? a.gs.total : a.fs.total, R, F);
     const float *S = smem + ll.slab;
-    float *va = smem + ll.va, *vb = smem + ll.vb, *f2 = smem + ll.f2, *lg = smem + ll.lg, *sg = smem + ll.sg;
+    float *va = smem + ll.va, *vb = smem + ll.vb, *f2 = smem + ll.f2, *sg = smem + ll.sg;
     float *ring = smem + ll.ring, *nzr = smem + ll.nz, *gh2 = smem + ll.gh2, *gh1 = smem + ll.gh1;
     float *h2own = smem + ll.h2own, *xprev = smem + ll.xprev;
     int *abort_flag = reinterpret_cast<int *>(smem + ll.flag);
@@ -110,6 +113,51 @@ __global__ __launch_bounds__(kThreads) void fatchord_split_kernel(SplitArgs a) {
             XG(SH_S0 + (t & 1)) + poll_off, RT, RT, (uint32_t)t + 1u, a.ctl, a.timeout_ticks, t, SH_S0 + (t & 1),
             abort_flag, lane, store_sg);
     };
+    // fc3 logits of step t (:223) from the FC workgroups' partial sums (hop F2), one wave: lane l
+    // polls logit j = l & 31 of producers (l >> 5)·kPh … +kPh-1 and sums them pairwise; the two
+    // halves meet across the wave (identical bits in both), + b3.  Lanes with j >= 30 re-read
+    // logit 0 (their result is not used).
+    constexpr int kPh = F / kSplitFcRows / 2;
+    static_assert(kPh >= 1 && (kPh & (kPh - 1)) == 0 && kPh <= 16, "logit gather layout");
+    auto gather_logits = [&](uint32_t tag, int t) -> float {
+        const int j = lane & 31, jj = j < NC ? j : 0;
+        const unsigned long long *gp = XG(SH_F2) + poll_off + (size_t)(lane >> 5) * kPh * kSplitLogitLine + jj;
+        const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
+        unsigned spins = 0;
+        float p[kPh];
+        for (;;) {
+            unsigned long long v[kPh];
+#pragma unroll
+            for (int k = 0; k < kPh; ++k)
+                v[k] = __hip_atomic_load(gp + k * kSplitLogitLine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            bool ok = true;
+#pragma unroll
+            for (int k = 0; k < kPh; ++k) ok &= (uint32_t)(v[k] >> 32) == tag;
+            if (ok) {
+#pragma unroll
+                for (int k = 0; k < kPh; ++k) p[k] = __uint_as_float((uint32_t)v[k]);
+                break;
+            }
+            if ((++spins & 63u) == 0) {
+                const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - c0) > a.timeout_ticks;
+                const bool other = __hip_atomic_load(&a.ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+                if (late || other) {
+                    if (late) record_abort(a.ctl, -4, t, SH_F2, w);
+                    *abort_flag = 1;
+#pragma unroll
+                    for (int k = 0; k < kPh; ++k) p[k] = 0.0f;
+                    break;
+                }
+            }
+        }
+#pragma unroll
+        for (int n = kPh / 2; n >= 1; n /= 2)
+#pragma unroll
+            for (int k = 0; k < n; ++k) p[k] += p[k + n];
+        float s = p[0];
+        s += __shfl_xor(s, 32);
+        return s + S[a.gs.b3 + jj];
+    };
 
     // ---- prologue: slab → LDS, state (zero, or carried from the previous time chunk), the
     // terms and noise of the first two steps; at t = 0 the GRU1 terms of step 0 (GH1 = 0)
@@ -131,7 +179,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_split_kernel(SplitArgs a) {
             h2own[tid] = resume ? st[6 * R + 24 + tid] : 0.0f;
             abort_flag[tid] = 0;
         }
-        if (tid == 0) xprev[0] = a.t0 > 0 ? a.state[(size_t)w * split_state_w(R) + 6 * R + 28] : 0.0f;
+        if (tid == 0) xprev[(a.t0 + 1) & 1] = a.t0 > 0 ? a.state[(size_t)w * split_state_w(R) + 6 * R + 28] : 0.0f;
         for (int t = a.t0; t < a.t0 + 2; ++t) {
             if (t <= t_terms)
                 for (int i = tid; i < kSplitTerms; i += kThreads)
@@ -152,7 +200,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_split_kernel(SplitArgs a) {
     auto loader_top = [&](int t) {
         if (dbg_on && t > a.t0 && t - 1 - a.t0 < a.dbg_steps && lane < kStamps)
             a.dbg[((size_t)w * a.dbg_steps + (t - 1 - a.t0)) * kStamps + lane] = stamp[((t - 1) & 1) * kStamps + lane];
-        if (w == 0 && lane == 0 && t > a.t0) a.out[(size_t)a.b0 * a.L + (t - 1)] = xprev[0];
+        if (w == 0 && lane == 0 && t > a.t0) a.out[(size_t)a.b0 * a.L + (t - 1)] = xprev[(t - 1) & 1];
         const int t2 = t + 2;
         if (t2 < a.L) fill_noise(t2);
         if (t2 <= t_terms && lane < kSplitTerms / 4)
@@ -160,7 +208,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_split_kernel(SplitArgs a) {
                                              WRNN_LPTR(RING(t2)), 16, 0, 0);
     };
 
-    float x = xprev[0];   // x_{t-1}, wave-uniform in every compute wave
+    float x = xprev[(a.t0 + 1) & 1];   // x_{t-1}, wave-uniform in every compute wave
     for (int t = a.t0; t < t_end; ++t) {
         const uint32_t tag = (uint32_t)t + 1u;
         const bool more = t + 1 < a.L;
@@ -208,8 +256,13 @@ __global__ __launch_bounds__(kThreads) void fatchord_split_kernel(SplitArgs a) {
             // stores leave the CU (vmcnt(0)): polls queued behind them slow the critical y hop
             if (kDrainPub && wave != 1 && !loader) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (wave == 0) {
-                gather<NG_F, kPollThreads>(XG(SH_F2) + poll_off, 0, F, F, tag, a.ctl, a.timeout_ticks, t, SH_F2,
-                                           abort_flag, lane, [&](int, int k, float v) { f2[k] = v; });
+                // ---- D + E: fc3 logits (hop F2: partial sums) → MoL sample (:223-229) → x_t
+                const float ul = NZ(t)[lane < 10 ? lane : 0], u10 = NZ(t)[10];
+                const float s = gather_logits(tag, t);
+                SSTAMP(4);
+                const float xs = mol_sample_reg(s, ul, u10, lane);
+                if (lane == 0) xprev[t & 1] = xs;
+                SSTAMP(5);
             } else if (wave == 1) {
                 if (more) {
                     const float3 v = row_dot3(S + a.gs.whh1 + (row * 3 + 0) * R, S + a.gs.whh1 + (row * 3 + 1) * R,
@@ -271,41 +324,32 @@ __global__ __launch_bounds__(kThreads) void fatchord_split_kernel(SplitArgs a) {
             bar();
             SSTAMP(2);
             if (*abort_flag) return;
-            // ---- C': fc2 (:220-221), relu → hop F2
+            // ---- C': fc2 (:220-221), relu → the own 16 rows of f2 (LDS)
             if (!loader) {
                 const float v = row_dot(S + a.fs.w2 + e * F, vb, F / 4, li) + RING(t)[ST_V2 + e];
-                if (li < a.reps)
-                    publish(XG(SH_F2) + (size_t)li * a.rep_stride + g * kSplitFcRows + e, tag, v > 0.0f ? v : 0.0f);
-                if (dbg_on && tid == 0) stamp[(t & 1) * kStamps + 7] = (unsigned)__builtin_amdgcn_s_memrealtime();
+                if (li == 0) f2[e] = v > 0.0f ? v : 0.0f;
             }
-            // the FC workgroups need neither f2 nor x: they go straight to the next step's y
             if (loader) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             bar();
             SSTAMP(3);
             if (*abort_flag) return;
+            // ---- D': fc3 partial logits over the own f2 rows (:223) → hop F2; compute wave k
+            // publishes replicas k, k + 4, …  The FC workgroups need no x: on to the next y.
+            if (!loader && lane < NC) {
+                const float *w3p = S + a.fs.w3p + lane;
+                float p = 0.0f;
+#pragma unroll
+                for (int k = 0; k < kSplitFcRows; ++k) p = fmaf(w3p[k * kSplitLogitLine], f2[k], p);
+                for (int r = wave; r < a.reps; r += kWaves)
+                    publish(XG(SH_F2) + (size_t)r * a.rep_stride + g * kSplitLogitLine + lane, tag, p);
+            }
+            if (dbg_on && tid == 0) stamp[(t & 1) * kStamps + 7] = (unsigned)__builtin_amdgcn_s_memrealtime();
             continue;
         }
-
-        // ---- D: fc3 (:223), 30 rows over the 16 engines: rows e and e + 16
-        if (!loader) {
-            const int e = wave * 4 + row, e2 = e + 16 < NC ? e + 16 : NC - 1;
-            const float2 v = row_dot2(S + a.gs.w3 + e * F, S + a.gs.w3 + e2 * F, f2, F / 4, li);
-            if (li == 0) {
-                lg[e] = v.x + S[a.gs.b3 + e];
-                if (e + 16 < NC) lg[e + 16] = v.y + S[a.gs.b3 + e + 16];
-            }
-        }
-        bar();
-        SSTAMP(4);
-        // ---- E: sample (:225-229) in every compute wave: x_t stays in registers
-        if (!loader) {
-            x = mol_sample(lg, NZ(t), lane);
-            if (tid == 0) xprev[0] = x;
-        }
-        SSTAMP(5);
+        x = xprev[t & 1];   // sampled by wave 0 in phase C
     }
     __syncthreads();
-    if (w == 0 && tid == 0) a.out[(size_t)a.b0 * a.L + (t_end - 1)] = xprev[0];
+    if (w == 0 && tid == 0) a.out[(size_t)a.b0 * a.L + (t_end - 1)] = xprev[(t_end - 1) & 1];
     // carry the recurrent state to the next time chunk
     float *st = a.state + (size_t)w * split_state_w(R);
     for (int i = tid; i < R; i += kThreads) {
@@ -316,7 +360,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_split_kernel(SplitArgs a) {
         for (int i = tid; i < RT; i += kThreads) st[2 * R + i] = sg[i];
     if (tid < 24) st[6 * R + tid] = gh2[tid];
     if (tid < 4) st[6 * R + 24 + tid] = h2own[tid];
-    if (tid == 0) st[6 * R + 28] = xprev[0];
+    if (tid == 0) st[6 * R + 28] = xprev[(t_end - 1) & 1];
 }
 
 #define WRNN_K_SPLIT512 fatchord_split_kernel<512, 512>

@@ -428,6 +428,30 @@ __device__ __forceinline__ float mol_sample(const float *l, const float *u, int 
     return x;
 }
 
+// The same sampler with the logits in registers: lane l holds logit (l & 31) (lanes 0..29 are
+// read), ul = u[lane] for lanes 0..9, u10 = u[10].  The argmax over lanes 0..9 runs in DPP
+// row 0 (ties → the smaller index, as mol_sample's first-max scan); same arithmetic.
+__device__ __forceinline__ float mol_sample_reg(float s, float ul, float u10, int lane) {
+    float v = lane < 10 ? s - ul : -INFINITY;
+    int i = lane;
+#define WRNN_AM_STAGE(ctrl)                                                           \
+    {                                                                                 \
+        float ov = WRNN_DPP(v, ctrl);                                                 \
+        int oi = __builtin_amdgcn_mov_dpp(i, (ctrl), 0xF, 0xF, false);                \
+        am_merge(v, i, ov, oi);                                                       \
+    }
+    WRNN_AM_STAGE(0xB1) WRNN_AM_STAGE(0x4E) WRNN_AM_STAGE(0x141) WRNN_AM_STAGE(0x140)
+#undef WRNN_AM_STAGE
+    const int k = __builtin_amdgcn_readlane(i, 0);
+    const float mean = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, s), 10 + k));
+    const float ls = fmaxf(__builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, s), 20 + k)),
+                           -32.23619130191664f);
+    float x = mean + expf(ls) * u10;
+    x = x < -1.0f ? -1.0f : x;
+    x = x > 1.0f ? 1.0f : x;
+    return x;
+}
+
 // RAW (fatchord_version.py:231-237): softmax → Categorical (probs renormalised) → argmax(p / q),
 // q ~ Exp(1) (the multinomial sampling path Categorical.sample() takes).  Returns the label.
 template <int kClsPerLane>
