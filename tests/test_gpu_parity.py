@@ -167,6 +167,38 @@ def test_rows_two_groups_vs_oracle(mode, B, monkeypatch):
 
 
 @pytest.mark.parametrize("mode", ["MOL", "RAW"])
+@pytest.mark.parametrize("B", [1, 6, 16])
+@pytest.mark.parametrize("dims", ["default", "tiny"])
+def test_rows_granule_and_bulk_handoffs(mode, B, dims, monkeypatch):
+    """Small row groups hand activations over as tagged granules polled straight into LDS;
+    larger ones by bulk stores + flag + DMA.  Both forced, against the oracle (injected noise),
+    with time-chunked launches so the granule tags continue across launches; tiny dims have
+    rnn_dims != fc_dims != n_classes (tile row strides differ per hop)."""
+    monkeypatch.setenv("WRNN_PATH", "rows")
+    monkeypatch.setenv("WRNN_TERMS_MB", "4")
+    from oracle import oracle
+    if dims == "tiny":
+        d = syn.TINY_MOL if mode == "MOL" else syn.TINY_RAW
+    else:
+        d = syn.DEFAULT_MOL if mode == "MOL" else syn.DEFAULT_RAW
+    L = 300
+    state = syn.make_fatchord_state(d, 41)
+    mels, aux = syn.make_conditioning(B, L, d.feat_dims, d.res_out_dims, 42)
+    noise = syn.make_noise(mode, B, L, d.n_classes, 43)
+    ref, ref_lab = oracle.fatchord_loop(state, mode, mels, aux, noise)
+    for gran in ("0", "1"):
+        monkeypatch.setenv("WRNN_ROWS_GRANULES", gran)
+        loop = _loop(d)
+        loop.set_weights(state)
+        out, lab = loop.generate(_cond(mels, aux), noise=torch.from_numpy(noise).to(DEV), want_labels=True)
+        assert loop.info["last_path"] == 2
+        if mode == "RAW":
+            _report_raw(lab.cpu().numpy(), ref_lab)
+        else:
+            assert np.abs(out.cpu().numpy() - ref).max() <= gf.MOL_TOL, gran
+
+
+@pytest.mark.parametrize("mode", ["MOL", "RAW"])
 def test_row_groups_agree_under_philox(mode, monkeypatch):
     """One group of G workgroups vs two groups of G/2: same Philox keying by global row, so the
     same audio (RAW labels equal, MoL within tolerance)."""

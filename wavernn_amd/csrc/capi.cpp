@@ -90,6 +90,8 @@ struct wrnn_ctx {
     size_t X_cap = 0, T_cap = 0, act_cap = 0, state_cap = 0;   // floats
     unsigned *d_flags = nullptr;                    // [2 row groups][kRowsHops][kFlagSlots][kFlagStride]
     unsigned long long *d_xr = nullptr;             // x granules, [2 row groups][kXReps][kXRepStride]
+    unsigned long long *d_gact = nullptr;           // rows granule mode: [2 row groups][kRowsHops][gstride]
+    size_t gact_cap = 0;
     // the same weights over G/2 workgroups (twice the units each) for two row groups per launch
     // (large B: halves the activation rows every workgroup streams per stage); swapped into the
     // r* fields above while in use
@@ -752,10 +754,13 @@ int grow(wrnn_t *h, float *&p, size_t &cap, size_t n) {
 // MI355X (MoL 512, us/step, one group → two): B=2 17.2 → 15.7, B=10 18.3 → 16.9, B=32 26.6 →
 // 19.5, B=115 51.2 → 40.2: half the rows streamed per stage and half the flags per hop.
 constexpr int kGroupRows = 2;
+constexpr size_t kRowsGranMax = 4096;   // values per row group and hop up to which hops use granules
 
 int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed, int64_t row_offset,
                   float *out, int32_t *labels, hipStream_t st) {
     const wrnn_config &c = h->cfg;
+    const char *gran_env = std::getenv("WRNN_ROWS_GRANULES");
+    const int gran_force = gran_env ? std::atoi(gran_env) : -1;
     const char *grp_env = std::getenv("WRNN_ROW_GROUPS");
     const int grp_force = grp_env ? std::atoi(grp_env) : 0;
     const bool can_group = h->g2.ok && !h->sparse && grp_force != 1;
@@ -802,6 +807,15 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
             return WRNN_EHIP;
         HIP_TRY(h, hipMemsetAsync(h->d_flags, 0, ng * flag_words * 4, st));
         HIP_TRY(h, hipMemsetAsync(h->d_xr, 0, ng * xr_words * 8, st));
+        // granule hand-offs while a group's hop vector is small (kRowsGranMax values; measured
+        // crossover); WRNN_ROWS_GRANULES=0|1 forces bulk / granules.  The granules
+        // are zeroed per row block: tags restart at 1 with every generate()
+        const bool gran = gran_force == 1 || (gran_force != 0 && (size_t)Bg * h->KA <= kRowsGranMax);
+        const long long gstride = (((long long)Bg * h->KA + kRowsGranPad + 15) / 16) * 16;
+        if (gran) {
+            HIP_TRY(h, ensure(h->d_gact, h->gact_cap, (size_t)ng * kRowsHops * gstride));
+            HIP_TRY(h, hipMemsetAsync(h->d_gact, 0, (size_t)ng * kRowsHops * gstride * 8, st));
+        }
         for (int t0 = 0; t0 < L; t0 += Lc_max) {
             const int Lc = std::min(Lc_max, L - t0);
             // conditioning terms of steps [t0, t0 + Lc), per group: cI, then one fp32 GEMM for
@@ -824,6 +838,8 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
             a.act = h->d_act;
             a.flags = h->d_flags;
             a.xg = h->d_xr;
+            a.gact = gran ? h->d_gact : nullptr;
+            a.gstride = gstride;
             a.state = h->d_state;
             a.ctl = h->d_ctl;
             a.seed = seed;
@@ -858,6 +874,7 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
                 g1.act = h->d_act + act_grp;
                 g1.flags = h->d_flags + flag_words;
                 g1.xg = h->d_xr + xr_words;
+                g1.gact = gran ? h->d_gact + (size_t)kRowsHops * gstride : nullptr;
                 g1.state = h->d_state + state_grp;
                 g1.row0 = row_offset + b0 + Bg;
                 g1.B = group_rows(Bl, 1);
@@ -876,6 +893,8 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
 int generate_dm(wrnn_t *h, int B, int L, const float *noise, uint64_t seed, int64_t row_offset, float *out,
                 int32_t *labels, hipStream_t st) {
     // two row groups per launch (G/2 workgroups each) unless WRNN_ROW_GROUPS=1 or one row
+    const char *gran_env = std::getenv("WRNN_ROWS_GRANULES");
+    const int gran_force = gran_env ? std::atoi(gran_env) : -1;
     const char *grp_env = std::getenv("WRNN_ROW_GROUPS");
     const bool grouped = h->dm2.ok && B >= 2 && !(grp_env && std::atoi(grp_env) == 1);
     DmScope sc(*h, h->dm2, grouped);
@@ -1458,7 +1477,8 @@ void wrnn_destroy(wrnn_t *h) {
                     (void *)h->d_ctl, (void *)h->d_rslab, (void *)h->d_Wt, (void *)h->d_X, (void *)h->d_T,
                     (void *)h->d_act, (void *)h->d_state, (void *)h->d_flags, (void *)h->d_xr, (void *)h->d_dmslab,
                     (void *)h->d_dmflags, (void *)h->d_dmxg, (void *)h->d_sgslab, (void *)h->d_sfslab,
-                    (void *)h->d_sWt, (void *)h->g2.d_slab, (void *)h->g2.d_Wt, (void *)h->dm2.d_slab})
+                    (void *)h->d_sWt, (void *)h->g2.d_slab, (void *)h->g2.d_Wt, (void *)h->dm2.d_slab,
+                    (void *)h->d_gact})
         if (p) (void)hipFree(p);
     if (h->blas) (void)rocblas_destroy_handle(h->blas);
     delete h;

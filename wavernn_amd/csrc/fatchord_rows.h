@@ -12,6 +12,11 @@ namespace wrnn {
 // lane stores the step into the workgroup's flag; consumers poll every producer's flag, then
 // load the rows with sc1 LDS-DMA (MI355X_MICROARCH.md "Valid forms", first table row).
 constexpr int kRowsHops = 5;        // h1, h2, f1, f2, logits (RAW)
+// Granule hand-offs (small row counts): a stage's activations travel as 8-byte {tag, value}
+// granules that the loader waves poll straight into the LDS tile — no store drain, barrier, flag
+// or post-flag DMA.  kRowsGranNG loads per loader lane per poll round (4 loader waves).
+constexpr int kRowsGranNG = 16;
+constexpr int kRowsGranPad = kRowsGranNG * 256;   // granules a poll round may read past a vector
 constexpr int kFlagStride = 32;     // uints between two producers' flags (one 128-B line each)
 constexpr int kFlagSlots = 256;     // producer slots per hop: >= G, fixed so polls may over-read
 constexpr int kRowsMax = 256;       // rows per launch (x hand-off: <= 4 granules per polling lane)
@@ -64,6 +69,8 @@ struct RowsArgs {
     float *act;                   // [kRowsHops][2][B][KA] activations, parity = step & 1
     unsigned *flags;              // [kRowsHops][kFlagSlots][kFlagStride]
     unsigned long long *xg;       // [kXReps][kXRepStride] x granules {tag | value}
+    unsigned long long *gact;     // granule mode: [kRowsHops][gstride] {tag = step + 1 | value}; else nullptr
+    long long gstride;            // granules per hop (>= B·KA + kRowsGranPad)
     float *state;                 // [G][B][SW] carried state, then x [B]
     int *ctl;                     // as LoopArgs::ctl
     unsigned long long seed;
@@ -84,6 +91,7 @@ struct RowsGroup {
     float *act;
     unsigned *flags;
     unsigned long long *xg;
+    unsigned long long *gact;
     float *state;
     long long row0;
     int B, b0;

@@ -53,6 +53,7 @@ __global__ __launch_bounds__(kRowsThreads) void fatchord_rows_kernel(RowsArgs a,
         a.act = g1.act;
         a.flags = g1.flags;
         a.xg = g1.xg;
+        a.gact = g1.gact;
         a.state = g1.state;
         a.row0 = g1.row0;
         a.B = g1.B;
@@ -92,9 +93,26 @@ __global__ __launch_bounds__(kRowsThreads) void fatchord_rows_kernel(RowsArgs a,
     } while (0)
     auto actp = [&](int hop, int t) { return a.act + hop * hop_sz + (size_t)(t & 1) * B * KA; };
     auto flagp = [&](int hop) { return a.flags + (size_t)hop * kFlagSlots * kFlagStride; };
+    const bool gran = a.gact != nullptr;
     auto signal = [&](int hop, int t) {                // after every storing wave's vmcnt(0) + a barrier
-        if (tid == 0) __hip_atomic_store(flagp(hop) + w * kFlagStride, (unsigned)t + 1u, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
+        if (!gran && tid == 0)
+            __hip_atomic_store(flagp(hop) + w * kFlagStride, (unsigned)t + 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    };
+    // one activation value of row b, column k of hop `hop` at step t: a granule, or an sc1 store
+    // into the bulk matrix `bulk` (row stride K)
+    auto put = [&](int hop, float *bulk, int b, int K, int k, int t, float v) {
+        if (gran) publish(a.gact + (size_t)hop * a.gstride + (size_t)b * K + k, (uint32_t)t + 1u, v);
+        else store_sc1(bulk + (size_t)b * K + k, v);
+    };
+    // granule mode: rows [r0, r0 + nr) of hop `hop` (step t) polled by the four loader waves
+    // straight into an LDS tile, rows packed at stride K like the bulk DMA's
+    auto gran_tile = [&](float *dst, int hop, int K, int r0, int nr, int t) {
+        const int lid = (wave - kRowsLead) * 64 + lane;
+        auto st_ = [&](int b, int j, float v) { dst[b * K + j] = v; };
+        gather_chunked<kRowsGranNG, 256, decltype(st_)>(a.gact + (size_t)hop * a.gstride + (size_t)r0 * K, nr * K, K,
+                                                        (uint32_t)t + 1u, a.ctl, a.timeout_ticks, t, hop, abort_flag,
+                                                        lid, st_);
     };
     // LDS-DMA (sc1) of n floats (contiguous rows) from src into dst, issued by one wave
     auto dma = [&](float *dst, const float *src, int n) {
@@ -170,7 +188,9 @@ __global__ __launch_bounds__(kRowsThreads) void fatchord_rows_kernel(RowsArgs a,
     auto run_stage = [&](int hop, int K, auto &&jobs) -> bool {
         const float *src = actp(hop, t_cur);
         const int ntiles = (B + TB - 1) / TB;
-        if (loader) {
+        if (loader && gran) {
+            gran_tile(tbuf(0), hop, K, 0, min(TB, B), t_cur);
+        } else if (loader) {
             const int go_val = (t_cur + 1) * kRowsHops + hop;
             if (lead) {
                 wait_flags(flagp(hop), G, (unsigned)t_cur + 1u, a.ctl, a.timeout_ticks, t_cur, hop, abort_flag);
@@ -194,8 +214,12 @@ __global__ __launch_bounds__(kRowsThreads) void fatchord_rows_kernel(RowsArgs a,
             const int tb0 = k * TB, nb = min(TB, B - tb0);
             const unsigned long long c0 = dbgw ? __builtin_amdgcn_s_memrealtime() : 0;
             if (loader && k + 1 < ntiles) {
-                dma_part(tbuf(k + 1), src + (size_t)(tb0 + TB) * K, min(TB, B - tb0 - TB) * K);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (gran) {
+                    gran_tile(tbuf(k + 1), hop, K, tb0 + TB, min(TB, B - tb0 - TB), t_cur);
+                } else {
+                    dma_part(tbuf(k + 1), src + (size_t)(tb0 + TB) * K, min(TB, B - tb0 - TB) * K);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
             }
             if (compute) jobs(tbuf(k), tb0, nb);
             if (dbgw) busy += __builtin_amdgcn_s_memrealtime() - c0;
@@ -204,8 +228,10 @@ __global__ __launch_bounds__(kRowsThreads) void fatchord_rows_kernel(RowsArgs a,
         if (dbgw && hop == RH_H2 && t_cur - a.t0 < a.dbg_steps && lane == 0 && (wave == 0 || lead))
             dbgw[(size_t)(t_cur - a.t0) * kStamps + (lead ? 8 : 5)] = (unsigned)busy;
         if (hop == RH_H2) RSTAMP_T(14);
-        if (compute) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        bar();
+        if (!gran) {   // bulk: every storing wave drains before the stage's signal
+            if (compute) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            bar();
+        }
         if (hop == RH_H2) RSTAMP_T(15);
         return true;
     };
@@ -244,9 +270,9 @@ __global__ __launch_bounds__(kRowsThreads) void fatchord_rows_kernel(RowsArgs a,
                 }
                 const float hn = gru_gate_math(gi[0], gi[1], gi[2], gh[0], gh[1], gh[2], sb[u]);
                 sb[u] = hn;
-                store_sc1(h1o + (size_t)b * R + j, hn);
+                put(RH_H1, h1o, b, R, j, t, hn);
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (!gran) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         bar();
         signal(RH_H1, t);
@@ -299,7 +325,7 @@ __global__ __launch_bounds__(kRowsThreads) void fatchord_rows_kernel(RowsArgs a,
                                 }
                                 const float hn = gru_gate_math(gi[0], gi[1], gi[2], gh[0], gh[1], gh[2], sb[O_H2 + u]);
                                 sb[O_H2 + u] = hn;
-                                store_sc1(h2o + (size_t)b * R + w * U + u, hn);
+                                put(RH_H2, h2o, b, R, w * U + u, t, hn);
                             } else {      // GH1 of the next step
 #pragma unroll
                                 for (int g = 0; g < 3; ++g) sb[O_GH1 + g * U + u] = acc[g];
@@ -344,7 +370,7 @@ __global__ __launch_bounds__(kRowsThreads) void fatchord_rows_kernel(RowsArgs a,
                                 if (r >= UFv) break;
                                 const float v = acc[q] +
                                                 (st[b * SW + O_V1 + r] + fmaf(xs[b], S[s.q3 + r], T[b * NT + 6 * U + r]));
-                                store_sc1(f1o + (size_t)b * F + w * UF + r, v > 0.0f ? v : 0.0f);
+                                put(RH_F1, f1o, b, F, w * UF + r, t, v > 0.0f ? v : 0.0f);
                             }
                     } else {
                         const int jj = jb - nj1;
@@ -392,7 +418,7 @@ __global__ __launch_bounds__(kRowsThreads) void fatchord_rows_kernel(RowsArgs a,
                             const int r = r0 + q;
                             if (r >= UFv) break;
                             const float v = acc[q] + T[b * NT + 6 * U + UF + r];
-                            store_sc1(f2o + (size_t)b * F + w * UF + r, v > 0.0f ? v : 0.0f);
+                            put(RH_F2, f2o, b, F, w * UF + r, t, v > 0.0f ? v : 0.0f);
                         }
                 }
             });
@@ -417,7 +443,7 @@ __global__ __launch_bounds__(kRowsThreads) void fatchord_rows_kernel(RowsArgs a,
                         for (int q = 0; q < 2; ++q) {
                             const int r = r0 + q;
                             if (r >= UCv) break;
-                            store_sc1(lgo + (size_t)b * NC + w * UC + r, acc[q] + S[s.b3 + r]);
+                            put(RH_LG, lgo, b, NC, w * UC + r, t, acc[q] + S[s.b3 + r]);
                         }
                 }
             });
@@ -428,7 +454,14 @@ __global__ __launch_bounds__(kRowsThreads) void fatchord_rows_kernel(RowsArgs a,
             const int hop = MOL ? RH_F2 : RH_LG;
             const int K = MOL ? F : NC;
             const float *src = actp(hop, t);
-            if (lead) {
+            if (lead && gran) {
+                for (int sr = 0; sr < NS && w + sr * G < B; ++sr) {
+                    float *dst = tile + sr * ll.KT;
+                    auto st_ = [&](int, int j, float v) { dst[j] = v; };
+                    gather_chunked<8, 64, decltype(st_)>(a.gact + (size_t)hop * a.gstride + (size_t)(w + sr * G) * K, K,
+                                                        K, want, a.ctl, a.timeout_ticks, t, hop, abort_flag, lane, st_);
+                }
+            } else if (lead) {
                 wait_flags(flagp(hop), G, want, a.ctl, a.timeout_ticks, t, hop, abort_flag);
                 if (!*abort_flag)
                     for (int sr = 0; sr < NS && w + sr * G < B; ++sr)
