@@ -83,3 +83,20 @@ def test_dm_row_groups_agree(monkeypatch):
         res[g] = loop.generate(9, 300, seed=5)[1]
         loop.close()
     assert torch.equal(res["1"], res["2"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [3, 20, 40])
+def test_dm_granule_and_bulk_handoffs(B, monkeypatch):
+    """Granule hand-offs (small row groups) and bulk flag + DMA hand-offs, both forced: the
+    combined labels are bit-exact between the two (Philox keyed by global row)."""
+    from wavernn_amd.loop import DeepmindLoop
+    d = syn.DEFAULT_DM
+    res = {}
+    for g in ("0", "1"):
+        monkeypatch.setenv("WRNN_ROWS_GRANULES", g)
+        loop = DeepmindLoop(d.hidden_size, d.quantisation)
+        loop.set_weights(syn.make_deepmind_state(d, 23))
+        res[g] = loop.generate(B, 300, seed=7)[1]
+        loop.close()
+    assert torch.equal(res["0"], res["1"])

@@ -755,6 +755,7 @@ int grow(wrnn_t *h, float *&p, size_t &cap, size_t n) {
 // 19.5, B=115 51.2 → 40.2: half the rows streamed per stage and half the flags per hop.
 constexpr int kGroupRows = 2;
 constexpr size_t kRowsGranMax = 4096;   // values per row group and hop up to which hops use granules
+constexpr size_t kDmGranMax = 8192;     // the same for the deepmind kernel (one poll round of all waves)
 
 int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed, int64_t row_offset,
                   float *out, int32_t *labels, hipStream_t st) {
@@ -916,6 +917,14 @@ int generate_dm(wrnn_t *h, int B, int L, const float *noise, uint64_t seed, int6
         HIP_TRY(h, ensure(h->d_dmxg, h->dmxg_cap, 2 * xg_words));
         HIP_TRY(h, hipMemsetAsync(h->d_dmflags, 0, ng * flag_words * 4, st));
         HIP_TRY(h, hipMemsetAsync(h->d_dmxg, 0, ng * xg_words * 8, st));
+        // granule hand-offs while a group's hop vector is small (kDmGranMax values);
+        // WRNN_ROWS_GRANULES=0|1 forces bulk / granules
+        const bool gran = gran_force == 1 || (gran_force != 0 && (size_t)Bg * h->KA <= kDmGranMax);
+        const long long gstride = (((long long)Bg * h->KA + kDmGranPad + 15) / 16) * 16;
+        if (gran) {
+            HIP_TRY(h, ensure(h->d_gact, h->gact_cap, (size_t)ng * kDmHops * gstride));
+            HIP_TRY(h, hipMemsetAsync(h->d_gact, 0, (size_t)ng * kDmHops * gstride * 8, st));
+        }
         DmArgs a{};
         a.slab = h->d_dmslab;
         a.noise = noise;
@@ -924,6 +933,8 @@ int generate_dm(wrnn_t *h, int B, int L, const float *noise, uint64_t seed, int6
         a.act = h->d_act;
         a.flags = h->d_dmflags;
         a.xg = h->d_dmxg;
+        a.gact = gran ? h->d_gact : nullptr;
+        a.gstride = gstride;
         a.state = h->d_state;
         a.ctl = h->d_ctl;
         a.seed = seed;
@@ -950,6 +961,7 @@ int generate_dm(wrnn_t *h, int B, int L, const float *noise, uint64_t seed, int6
             g1.act = h->d_act + act_grp;
             g1.flags = h->d_dmflags + flag_words;
             g1.xg = h->d_dmxg + xg_words;
+            g1.gact = gran ? h->d_gact + (size_t)kDmHops * gstride : nullptr;
             g1.state = h->d_state + state_grp;
             g1.row0 = row_offset + b0 + Bg;
             g1.B = group_rows(Bl, 1);

@@ -13,6 +13,11 @@ enum DmHop { DH_HC = 0, DH_O1 = 1, DH_LC = 2, DH_HF = 3, DH_O3 = 4, DH_LF = 5, k
 // 8 waves: 0-3 compute (16 dot engines), 4-7 split each tile's LDS-DMA; wave 4 also polls flags
 constexpr int kDmLoaders = 4;
 constexpr int kDmThreads = kCompute + 64 * kDmLoaders;
+// Granule hand-offs (as fatchord_rows.h) while a group's hop vector holds <= kDmGranMax values:
+// a stage's first tile is polled by all eight waves (the compute waves would only wait at the
+// barrier), 16 loads per lane per round; later tiles by the four loader waves.
+constexpr int kDmGranNG = 16;
+constexpr int kDmGranPad = kDmGranNG * kDmThreads;
 
 // Per-workgroup resident weights (floats).  Workgroup w owns coarse units j = w·U + u and the
 // fine units S + j (u < U) — their u/r/e rows of R (3H × H, no bias, deepmind_version.py:16),
@@ -35,6 +40,8 @@ struct DmArgs {
     float *act;                   // [kDmHops][2][B][KA]
     unsigned *flags;              // [kDmHops][kFlagSlots][kFlagStride]
     unsigned long long *xg;       // [2 (coarse, fine)][kXReps][kXRepStride]
+    unsigned long long *gact;     // granule mode: [kDmHops][gstride] {tag = step + 1 | value}; else nullptr
+    long long gstride;
     float *state;                 // [G][B][SW] carried state, then prev labels [2][B]
     int *ctl;
     unsigned long long seed;
@@ -50,6 +57,7 @@ struct DmGroup {
     float *act;
     unsigned *flags;
     unsigned long long *xg;
+    unsigned long long *gact;
     float *state;
     long long row0;
     int B, b0;

@@ -36,6 +36,7 @@ __global__ __launch_bounds__(kDmThreads) void deepmind_rows_kernel(DmArgs a, DmG
         a.act = g1.act;
         a.flags = g1.flags;
         a.xg = g1.xg;
+        a.gact = g1.gact;
         a.state = g1.state;
         a.row0 = g1.row0;
         a.B = g1.B;
@@ -65,9 +66,31 @@ __global__ __launch_bounds__(kDmThreads) void deepmind_rows_kernel(DmArgs a, DmG
     const size_t hop_sz = (size_t)2 * B * KA;
     auto actp = [&](int hop, int t) { return a.act + hop * hop_sz + (size_t)(t & 1) * B * KA; };
     auto flagp = [&](int hop) { return a.flags + (size_t)hop * kFlagSlots * kFlagStride; };
+    const bool gran = a.gact != nullptr;
     auto signal = [&](int hop, int t) {
-        if (tid == 0) __hip_atomic_store(flagp(hop) + w * kFlagStride, (unsigned)t + 1u, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
+        if (!gran && tid == 0)
+            __hip_atomic_store(flagp(hop) + w * kFlagStride, (unsigned)t + 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    };
+    // one activation value (row b, column k, row stride K) of hop `hop` at step t: a granule, or
+    // an sc1 store into the bulk matrix
+    auto put = [&](int hop, float *bulk, int b, int K, int k, int t, float v) {
+        if (gran) publish(a.gact + (size_t)hop * a.gstride + (size_t)b * K + k, (uint32_t)t + 1u, v);
+        else store_sc1(bulk + (size_t)b * K + k, v);
+    };
+    // granule mode: rows [r0, r0 + nr) of a hop polled by the four loader waves into LDS (stride K)
+    auto gran_tile = [&](float *dst, int hop, int K, int r0, int nr, int t) {
+        const int lid = (wave - kLoaderWave) * 64 + lane;
+        auto st_ = [&](int b, int j, float v) { dst[b * K + j] = v; };
+        gather_chunked<kDmGranNG, 64 * kDmLoaders, decltype(st_)>(
+            a.gact + (size_t)hop * a.gstride + (size_t)r0 * K, nr * K, K, (uint32_t)t + 1u, a.ctl, a.timeout_ticks, t,
+            hop, abort_flag, lid, st_);
+    };
+    auto gran_tile_all = [&](float *dst, int hop, int K, int r0, int nr, int t) {   // every wave
+        auto st_ = [&](int b, int j, float v) { dst[b * K + j] = v; };
+        gather_chunked<kDmGranNG, kDmThreads, decltype(st_)>(
+            a.gact + (size_t)hop * a.gstride + (size_t)r0 * K, nr * K, K, (uint32_t)t + 1u, a.ctl, a.timeout_ticks, t,
+            hop, abort_flag, tid, st_);
     };
     auto xgp = [&](int which) { return a.xg + (size_t)which * kXReps * kXRepStride; };
     auto dma = [&](float *dst, const float *src, int n) {
@@ -121,7 +144,9 @@ __global__ __launch_bounds__(kDmThreads) void deepmind_rows_kernel(DmArgs a, DmG
     auto run_stage = [&](int hop, int K, auto &&jobs) -> bool {
         const float *src = actp(hop, t_cur);
         const int ntiles = (B + TB - 1) / TB;
-        if (loader) {   // wave 4 polls the flags and releases waves 5-7 through an LDS word
+        if (gran) {
+            gran_tile_all(tbuf(0), hop, K, 0, min(TB, B), t_cur);
+        } else if (loader) {   // wave 4 polls the flags and releases waves 5-7 through an LDS word
             const int go_val = (t_cur + 1) * kDmHops + hop;
             if (lead) {
                 wait_flags(flagp(hop), G, (unsigned)t_cur + 1u, a.ctl, a.timeout_ticks, t_cur, hop, abort_flag);
@@ -138,14 +163,20 @@ __global__ __launch_bounds__(kDmThreads) void deepmind_rows_kernel(DmArgs a, DmG
         for (int k = 0; k < ntiles; ++k) {
             const int tb0 = k * TB, nb = min(TB, B - tb0);
             if (loader && k + 1 < ntiles) {
-                dma_part(tbuf(k + 1), src + (size_t)(tb0 + TB) * K, min(TB, B - tb0 - TB) * K);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (gran) {
+                    gran_tile(tbuf(k + 1), hop, K, tb0 + TB, min(TB, B - tb0 - TB), t_cur);
+                } else {
+                    dma_part(tbuf(k + 1), src + (size_t)(tb0 + TB) * K, min(TB, B - tb0 - TB) * K);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
             }
             if (compute) jobs(tbuf(k), tb0, nb);
             bar();
         }
-        if (compute) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        bar();
+        if (!gran) {   // bulk: every storing wave drains before the stage's signal
+            if (compute) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            bar();
+        }
         return true;
     };
     // output rows r0, r0+1 of an S-input layer (O1..O4) on 4 activation rows
@@ -159,9 +190,9 @@ __global__ __launch_bounds__(kDmThreads) void deepmind_rows_kernel(DmArgs a, DmG
     };
     const int nUO = (UOv + 1) / 2, nUO2 = (UO2v + 1) / 2;
     // a layer stage: [out rows → act (relu optional) | R half-columns of the next step]
-    auto layer_jobs = [&](int wbase, int bbase, int nrows, int nstep, bool relu, float *dst, int dstK, int rowoff,
-                          int rhalf, int next_par) {
-        return [=, &st](const float *tl_, int tb0, int nb) {
+    auto layer_jobs = [&](int wbase, int bbase, int nrows, int nstep, bool relu, int dhop, float *dst, int dstK,
+                          int rowoff, int rhalf, int next_par, int t) {
+        return [=, &st, &put](const float *tl_, int tb0, int nb) {
             const int nbb = (nb + kNX - 1) / kNX, n1 = nstep * nbb, nj1 = round4(n1);
             const int nj2 = nj1 + (rhalf >= 0 ? 2 * Uv * nbb : 0);
             for (int jb = eng; jb < nj2; jb += kDotEngines) {
@@ -178,7 +209,7 @@ __global__ __launch_bounds__(kDmThreads) void deepmind_rows_kernel(DmArgs a, DmG
                             if (r >= nrows) break;
                             float v = acc[q] + W[bbase + r];
                             if (relu) v = v > 0.0f ? v : 0.0f;
-                            store_sc1(dst + (size_t)b * dstK + rowoff + r, v);
+                            put(dhop, dst, b, dstK, rowoff + r, t, v);
                         }
                 } else {
                     const int jj = jb - nj1, hu = jj % (2 * Uv), bb = jj / (2 * Uv);
@@ -194,7 +225,7 @@ __global__ __launch_bounds__(kDmThreads) void deepmind_rows_kernel(DmArgs a, DmG
         };
     };
     // gate update of own units of half h2 for every row; x3 = third I_fine input (fine only)
-    auto gates = [&](int h2, int par, float *dst, const float *xcur) {
+    auto gates = [&](int h2, int par, int dhop, float *dst, const float *xcur, int t) {
         for (int i = tid; i < B * Uv; i += kCompute) {
             const int b = i / Uv, u = i - b * Uv, j = w * U + u;
             const float x0 = pcv[b] / 127.5f - 1.0f, x1 = pfv[b] / 127.5f - 1.0f;   // (:106-108)
@@ -220,14 +251,22 @@ __global__ __launch_bounds__(kDmThreads) void deepmind_rows_kernel(DmArgs a, DmG
             const float ee = tanh_((rr * Rg[2] + I[2]) + W[s.be + h2 * U + u]);
             const float hn = uu * sb[h2 * O_HF + u] + (1.0f - uu) * ee;
             sb[h2 * O_HF + u] = hn;
-            store_sc1(dst + (size_t)b * S + j, hn);
+            put(dhop, dst, b, S, j, t, hn);
         }
     };
     // row-distributed sampling from the logits hop; publishes the label granule
     auto sample = [&](int hop, int which, int t, bool fine) -> bool {
         if (w >= B) return true;
         const float *src = actp(hop, t);
-        if (lead) {
+        if (lead && gran) {
+            for (int sr = 0; sr < NS && w + sr * G < B; ++sr) {
+                float *dst = tile + sr * ll.KT;
+                auto st_ = [&](int, int j, float v) { dst[j] = v; };
+                gather_chunked<8, 64, decltype(st_)>(a.gact + (size_t)hop * a.gstride + (size_t)(w + sr * G) * Q, Q, Q,
+                                                    (uint32_t)t + 1u, a.ctl, a.timeout_ticks, t, hop, abort_flag, lane,
+                                                    st_);
+            }
+        } else if (lead) {
             wait_flags(flagp(hop), G, (unsigned)t + 1u, a.ctl, a.timeout_ticks, t, hop, abort_flag);
             if (!*abort_flag)
                 for (int sr = 0; sr < NS && w + sr * G < B; ++sr) dma(tile + sr * ll.KT, src + (size_t)(w + sr * G) * Q, Q);
@@ -265,16 +304,16 @@ __global__ __launch_bounds__(kDmThreads) void deepmind_rows_kernel(DmArgs a, DmG
         t_cur = t;
         // ---- coarse gates → h_c
         if (compute) {
-            gates(0, par, actp(DH_HC, t), nullptr);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            gates(0, par, DH_HC, actp(DH_HC, t), nullptr, t);
+            if (!gran) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         bar();
         signal(DH_HC, t);
         // ---- O1 (relu) on h_c; R[:, :S]·h_c for the next step
-        if (!run_stage(DH_HC, S, layer_jobs(s.o1, s.o1b, UOv, nUO, true, actp(DH_O1, t), S, w * UO, 0, t + 1))) return;
+        if (!run_stage(DH_HC, S, layer_jobs(s.o1, s.o1b, UOv, nUO, true, DH_O1, actp(DH_O1, t), S, w * UO, 0, t + 1, t))) return;
         signal(DH_O1, t);
         // ---- O2 → coarse logits
-        if (!run_stage(DH_O1, S, layer_jobs(s.o2, s.o2b, UO2v, nUO2, false, actp(DH_LC, t), Q, w * UO2, -1, 0))) return;
+        if (!run_stage(DH_O1, S, layer_jobs(s.o2, s.o2b, UO2v, nUO2, false, DH_LC, actp(DH_LC, t), Q, w * UO2, -1, 0, t))) return;
         signal(DH_LC, t);
         // ---- sample c_t; everyone collects c_t of every row
         if (!sample(DH_LC, 0, t, false)) return;
@@ -283,16 +322,16 @@ __global__ __launch_bounds__(kDmThreads) void deepmind_rows_kernel(DmArgs a, DmG
         if (*abort_flag) return;
         // ---- fine gates → h_f
         if (compute) {
-            gates(1, par, actp(DH_HF, t), cnew);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            gates(1, par, DH_HF, actp(DH_HF, t), cnew, t);
+            if (!gran) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         bar();
         signal(DH_HF, t);
         // ---- O3 (relu) on h_f; R[:, S:]·h_f for the next step
-        if (!run_stage(DH_HF, S, layer_jobs(s.o3, s.o3b, UOv, nUO, true, actp(DH_O3, t), S, w * UO, 1, t + 1))) return;
+        if (!run_stage(DH_HF, S, layer_jobs(s.o3, s.o3b, UOv, nUO, true, DH_O3, actp(DH_O3, t), S, w * UO, 1, t + 1, t))) return;
         signal(DH_O3, t);
         // ---- O4 → fine logits
-        if (!run_stage(DH_O3, S, layer_jobs(s.o4, s.o4b, UO2v, nUO2, false, actp(DH_LF, t), Q, w * UO2, -1, 0))) return;
+        if (!run_stage(DH_O3, S, layer_jobs(s.o4, s.o4b, UO2v, nUO2, false, DH_LF, actp(DH_LF, t), Q, w * UO2, -1, 0, t))) return;
         signal(DH_LF, t);
         // ---- sample f_t; collect f_t of every row; previous labels ← (c_t, f_t)
         if (!sample(DH_LF, 1, t, true)) return;
