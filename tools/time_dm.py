@@ -5,8 +5,12 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from wavernn_amd import _native  # noqa: E402
 from wavernn_amd import synthetic as syn  # noqa: E402
 from wavernn_amd.loop import DeepmindLoop  # noqa: E402
+
+if os.environ.get("TIME_DM_LIB"):   # A/B of two builds of the library (diagnostics only)
+    _native.LIB_PATH = os.environ["TIME_DM_LIB"]
 
 
 def main(rows):
