@@ -48,7 +48,8 @@ constexpr bool kDrainPub = WRNN_DRAIN_PUB;
         if (dbg_on && tid == 0) stamp[(t & 1) * kStamps + (k)] = (unsigned)__builtin_amdgcn_s_memrealtime(); \
     } while (0)
 
-template <int kR, int kF>
+// kDbg: the WRNN_DEBUG_STAMPS build of the kernel (stamp code compiled out of the production one)
+template <int kR, int kF, bool kDbg>
 __global__ __launch_bounds__(kThreads) void fatchord_split_kernel(SplitArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int R = kR, F = kF, NC = 30, RT = kTermsPerUnit * R;
@@ -66,7 +67,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_split_kernel(SplitArgs a) {
     int *abort_flag = reinterpret_cast<int *>(smem + ll.flag);
     unsigned *stamp = reinterpret_cast<unsigned *>(smem + ll.stamp);
     const bool loader = wave == kLoaderWave;
-    const bool dbg_on = a.dbg != nullptr;
+    const bool dbg_on = kDbg && a.dbg != nullptr;
     const int N = (a.Gg + a.Gf) * kSplitTerms;        // terms per step, all workgroups
     const int term0 = w * kSplitTerms;                // this workgroup's columns
     const int t_end = a.t0 + a.Lc;
@@ -363,24 +364,36 @@ __global__ __launch_bounds__(kThreads) void fatchord_split_kernel(SplitArgs a) {
     if (tid == 0) st[6 * R + 28] = xprev[(t_end - 1) & 1];
 }
 
-#define WRNN_K_SPLIT512 fatchord_split_kernel<512, 512>
+#define WRNN_K_SPLIT512 fatchord_split_kernel<512, 512, false>
+#define WRNN_K_SPLIT512_DBG fatchord_split_kernel<512, 512, true>
 
 bool split_has_kernel(int R, int F) { return R == 512 && F == 512; }
 
 hipError_t launch_split(const SplitArgs &a, size_t lds_bytes, hipStream_t st) {
     SplitArgs args = a;
     void *params[] = {&args};
-    return hipLaunchKernel((const void *)WRNN_K_SPLIT512, dim3(a.Gg + a.Gf), dim3(kThreads), params, lds_bytes, st);
+    const void *k = a.dbg ? (const void *)WRNN_K_SPLIT512_DBG : (const void *)WRNN_K_SPLIT512;
+    return hipLaunchKernel(k, dim3(a.Gg + a.Gf), dim3(kThreads), params, lds_bytes, st);
 }
 
 hipError_t prepare_split_kernel(int max_lds_bytes) {
-    return hipFuncSetAttribute((const void *)WRNN_K_SPLIT512, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               max_lds_bytes);
+    for (const void *k : {(const void *)WRNN_K_SPLIT512, (const void *)WRNN_K_SPLIT512_DBG}) {
+        hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds_bytes);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t split_occupancy(int *blocks_per_cu, size_t lds_bytes) {
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, (const void *)WRNN_K_SPLIT512, kThreads,
-                                                        lds_bytes);
+    int best = 1 << 30;
+    for (const void *k : {(const void *)WRNN_K_SPLIT512, (const void *)WRNN_K_SPLIT512_DBG}) {
+        int n = 0;
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kThreads, lds_bytes);
+        if (e != hipSuccess) return e;
+        best = n < best ? n : best;
+    }
+    *blocks_per_cu = best;
+    return hipSuccess;
 }
 
 }  // namespace wrnn
