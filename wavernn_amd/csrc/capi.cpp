@@ -813,9 +813,12 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
         // are zeroed per row block: tags restart at 1 with every generate()
         const bool gran = gran_force == 1 || (gran_force != 0 && (size_t)Bg * h->KA <= kRowsGranMax);
         const long long gstride = (((long long)Bg * h->KA + kRowsGranPad + 15) / 16) * 16;
-        if (gran) {
-            HIP_TRY(h, ensure(h->d_gact, h->gact_cap, (size_t)ng * kRowsHops * gstride));
-            HIP_TRY(h, hipMemsetAsync(h->d_gact, 0, (size_t)ng * kRowsHops * gstride * 8, st));
+        // bulk mode, MoL: the f2 hop alone as granules (one hop region per group)
+        const bool f2g = !gran && mol;
+        if (gran || f2g) {
+            const size_t n = (size_t)ng * (gran ? kRowsHops : 1) * gstride;
+            HIP_TRY(h, ensure(h->d_gact, h->gact_cap, n));
+            HIP_TRY(h, hipMemsetAsync(h->d_gact, 0, n * 8, st));
         }
         for (int t0 = 0; t0 < L; t0 += Lc_max) {
             const int Lc = std::min(Lc_max, L - t0);
@@ -841,6 +844,7 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
             a.xg = h->d_xr;
             a.gact = gran ? h->d_gact : nullptr;
             a.gstride = gstride;
+            a.gf2 = f2g ? h->d_gact : nullptr;
             a.state = h->d_state;
             a.ctl = h->d_ctl;
             a.seed = seed;
@@ -876,6 +880,7 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
                 g1.flags = h->d_flags + flag_words;
                 g1.xg = h->d_xr + xr_words;
                 g1.gact = gran ? h->d_gact + (size_t)kRowsHops * gstride : nullptr;
+                g1.gf2 = f2g ? h->d_gact + gstride : nullptr;
                 g1.state = h->d_state + state_grp;
                 g1.row0 = row_offset + b0 + Bg;
                 g1.B = group_rows(Bl, 1);

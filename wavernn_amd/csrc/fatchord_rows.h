@@ -71,6 +71,8 @@ struct RowsArgs {
     unsigned long long *xg;       // [kXReps][kXRepStride] x granules {tag | value}
     unsigned long long *gact;     // granule mode: [kRowsHops][gstride] {tag = step + 1 | value}; else nullptr
     long long gstride;            // granules per hop (>= B·KA + kRowsGranPad)
+    unsigned long long *gf2;      // bulk mode, MoL: the f2 hop as granules [B][F] (samplers poll their
+                                  // row directly instead of all flags + DMA); else nullptr
     float *state;                 // [G][B][SW] carried state, then x [B]
     int *ctl;                     // as LoopArgs::ctl
     unsigned long long seed;
@@ -92,6 +94,7 @@ struct RowsGroup {
     unsigned *flags;
     unsigned long long *xg;
     unsigned long long *gact;
+    unsigned long long *gf2;
     float *state;
     long long row0;
     int B, b0;

@@ -54,6 +54,7 @@ __global__ __launch_bounds__(kRowsThreads) void fatchord_rows_kernel(RowsArgs a,
         a.flags = g1.flags;
         a.xg = g1.xg;
         a.gact = g1.gact;
+        a.gf2 = g1.gf2;
         a.state = g1.state;
         a.row0 = g1.row0;
         a.B = g1.B;
@@ -103,6 +104,7 @@ __global__ __launch_bounds__(kRowsThreads) void fatchord_rows_kernel(RowsArgs a,
     // into the bulk matrix `bulk` (row stride K)
     auto put = [&](int hop, float *bulk, int b, int K, int k, int t, float v) {
         if (gran) publish(a.gact + (size_t)hop * a.gstride + (size_t)b * K + k, (uint32_t)t + 1u, v);
+        else if (MOL && hop == RH_F2 && a.gf2) publish(a.gf2 + (size_t)b * K + k, (uint32_t)t + 1u, v);
         else store_sc1(bulk + (size_t)b * K + k, v);
     };
     // granule mode: rows [r0, r0 + nr) of hop `hop` (step t) polled by the four loader waves
@@ -454,12 +456,13 @@ __global__ __launch_bounds__(kRowsThreads) void fatchord_rows_kernel(RowsArgs a,
             const int hop = MOL ? RH_F2 : RH_LG;
             const int K = MOL ? F : NC;
             const float *src = actp(hop, t);
-            if (lead && gran) {
+            const unsigned long long *gsrc = gran ? a.gact + (size_t)hop * a.gstride : (MOL ? a.gf2 : nullptr);
+            if (lead && gsrc) {
                 for (int sr = 0; sr < NS && w + sr * G < B; ++sr) {
                     float *dst = tile + sr * ll.KT;
                     auto st_ = [&](int, int j, float v) { dst[j] = v; };
-                    gather_chunked<8, 64, decltype(st_)>(a.gact + (size_t)hop * a.gstride + (size_t)(w + sr * G) * K, K,
-                                                        K, want, a.ctl, a.timeout_ticks, t, hop, abort_flag, lane, st_);
+                    gather_chunked<8, 64, decltype(st_)>(gsrc + (size_t)(w + sr * G) * K, K, K, want, a.ctl,
+                                                        a.timeout_ticks, t, hop, abort_flag, lane, st_);
                 }
             } else if (lead) {
                 wait_flags(flagp(hop), G, want, a.ctl, a.timeout_ticks, t, hop, abort_flag);
