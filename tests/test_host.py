@@ -103,3 +103,52 @@ def test_golden_noise_layout_width():
     d, _, _, _, noise = gf.loop_inputs(fx)
     m = WaveRNN(**d.ctor_kwargs())
     assert noise.shape[-1] == m.noise_width() == d.n_classes
+
+
+@pytest.mark.parametrize("name,T", [("TINY_RAW", 6), ("DEFAULT_MOL", 2)])
+def test_training_forward_matches_numpy_restatement(name, T):
+    """Teacher-forced forward (fatchord_version.py:131-167) vs numpy fp64 on the same weights:
+    I → GRU1 (+res) → [·, a2] → GRU2 (+res) → [·, a3] → relu fc1 → [·, a4] → relu fc2 → fc3.
+    The upsample half is checked against the oracle in test_upsample_module_matches_oracle."""
+    d = getattr(syn, name)
+    m, state = _model(d, seed=4)
+    m.eval()
+    g = np.random.default_rng(1)
+    B = 2
+    mel = torch.from_numpy(g.uniform(0, 1, (B, d.feat_dims, T + 2 * d.pad)).astype(np.float32))
+    L = T * d.hop_length
+    x = torch.from_numpy(g.uniform(-1, 1, (B, L)).astype(np.float32))
+    step0 = m.get_step()
+    with torch.no_grad():
+        y = m(x, mel).numpy().astype(np.float64)
+        mels, aux = m.upsample(mel)
+    assert m.get_step() == step0 + 1
+    mels, aux = mels.numpy().astype(np.float64), aux.numpy().astype(np.float64)
+    f = {k: np.asarray(v, dtype=np.float64) for k, v in state.items()}
+    A = d.res_out_dims // 4
+    a = [aux[:, :, i * A:(i + 1) * A] for i in range(4)]
+    sig = lambda v: 1 / (1 + np.exp(-v))
+
+    def gru(inp, p):
+        H = f[f"{p}.weight_hh_l0"].shape[1]
+        h = np.zeros((inp.shape[0], H))
+        outs = []
+        for t in range(inp.shape[1]):
+            gi = inp[:, t] @ f[f"{p}.weight_ih_l0"].T + f[f"{p}.bias_ih_l0"]
+            gh = h @ f[f"{p}.weight_hh_l0"].T + f[f"{p}.bias_hh_l0"]
+            r = sig(gi[:, :H] + gh[:, :H])
+            z = sig(gi[:, H:2 * H] + gh[:, H:2 * H])
+            n = np.tanh(gi[:, 2 * H:] + r * gh[:, 2 * H:])
+            h = (1 - z) * n + z * h
+            outs.append(h)
+        return np.stack(outs, 1)
+
+    lin = lambda v, p: v @ f[f"{p}.weight"].T + f[f"{p}.bias"]
+    h = lin(np.concatenate([x.numpy()[..., None].astype(np.float64), mels, a[0]], 2), "I")
+    h = gru(h, "rnn1") + h
+    h = gru(np.concatenate([h, a[1]], 2), "rnn2") + h
+    h = np.maximum(lin(np.concatenate([h, a[2]], 2), "fc1"), 0)
+    h = np.maximum(lin(np.concatenate([h, a[3]], 2), "fc2"), 0)
+    ref = lin(h, "fc3")
+    assert y.shape == (B, L, m.n_classes)
+    np.testing.assert_allclose(y, ref, rtol=1e-4, atol=1e-4)
