@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define WRNN_ABI_VERSION 3
+#define WRNN_ABI_VERSION 4
 
 enum wrnn_status {
     WRNN_OK = 0,
@@ -68,9 +68,10 @@ typedef struct {
     int32_t on_device;       /* 1: `data` is a device pointer, 0: host pointer */
 } wrnn_tensor;
 
-/* Launch geometry chosen for the handle (read-only).  Kernels: the role-split kernel (one MoL
- * row), the per-row latency kernel (rows in LDS, used while B <= max_rows) and the multi-row
- * kernel (rows through HBM). */
+/* Launch geometry chosen for the handle (read-only).  Kernels: the XCD-resident kernel (MoL
+ * rnn/fc 512, up to 8 rows per launch, one row on each XCD's 32 CUs), the role-split kernel
+ * (one MoL row), the per-row latency kernel (rows in LDS, used while B <= max_rows) and the
+ * multi-row kernel (rows through HBM). */
 typedef struct {
     int32_t grid;            /* workgroups (all co-resident, one persistent launch) */
     int32_t units_rnn;       /* hidden units per workgroup (GRU rows ×3)            */
@@ -86,7 +87,8 @@ typedef struct {
                                                   the GRU weights are block-sparse, else 0 */
     int32_t split_grid;      /* batch-1 MoL role-split kernel: GRU + FC workgroups (0: unavailable) */
     int32_t last_path;       /* kernel of the last wrnn_generate: 1 latency, 2 multi-row,
-                                3 deepmind, 4 role-split (0: none yet) */
+                                3 deepmind, 4 role-split, 5 XCD-resident (0: none yet) */
+    int32_t xcd_rows;        /* XCD-resident kernel: rows per launch (0: unavailable)          */
 } wrnn_info;
 
 /* Create a handle on `device` (replaces WaveRNN.__init__ for the loop's dims,

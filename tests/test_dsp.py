@@ -41,3 +41,19 @@ def test_wav_round_trip(tmp_path):
     np.testing.assert_allclose(y, (pcm[:, 0] / 32768.0 + pcm[:, 1] / 32768.0) / 2, atol=1e-7)
     with pytest.raises(ValueError):
         dsp.load_wav(p, 16000)
+
+
+def test_wav_integer_pcm_scaling(tmp_path):
+    """uint8 PCM → (x − 128) / 128; int32 (and 24-bit, which scipy reads left-justified into
+    int32) → x / 2**31: librosa's full-scale conventions."""
+    from scipy.io import wavfile
+    u8 = np.array([0, 1, 64, 128, 200, 255], dtype=np.uint8)
+    wavfile.write(str(tmp_path / "u8.wav"), 22050, u8)
+    y = dsp.load_wav(tmp_path / "u8.wav", 22050)
+    assert y.dtype == np.float32
+    np.testing.assert_array_equal(y, (u8.astype(np.float32) - 128.0) / 128.0)
+    i32 = np.array([-2 ** 31, -1, 0, 1, 2 ** 30, 2 ** 31 - 1], dtype=np.int32)
+    wavfile.write(str(tmp_path / "i32.wav"), 22050, i32)
+    y = dsp.load_wav(tmp_path / "i32.wav", 22050)
+    np.testing.assert_array_equal(y, i32.astype(np.float32) / np.float32(2 ** 31))
+    assert y.min() == -1.0 and y.max() <= 1.0

@@ -265,6 +265,27 @@ def test_split_vs_reference_fixture(name, monkeypatch):
     assert err.max() <= gf.MOL_TOL, f"max |Δ| {err.max()} at {np.unravel_index(err.argmax(), err.shape)}"
 
 
+@pytest.mark.parametrize("reps", [1, 3, 16, 17, 32])
+def test_split_hand_off_replicas(reps, monkeypatch):
+    """Every replica count the launcher accepts (WRNN_REPLICAS, clamped to [1, 32]): each FC
+    workgroup polls replica w % reps, so every replica of every hop must be published (17..32
+    exercise the second publishing lane of the 16-lane engines)."""
+    from oracle import oracle
+    monkeypatch.setenv("WRNN_PATH", "split")
+    monkeypatch.setenv("WRNN_REPLICAS", str(reps))
+    d = syn.DEFAULT_MOL
+    L = 300
+    state = syn.make_fatchord_state(d, 61)
+    mels, aux = syn.make_conditioning(1, L, d.feat_dims, d.res_out_dims, 62)
+    noise = syn.make_noise("MOL", 1, L, d.n_classes, 63)
+    ref, _ = oracle.fatchord_loop(state, "MOL", mels, aux, noise)
+    loop = _split_loop(d)
+    loop.set_weights(state)
+    out, _ = loop.generate(_cond(mels, aux), noise=torch.from_numpy(noise).to(DEV))
+    assert loop.info["last_path"] == 4
+    assert np.abs(out.cpu().numpy() - ref).max() <= gf.MOL_TOL
+
+
 def test_split_is_the_batch1_default_and_carries_time_chunks(monkeypatch):
     """B = 1 MoL takes the role-split kernel by default; with a tiny terms budget the utterance
     runs as several launches that carry h1 / h2 / the GRU1 terms / GH2 / x across the

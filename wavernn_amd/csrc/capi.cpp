@@ -19,6 +19,7 @@
 #include "fatchord_rows.h"
 #include "deepmind_rows.h"
 #include "fatchord_split.h"
+#include "fatchord_xcd.h"
 
 namespace wrnn {
 hipError_t launch_ci_gemm(const float *cond, int CD, int Bt, int b0, int Bc, int t0, int L, const float *W, int ldw,
@@ -39,6 +40,9 @@ hipError_t launch_split(const SplitArgs &a, size_t lds_bytes, hipStream_t st);
 hipError_t prepare_split_kernel(int max_lds_bytes);
 hipError_t split_occupancy(int *blocks_per_cu, size_t lds_bytes);
 bool split_has_kernel(int R, int F);
+hipError_t launch_xcd(const XcdArgs &a, hipStream_t st);
+hipError_t prepare_xcd_kernel(int max_lds_bytes);
+hipError_t xcd_occupancy(int *blocks_per_cu);
 }  // namespace wrnn
 
 using namespace wrnn;
@@ -97,7 +101,7 @@ struct wrnn_ctx {
     // r* fields above while in use
     RowsPart g2{};
     rocblas_handle blas = nullptr;
-    int last_path = 0;                              // 1 = latency, 2 = rows, 3 = deepmind, 4 = split
+    int last_path = 0;                              // 1 = latency, 2 = rows, 3 = deepmind, 4 = split, 5 = xcd
     // deepmind_version (WRNN_MODE_DM): deepmind_rows.hip
     DmSlab ds{};
     int dmU = 0, dmUO = 0, dmUO2 = 0;
@@ -113,6 +117,13 @@ struct wrnn_ctx {
     SplitGruSlab sgs{};
     SplitFcSlab sfs{};
     float *d_sgslab = nullptr, *d_sfslab = nullptr, *d_sWt = nullptr;
+    // XCD-resident MoL kernel (rnn / fc 512): fatchord_xcd.hip
+    bool xcd_ok = false;
+    XcdSlab xs{};
+    float *d_xslab = nullptr, *d_xWt = nullptr, *d_xstate = nullptr;
+    size_t xstate_cap = 0;
+    unsigned long long *d_xgx = nullptr;
+    int *d_members = nullptr;
 };
 
 namespace {
@@ -707,6 +718,90 @@ void pack_split_terms_weights(const wrnn_ctx &h, std::vector<float> &Wt) {
         }
 }
 
+// ---- XCD-resident kernel (fatchord_xcd.h): workgroup c of an XCD owns units and fc rows
+// 16c..16c+15; wave w of it units / fc rows 16c + 2w + {0, 1}
+void make_xcd_slab(wrnn_ctx &h) {
+    const int R = h.cfg.rnn_dims;
+    int o = 0;
+    auto take = [&](int n) { int at = o; o += round4(n); return at; };
+    XcdSlab &x = h.xs;
+    x.wih2 = take(kXWaves * 6 * R);
+    x.w1 = take(kXWaves * 2 * R);
+    x.w2 = take(kXWaves * 2 * R);
+    x.whh2 = take(48 * R);
+    x.whh1 = take(48 * R);
+    x.w3 = take(kXWaves * 2 * 32);
+    x.q1a = take(3 * R);
+    x.cst = take(kXCst);
+    x.total = o;
+}
+
+void pack_xcd_slab(const wrnn_ctx &h, std::vector<float> &slab) {
+    const int R = h.cfg.rnn_dims, F = h.cfg.fc_dims, A = h.cfg.aux_dims, NC = h.cfg.n_classes;
+    auto W = [&](const char *n) { return h.w.at(n).data(); };
+    const float *IW = W("I.weight");
+    const int nin = 1 + h.cfg.feat_dims + A;
+    const XcdSlab &x = h.xs;
+    slab.assign((size_t)kXcdWgs * x.total, 0.0f);
+    std::vector<float> q1a(3 * R);
+    for (int r = 0; r < 3 * R; ++r) q1a[r] = xcol_dot(W("rnn1.weight_ih_l0") + (size_t)r * R, IW, nin, R);
+    for (int c = 0; c < kXcdWgs; ++c) {
+        float *out = slab.data() + (size_t)c * x.total;
+        std::memcpy(out + x.q1a, q1a.data(), (size_t)3 * R * 4);
+        for (int w = 0; w < kXWaves; ++w)
+            for (int i = 0; i < 2; ++i) {
+                const int u = 2 * w + i, j = c * kXUnits + u;     // unit j, fc row j
+                for (int q = 0; q < 3; ++q)
+                    std::memcpy(out + x.wih2 + (size_t)(w * 6 + 2 * q + i) * R,
+                                W("rnn2.weight_ih_l0") + (size_t)(q * R + j) * (R + A), R * 4);
+                std::memcpy(out + x.w1 + (size_t)(w * 2 + i) * R, W("fc1.weight") + (size_t)j * (R + A), R * 4);
+                std::memcpy(out + x.w2 + (size_t)(w * 2 + i) * R, W("fc2.weight") + (size_t)j * (F + A), F * 4);
+                for (int k = 0; k < NC; ++k) out[x.w3 + (w * 2 + i) * 32 + k] = W("fc3.weight")[(size_t)k * F + j];
+            }
+        for (int u = 0; u < kXUnits; ++u) {
+            const int j = c * kXUnits + u;
+            out[x.cst + XC_WI0 + u] = IW[(size_t)j * nin];
+            for (int q = 0; q < 3; ++q) {
+                const int src = q * R + j, rr = u * 3 + q;
+                std::memcpy(out + x.whh1 + (size_t)rr * R, W("rnn1.weight_hh_l0") + (size_t)src * R, R * 4);
+                std::memcpy(out + x.whh2 + (size_t)rr * R, W("rnn2.weight_hh_l0") + (size_t)src * R, R * 4);
+                out[x.cst + XC_Q2 + rr] = xcol_dot(W("rnn2.weight_ih_l0") + (size_t)src * (R + A), IW, nin, R);
+                out[x.cst + XC_BIH1 + rr] = W("rnn1.bias_ih_l0")[src];
+                out[x.cst + XC_BHH1 + rr] = W("rnn1.bias_hh_l0")[src];
+                out[x.cst + XC_BIH2 + rr] = W("rnn2.bias_ih_l0")[src];
+                out[x.cst + XC_BHH2 + rr] = W("rnn2.bias_hh_l0")[src];
+            }
+        }
+        for (int k = 0; k < NC; ++k) out[x.cst + XC_B3 + k] = W("fc3.bias")[k];
+    }
+}
+
+// Terms-GEMM weights [kXcdWgs·kXTerms][KX] against X = [cI | a2 a3 a4 | 1 0 0 0] (XTerm slots)
+void pack_xcd_terms_weights(const wrnn_ctx &h, std::vector<float> &Wt) {
+    const int R = h.cfg.rnn_dims, F = h.cfg.fc_dims, A = h.cfg.aux_dims, KX = h.KX;
+    auto W = [&](const char *n) { return h.w.at(n).data(); };
+    Wt.assign((size_t)kXcdWgs * kXTerms * KX, 0.0f);
+    for (int c = 0; c < kXcdWgs; ++c) {
+        auto row = [&](int slot) { return Wt.data() + ((size_t)c * kXTerms + slot) * KX; };
+        for (int u = 0; u < kXUnits; ++u) {
+            const int j = c * kXUnits + u;
+            for (int q = 0; q < 3; ++q) {
+                const int src = q * R + j;
+                std::memcpy(row(XT_P1 + u * 3 + q), W("rnn1.weight_ih_l0") + (size_t)src * R, R * 4);
+                const float *ih2 = W("rnn2.weight_ih_l0") + (size_t)src * (R + A);
+                std::memcpy(row(XT_P2 + u * 3 + q), ih2, R * 4);
+                std::memcpy(row(XT_P2 + u * 3 + q) + R, ih2 + R, A * 4);          // a2
+            }
+            row(XT_CI + u)[j] = 1.0f;                                            // cI_j itself
+            float *v1 = row(XT_V1 + u), *v2 = row(XT_V2 + u);
+            std::memcpy(v1 + R + A, W("fc1.weight") + (size_t)j * (R + A) + R, A * 4);       // a3
+            v1[R + 3 * A] = W("fc1.bias")[j];
+            std::memcpy(v2 + R + 2 * A, W("fc2.weight") + (size_t)j * (F + A) + F, A * 4);   // a4
+            v2[R + 3 * A] = W("fc2.bias")[j];
+        }
+    }
+}
+
 }  // namespace
 
 namespace {
@@ -1054,6 +1149,80 @@ int generate_split(wrnn_t *h, const float *cond, int B, int L, const float *nois
     return WRNN_OK;
 }
 
+// MoL rows through the XCD-resident kernel: up to 8 rows per launch (row k on XCD k), time
+// chunks sized so terms + GEMM input stay within WRNN_TERMS_MB (default 8192 MiB).  Each chunk's
+// terms cover one step past its end (step t publishes the GRU1 terms of t + 1); the recurrent
+// state is carried per workgroup in d_xstate.
+int generate_xcd(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed, int64_t row_offset,
+                 float *out, hipStream_t st) {
+    const wrnn_config &c = h->cfg;
+    const int R = c.rnn_dims, A = c.aux_dims, N = kXcdWgs * kXTerms;
+    if (!h->blas && rocblas_create_handle(&h->blas) != rocblas_status_success)
+        return fail(h, WRNN_EHIP, "rocblas_create_handle failed");
+    if (rocblas_set_stream(h->blas, st) != rocblas_status_success) return fail(h, WRNN_EHIP, "rocblas_set_stream failed");
+    const char *mb_env = std::getenv("WRNN_TERMS_MB");
+    const double budget = (mb_env ? std::atof(mb_env) : 8192.0) * (1 << 20) / 4.0;   // floats
+    const size_t xg_words = (size_t)kXcds * kXXcdStride;
+    if (!h->d_members) {
+        HIP_TRY(h, hipMalloc(&h->d_members, kXcds * sizeof(int)));
+        HIP_TRY(h, hipMalloc(&h->d_xgx, xg_words * 8));
+    }
+    const char *dbg_env = std::getenv("WRNN_DEBUG_STAMPS");
+    const int dbg_steps = dbg_env ? std::min(L, std::atoi(dbg_env)) : 0;
+    unsigned *d_dbg = nullptr;
+    int dbg_G = 0;
+    const float one = 1.0f, zero = 0.0f;
+    for (int b0 = 0; b0 < B; b0 += kXcds) {
+        const int nb = std::min(kXcds, B - b0);
+        const int Lc_max = (int)std::max(1.0, std::min((double)L, budget / ((double)nb * (N + h->KX)) - 1.0));
+        if (grow(h, h->d_X, h->X_cap, (size_t)(Lc_max + 1) * nb * h->KX) ||
+            grow(h, h->d_T, h->T_cap, (size_t)(Lc_max + 1) * nb * N) ||
+            grow(h, h->d_xstate, h->xstate_cap, (size_t)nb * kXcdWgs * kXStateW))
+            return WRNN_EHIP;
+        if (dbg_steps > 0 && !d_dbg) {
+            dbg_G = nb * kXcdWgs;
+            HIP_TRY(h, hipMalloc(&d_dbg, (size_t)dbg_G * dbg_steps * kStamps * 4));
+            HIP_TRY(h, hipMemsetAsync(d_dbg, 0, (size_t)dbg_G * dbg_steps * kStamps * 4, st));
+        }
+        HIP_TRY(h, hipMemsetAsync(h->d_xgx, 0, (size_t)nb * kXXcdStride * 8, st));   // tags restart at 1
+        for (int t0 = 0; t0 < L; t0 += Lc_max) {
+            const int Lc = std::min(Lc_max, L - t0);
+            const int rows = std::min(Lc + 1, L - t0);     // terms rows: steps [t0, t0 + rows)
+            HIP_TRY(h, launch_ci_gemm(cond, h->CD, B, b0, nb, t0, rows, h->d_IW, 1 + c.feat_dims + A, h->d_Ib, R,
+                                      c.feat_dims + A, h->d_X, h->KX, st));
+            HIP_TRY(h, launch_pack_terms_input(cond, h->CD, B, b0, nb, t0, rows, c.feat_dims, A, R, h->KX, h->d_X, st));
+            if (rocblas_sgemm(h->blas, rocblas_operation_transpose, rocblas_operation_none, N, rows * nb, h->KX, &one,
+                              h->d_xWt, h->KX, h->d_X, h->KX, &zero, h->d_T, N) != rocblas_status_success)
+                return fail(h, WRNN_EHIP, "rocblas_sgemm (conditioning terms) failed");
+            HIP_TRY(h, hipMemsetAsync(h->d_members, 0, kXcds * sizeof(int), st));
+            XcdArgs a{};
+            a.slab = h->d_xslab;
+            a.terms = h->d_T;
+            a.noise = noise;
+            a.out = out;
+            a.state = h->d_xstate;
+            a.xg = h->d_xgx;
+            a.members = h->d_members;
+            a.ctl = h->d_ctl;
+            a.seed = seed;
+            a.row0 = row_offset + b0;
+            a.timeout_ticks = h->timeout_ticks;
+            a.L = L;
+            a.t0 = t0;
+            a.Lc = Lc;
+            a.Bt = B;
+            a.b0 = b0;
+            a.nb = nb;
+            a.s = h->xs;
+            a.dbg = (b0 == 0 && t0 == 0) ? d_dbg : nullptr;
+            a.dbg_steps = std::min(dbg_steps, Lc);
+            HIP_TRY(h, launch_xcd(a, st));
+        }
+    }
+    if (d_dbg) return dump_stamps(h, d_dbg, dbg_steps, st, dbg_G);
+    return WRNN_OK;
+}
+
 int generate_latency(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed,
                      int64_t row_offset, float *out, int32_t *labels, hipStream_t st) {
     const wrnn_config &c = h->cfg;
@@ -1269,6 +1438,14 @@ int wrnn_create(const wrnn_config *cfg, int device, wrnn_t **out) {
             h->split_ok = per_cu >= 1;
         }
     }
+    // MoL rnn / fc 512: the XCD-resident kernel (one row per XCD) on a full 8 × 32-CU MI355X
+    if (mol && c.grid <= 0 && R == 512 && F == 512 && c.aux_dims == 32 && h->num_cus == kXcds * kXcdWgs &&
+        xcd_lds_layout().total * sizeof(float) <= (size_t)h->max_lds) {
+        make_xcd_slab(*h);
+        HIP_TRY(h, prepare_xcd_kernel(h->max_lds));
+        HIP_TRY(h, xcd_occupancy(&per_cu));
+        h->xcd_ok = per_cu >= 1;
+    }
     h->timeout_ticks = (long long)(c.timeout_ms > 0 ? c.timeout_ms : 2000) * 100000LL;   // 100 MHz
     HIP_TRY(h, hipMalloc(&h->d_ctl, kCtlWords * sizeof(int)));
     HIP_TRY(h, hipMemset(h->d_ctl, 0, kCtlWords * sizeof(int)));
@@ -1382,6 +1559,17 @@ int wrnn_set_weights(wrnn_t *h, const wrnn_tensor *tensors, int n) {
             HIP_TRY(h, hipMemcpy(*pr.first, pr.second->data(), pr.second->size() * 4, hipMemcpyHostToDevice));
         }
     }
+    if (h->xcd_ok) {
+        std::vector<float> slab, Wt;
+        pack_xcd_slab(*h, slab);
+        pack_xcd_terms_weights(*h, Wt);
+        for (auto pr : {std::make_pair(&h->d_xslab, &slab), std::make_pair(&h->d_xWt, &Wt)}) {
+            if (*pr.first) HIP_TRY(h, hipFree(*pr.first));
+            *pr.first = nullptr;
+            HIP_TRY(h, hipMalloc(pr.first, pr.second->size() * 4));
+            HIP_TRY(h, hipMemcpy(*pr.first, pr.second->data(), pr.second->size() * 4, hipMemcpyHostToDevice));
+        }
+    }
     h->ready = true;
     return WRNN_OK;
 }
@@ -1403,11 +1591,13 @@ int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise
     if (pe == "rows") rows = true;
     if (pe == "latency" && h->max_rows >= 1) rows = false;
     if (rows && !h->rows_ok) rows = false;
-    const bool split = h->split_ok && (pe == "split" || (pe.empty() && B == 1));
+    const bool xcd = h->xcd_ok && pe == "xcd";
+    const bool split = !xcd && h->split_ok && (pe == "split" || (pe.empty() && B == 1));
     HIP_TRY(h, hipMemsetAsync(h->d_ctl, 0, kCtlWords * sizeof(int), st));
     HIP_TRY(h, hipEventRecord(h->ev0, st));
-    h->last_path = h->dm ? 3 : split ? 4 : rows ? 2 : 1;
+    h->last_path = h->dm ? 3 : xcd ? 5 : split ? 4 : rows ? 2 : 1;
     const int rc = h->dm    ? generate_dm(h, B, L, noise, seed, row_offset, out, labels, st)
+                   : xcd   ? generate_xcd(h, cond, B, L, noise, seed, row_offset, out, st)
                    : split ? generate_split(h, cond, B, L, noise, seed, row_offset, out, st)
                    : rows  ? generate_rows(h, cond, B, L, noise, seed, row_offset, out, labels, st)
                            : generate_latency(h, cond, B, L, noise, seed, row_offset, out, labels, st);
@@ -1430,7 +1620,9 @@ int wrnn_check(wrnn_t *h, void *stream) {
         static const char *dm_hops[] = {"h_coarse", "o1", "coarse logits", "h_fine", "o3", "fine logits",
                                         "coarse label", "fine label"};
         static const char *split_hops[] = {"y", "f1", "f2", "h2", "h2", "gru1-terms", "gru1-terms"};
-        const char *name = h->last_path == 4   ? (hop >= 0 && hop < 7 ? split_hops[hop] : "?")
+        static const char *xcd_hops[] = {"y", "f1", "f2", "h2", "gru1-terms", "gru1-terms"};
+        const char *name = h->last_path == 5   ? (hop >= 0 && hop < 6 ? xcd_hops[hop] : "?")
+                           : h->last_path == 4 ? (hop >= 0 && hop < 7 ? split_hops[hop] : "?")
                            : h->last_path == 3 ? (hop >= 0 && hop < 8 ? dm_hops[hop] : "?")
                            : h->last_path == 2 ? (hop >= 0 && hop < 6 ? row_hops[hop] : "?")
                                                : (hop >= 0 && hop < 7 ? lat_hops[hop] : "?");
@@ -1480,6 +1672,7 @@ int wrnn_query(const wrnn_t *h, wrnn_info *info) {
     info->num_cus = h->num_cus;
     info->split_grid = h->split_ok ? h->sGg + h->sGf : 0;
     info->last_path = h->last_path;
+    info->xcd_rows = h->xcd_ok ? kXcds : 0;
     return WRNN_OK;
 }
 
@@ -1495,7 +1688,8 @@ void wrnn_destroy(wrnn_t *h) {
                     (void *)h->d_act, (void *)h->d_state, (void *)h->d_flags, (void *)h->d_xr, (void *)h->d_dmslab,
                     (void *)h->d_dmflags, (void *)h->d_dmxg, (void *)h->d_sgslab, (void *)h->d_sfslab,
                     (void *)h->d_sWt, (void *)h->g2.d_slab, (void *)h->g2.d_Wt, (void *)h->dm2.d_slab,
-                    (void *)h->d_gact})
+                    (void *)h->d_gact, (void *)h->d_xslab, (void *)h->d_xWt, (void *)h->d_xstate, (void *)h->d_xgx,
+                    (void *)h->d_members})
         if (p) (void)hipFree(p);
     if (h->blas) (void)rocblas_destroy_handle(h->blas);
     delete h;

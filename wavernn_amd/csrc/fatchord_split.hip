@@ -38,12 +38,28 @@ namespace wrnn {
 #define WRNN_OFF_SLEEP 32
 #endif
 constexpr int kOffSleep = WRNN_OFF_SLEEP;   // backoff (×64 cycles) of the off-critical polls
+static_assert(kOffSleep >= 0 && kOffSleep <= 127, "s_sleep takes a 7-bit count");
 // (same-box sweep, MI355X, us/step: 2 → 5.97, 12 → 5.89, 24 → 5.89, 32 → 5.83, 48 → 5.85;
 // fewer polls of the off-critical vectors leave the L2 channels to the critical hand-offs)
 #ifndef WRNN_DRAIN_PUB
 #define WRNN_DRAIN_PUB 1
 #endif
 constexpr bool kDrainPub = WRNN_DRAIN_PUB;
+#ifndef WRNN_SPLIT_PK
+#define WRNN_SPLIT_PK 1
+#endif
+constexpr bool kPk = WRNN_SPLIT_PK;          // critical dots as packed FMAs in 4 chains (row_dot_pk)
+#ifndef WRNN_SPLIT_PRE
+#define WRNN_SPLIT_PRE 1
+#endif
+constexpr bool kPre = WRNN_SPLIT_PRE;        // operands of the post-dot math read from LDS ahead
+
+// a critical-path 16-lane row dot over K floats
+template <int K>
+__device__ __forceinline__ float crit_dot(const float *__restrict__ w, const float *__restrict__ x, int li) {
+    if constexpr (kPk) return row_dot_pk<K / 4>(w, x, li);
+    else return row_dot(w, x, K / 4, li);
+}
 
 #define SSTAMP(k)                                                                                          \
     do {                                                                                                   \
@@ -124,6 +140,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_split_kernel(SplitArgs a) {
     static_assert(kPh >= 1 && (kPh & (kPh - 1)) == 0 && kPh <= 16, "logit gather layout");
     auto gather_logits = [&](uint32_t tag, int t) -> float {
         const int j = lane & 31, jj = j < NC ? j : 0;
+        const float b3 = S[a.gs.b3 + jj];
         const unsigned long long *gp = XG(SH_F2) + poll_off + (size_t)(lane >> 5) * kPh * kSplitLogitLine + jj;
         const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
         unsigned spins = 0;
@@ -159,7 +176,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_split_kernel(SplitArgs a) {
             for (int k = 0; k < n; ++k) p[k] += p[k + n];
         float s = p[0];
         s += __shfl_xor(s, 32);
-        return s + S[a.gs.b3 + jj];
+        return s + b3;
     };
 
     // ---- prologue: slab → LDS, state (zero, or carried from the previous time chunk), the
@@ -217,6 +234,22 @@ __global__ __launch_bounds__(kThreads) void fatchord_split_kernel(SplitArgs a) {
         const bool more = t + 1 < a.L;
         SSTAMP(0);
         if (gru) {
+            // GRU2's per-unit operands (all known before x): issued now, landed during GRU1
+            float pq2[3], pp2[3], pbi[3], pgh[3], pwi0 = 0.0f, pci = 0.0f, ph2 = 0.0f;
+            if (kPre && !loader) {
+                const int u = wave;
+                const float *tr = RING(t);
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    pq2[q] = S[a.gs.q2 + u * 3 + q];
+                    pp2[q] = tr[ST_P2 + u * 3 + q];
+                    pbi[q] = S[a.gs.bih2 + u * 3 + q];
+                    pgh[q] = gh2[(t & 1) * 12 + u * 3 + q] + S[a.gs.bhh2 + u * 3 + q];
+                }
+                pwi0 = S[a.gs.wi0 + u];
+                pci = tr[ST_CI + u];
+                ph2 = h2own[u];
+            }
             // ---- A: GRU1 (:208-210) for all units from the gathered terms
             if (!loader)
                 for (int j = tid; j < R; j += kCompute) {
@@ -233,18 +266,29 @@ __global__ __launch_bounds__(kThreads) void fatchord_split_kernel(SplitArgs a) {
             // ---- B: GRU2 (:213-214), wave u → unit u (gate rows on DPP rows 0..2)
             if (!loader) {
                 const int u = wave, j = g * kSplitUnits + u;
-                const float v = row_dot(S + a.gs.wih2 + (u * 3 + (row < 3 ? row : 0)) * R, va, R / 4, li);
+                const float v = crit_dot<R>(S + a.gs.wih2 + (u * 3 + (row < 3 ? row : 0)) * R, va, li);
                 const float *tr = RING(t);
                 float gi[3], gh[3];
+                if (!kPre) {
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) {
+                        pq2[q] = S[a.gs.q2 + u * 3 + q];
+                        pp2[q] = tr[ST_P2 + u * 3 + q];
+                        pbi[q] = S[a.gs.bih2 + u * 3 + q];
+                        pgh[q] = gh2[(t & 1) * 12 + u * 3 + q] + S[a.gs.bhh2 + u * 3 + q];
+                    }
+                    pwi0 = S[a.gs.wi0 + u];
+                    pci = tr[ST_CI + u];
+                    ph2 = h2own[u];
+                }
 #pragma unroll
                 for (int q = 0; q < 3; ++q) {
-                    gi[q] = (lane_bcast(v, 16 * q) + fmaf(x, S[a.gs.q2 + u * 3 + q], tr[ST_P2 + u * 3 + q])) +
-                            S[a.gs.bih2 + u * 3 + q];
-                    gh[q] = gh2[(t & 1) * 12 + u * 3 + q] + S[a.gs.bhh2 + u * 3 + q];
+                    gi[q] = (lane_bcast(v, 16 * q) + fmaf(x, pq2[q], pp2[q])) + pbi[q];
+                    gh[q] = pgh[q];
                 }
-                const float hn = gru_gate_math(gi[0], gi[1], gi[2], gh[0], gh[1], gh[2], h2own[u]);
+                const float hn = gru_gate_math(gi[0], gi[1], gi[2], gh[0], gh[1], gh[2], ph2);
                 // y = (x_I + h1) + h2 (:212, :216), x_I = cI + W_I[:, 0]·x
-                const float y = (fmaf(S[a.gs.wi0 + u], x, tr[ST_CI + u]) + va[j]) + hn;
+                const float y = (fmaf(pwi0, x, pci) + va[j]) + hn;
                 // y: one 128-B line per GRU workgroup (kYLine granules), so no two workgroups'
                 // sc1 stores share a line (4 producers per line cost the hop ~0.5 us)
                 if (lane < a.reps) publish(XG(SH_Y) + (size_t)lane * a.rep_stride + g * kYLine + u, tag, y);
@@ -302,6 +346,12 @@ __global__ __launch_bounds__(kThreads) void fatchord_split_kernel(SplitArgs a) {
             if (*abort_flag) return;
         } else {
             // ---- A': y (hop Y); the gathering wave first lets its f2 stores leave the CU
+            const int e = wave * 4 + row;                 // engine = fc row within the workgroup
+            float pv1 = 0.0f, pv2 = 0.0f;                 // fc1 / fc2 conditioning terms (+ biases)
+            if (kPre && !loader) {
+                pv1 = RING(t)[ST_V1 + e];
+                pv2 = RING(t)[ST_V2 + e];
+            }
             if (kDrainPub && wave == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (wave == 0)
                 gather_mapped<NG_R, kPollThreads>(XG(SH_Y) + poll_off, R, tag, a.ctl, a.timeout_ticks, t, SH_Y,
@@ -312,12 +362,12 @@ __global__ __launch_bounds__(kThreads) void fatchord_split_kernel(SplitArgs a) {
             SSTAMP(1);
             if (*abort_flag) return;
             if (loader) loader_top(t);
-            const int e = wave * 4 + row;                 // engine = fc row within the workgroup
             // ---- B': fc1 (:216-218), relu → hop F1
             if (!loader) {
-                const float v = row_dot(S + a.fs.w1 + e * R, va, R / 4, li) + RING(t)[ST_V1 + e];
-                if (li < a.reps)
-                    publish(XG(SH_F1) + (size_t)li * a.rep_stride + g * kSplitFcRows + e, tag, v > 0.0f ? v : 0.0f);
+                const float v = crit_dot<R>(S + a.fs.w1 + e * R, va, li) + (kPre ? pv1 : RING(t)[ST_V1 + e]);
+                // the 16 lanes of the engine publish replicas li, li + 16 (reps <= 32)
+                for (int r = li; r < a.reps; r += 16)
+                    publish(XG(SH_F1) + (size_t)r * a.rep_stride + g * kSplitFcRows + e, tag, v > 0.0f ? v : 0.0f);
                 if (dbg_on && tid == 0) stamp[(t & 1) * kStamps + 6] = (unsigned)__builtin_amdgcn_s_memrealtime();
             }
             if (kDrainPub && wave == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // f1 stores out first
@@ -329,7 +379,7 @@ __global__ __launch_bounds__(kThreads) void fatchord_split_kernel(SplitArgs a) {
             if (*abort_flag) return;
             // ---- C': fc2 (:220-221), relu → the own 16 rows of f2 (LDS)
             if (!loader) {
-                const float v = row_dot(S + a.fs.w2 + e * F, vb, F / 4, li) + RING(t)[ST_V2 + e];
+                const float v = crit_dot<F>(S + a.fs.w2 + e * F, vb, li) + (kPre ? pv2 : RING(t)[ST_V2 + e]);
                 if (li == 0) f2[e] = v > 0.0f ? v : 0.0f;
             }
             if (loader) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

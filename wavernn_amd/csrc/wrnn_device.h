@@ -262,6 +262,27 @@ __device__ __forceinline__ float row_dot(const float *__restrict__ w, const floa
     return row_sum16(acc);
 }
 
+// row_dot on the critical path: packed fp32 FMAs (v_pk_fma_f32 on the aligned float4 halves)
+// into four independent accumulators (even/odd chunk × xy/zw), so the per-lane chain is K4/32
+// dependent packed FMAs instead of K4/4 dependent scalar ones.  Compile-time K4.
+template <int K4>
+__device__ __forceinline__ float row_dot_pk(const float *__restrict__ w, const float *__restrict__ x, int li) {
+    static_assert(K4 % 32 == 0, "row_dot_pk: two chunks per lane per pass");
+    const f4v *w4 = reinterpret_cast<const f4v *>(w) + li;
+    const f4v *x4 = reinterpret_cast<const f4v *>(x) + li;
+    f2v a0 = {0.0f, 0.0f}, a1 = {0.0f, 0.0f}, a2 = {0.0f, 0.0f}, a3 = {0.0f, 0.0f};
+#pragma unroll
+    for (int k = 0; k < K4 / 16; k += 2) {
+        const f4v wa = w4[16 * k], xa = x4[16 * k], wb = w4[16 * (k + 1)], xb = x4[16 * (k + 1)];
+        a0 = __builtin_elementwise_fma(wa.xy, xa.xy, a0);
+        a1 = __builtin_elementwise_fma(wa.zw, xa.zw, a1);
+        a2 = __builtin_elementwise_fma(wb.xy, xb.xy, a2);
+        a3 = __builtin_elementwise_fma(wb.zw, xb.zw, a3);
+    }
+    const f2v s = (a0 + a1) + (a2 + a3);
+    return row_sum16(s.x + s.y);
+}
+
 // Two rows against one x in a single pass (ILP for the 30-row MoL head).
 __device__ __forceinline__ float2 row_dot2(const float *__restrict__ w0, const float *__restrict__ w1,
                                           const float *__restrict__ x, int K4, int li) {

@@ -5,7 +5,9 @@
 
 Mel input is a normalised (n_mels, n_hops) .npy in [0, 1] (checked like gen_wavernn.py:48-57).
 The test-set mode and wav input need the training data pipeline / librosa feature
-extraction, which are out of scope; they raise.
+extraction, which are out of scope; they raise.  (wavernn_amd.dsp
+.load_wav reads wavs for other callers, but unlike the reference's librosa.load it does not
+resample: a file at another rate than hp.sample_rate raises.)
 """
 from __future__ import annotations
 
