@@ -10,8 +10,13 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from oracle import oracle  # noqa: E402
+from wavernn_amd import _native  # noqa: E402
 from wavernn_amd import synthetic as syn  # noqa: E402
 from wavernn_amd.loop import FatchordLoop  # noqa: E402
+
+
+if os.environ.get("TIME_DM_LIB"):   # A/B of two builds of the library (diagnostics only)
+    _native.LIB_PATH = os.environ["TIME_DM_LIB"]
 
 
 def cond_of(mels, aux):
@@ -28,10 +33,15 @@ def main(L=20000):
         noise = syn.make_noise("MOL", B, Lp, d.n_classes, 9)
         ref, _ = oracle.fatchord_loop(state, "MOL", mels, aux, noise)
         os.environ["WRNN_PATH"] = "xcd"
+        os.environ.pop("WRNN_TERMS_MB", None)
         if chunk:
             os.environ["WRNN_TERMS_MB"] = chunk
         loop.set_weights(state)
-        out, _ = loop.generate(cond_of(mels, aux), noise=torch.from_numpy(noise).cuda())
+        try:
+            out, _ = loop.generate(cond_of(mels, aux), noise=torch.from_numpy(noise).cuda())
+        except Exception as e:   # a diagnostic build may abort; keep timing it
+            print(f"xcd parity B={B} L={Lp}: {e}", flush=True)
+            continue
         os.environ.pop("WRNN_TERMS_MB", None)
         err = np.abs(out.cpu().numpy() - ref)
         print(f"xcd parity B={B} L={Lp} chunked={bool(chunk)}: path {loop.info['last_path']} max|d| {err.max():.3g} "

@@ -1,0 +1,48 @@
+"""Per-stage timeline of the XCD-resident kernel (fatchord_xcd.hip) from its WRNN_DEBUG_STAMPS
+(s_memrealtime, 100 MHz, wave 0 of every workgroup).  For each step, times are relative to the
+earliest step start over the XCD's 32 workgroups; the table gives the median over steps of the
+min / median / max over the workgroups.
+    python tools/stamps_xcd.py [L]"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from wavernn_amd import synthetic as syn  # noqa: E402
+from wavernn_amd.loop import FatchordLoop  # noqa: E402
+
+STAMPS = [(0, "start (after B1)"), (1, "GRU1 done (after B2)"), (2, "Y published (GRU2)"), (3, "Y gathered"),
+          (4, "f1 published"), (5, "F1 gathered"), (6, "partials in LDS (after B5)"), (7, "F2 gathered"),
+          (8, "sample done"), (9, "w1: GH1 terms published"), (14, "w3: after B3"), (10, "w6: h2 gathered"),
+          (13, "w3: GH2 done"), (11, "w5: S terms gathered"), (12, "w7: ring done")]
+
+
+def main(L=3000):
+    os.makedirs("gpurun_out", exist_ok=True)
+    path = "gpurun_out/stamps_xcd.bin"
+    os.environ["WRNN_DEBUG_STAMPS"] = str(L)
+    os.environ["WRNN_DEBUG_FILE"] = path
+    os.environ["WRNN_PATH"] = "xcd"
+    d = syn.DEFAULT_MOL
+    loop = FatchordLoop(d.mode, d.rnn_dims, d.fc_dims, d.aux_dims, d.feat_dims, d.n_classes)
+    loop.set_weights(syn.make_fatchord_state(d, 0))
+    mels, aux = syn.make_conditioning(1, L, d.feat_dims, d.res_out_dims, 5)
+    cond = torch.from_numpy(np.concatenate([mels, aux], 2).transpose(1, 0, 2).copy()).cuda()
+    loop.generate(cond, seed=1)
+    raw = np.fromfile(path, dtype=np.uint32)
+    G, S, K = raw[:3].view(np.int32)
+    st = raw[3:].reshape(G, S, K).astype(np.int64)[:32, 200:S - 2]
+    t0 = st[:, :, 0].min(axis=0)
+    rel = (st - t0[None, :, None]) * 10e-3
+    period = np.diff(t0) * 10e-3
+    print(f"xcd kernel L={L}: step period median {np.median(period):.3f} us (stamped build)")
+    print("-- median over steps of (min / median / max over the 32 workgroups), us")
+    for k, lab in STAMPS:
+        x = rel[:, :, k]
+        print(f"   {lab:28s} {np.median(x.min(0)):6.2f} {np.median(np.median(x, 0)):6.2f} {np.median(x.max(0)):6.2f}")
+
+
+if __name__ == "__main__":
+    main(*(int(a) for a in sys.argv[1:]))

@@ -42,7 +42,10 @@ __device__ __forceinline__ float wave_max(float v) {
 
 // (value, index) argmax: larger value wins, ties go to the smaller index (torch: first max).
 __device__ __forceinline__ void am_merge(float &v, int &i, float ov, int oi) {
-    if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }
+    // branch-free (bitwise, not short-circuit): hipcc otherwise emits exec-mask branches per stage
+    const bool take = (ov > v) | ((ov == v) & (oi < i));
+    v = take ? ov : v;
+    i = take ? oi : i;
 }
 
 __device__ __forceinline__ int wave_argmax(float v, int i) {
