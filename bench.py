@@ -205,7 +205,9 @@ def main():
                             f"{'fold-batched target 11000/overlap 550' if args.batched else 'unbatched (batch=1)'}",
                 "mode": args.mode, "rnn_dims": d.rnn_dims, "fc_dims": d.fc_dims, "utterance_s": args.seconds,
                 "loop_steps": L, "rows": B, "samples_per_utterance": int(n_samples / args.steps),
-                "parallelism": f"utterance-sharded x{world}", "grid": info["grid"],
+                "parallelism": f"utterance-sharded x{world}",
+                "kernel": {5: "fatchord_xcd_kernel (one XCD, 32 CUs)", 4: "fatchord_split_kernel", 2: "fatchord_rows_kernel",
+                           1: "fatchord_loop_kernel"}.get(info["last_path"], str(info["last_path"])),
             },
             "rtf_per_gpu": value / world / d.sample_rate,
             "loop_kernel_ms": loop_ms_max,
@@ -215,9 +217,10 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": pmc_traffic_bytes(args.mode, args.batched, args.seconds),
                 "note": "achieved = algorithmic bytes (all loop weights fp32 per step + 836 B/row-step) per launch "
-                        "/ launch time (HIP events); weights are LDS-resident, the kernel is hand-off-latency bound. "
+                        "/ launch time (HIP events); the weights are LDS/VGPR-resident on one XCD's 32 CUs "
+                        "(fatchord_xcd_kernel), the kernel is hand-off-latency bound. "
                         f"traffic = FETCH_SIZE+WRITE_SIZE bytes per launch from profiles/{os.path.basename(PMC_PROFILE)}: "
-                        "granule polling/publishing, not weight streaming",
+                        "conditioning-terms reads; the hand-offs stay in the XCD's L2",
             },
         }
         if not args.batched and args.mode == "MOL":
@@ -235,8 +238,9 @@ def main():
                 "samples_per_s": outb.shape[0] / dtb, "rtf": outb.shape[0] / dtb / d.sample_rate,
                 "rows": int(condb.shape[1]), "loop_steps": int(condb.shape[0]), "device_ms": kb,
                 "us_per_loop_step": kb * 1e3 / condb.shape[0],
+                "kernel_path": model.loop_handle().info["last_path"],
                 "note": "same 5 s utterance, generate(batched=True) as gen_wavernn.py runs it with the 800k "
-                        "hparams; one multi-row persistent launch (fatchord_rows.hip) + conditioning-terms GEMM",
+                        "hparams (10 folds: XCD-resident kernel, 8 + 2 rows in two launches) + conditioning-terms GEMM",
             }
         if args.other_configs and world == 1 and args.mode == "MOL":
             rec["other_configs"] = other_configs(dev)

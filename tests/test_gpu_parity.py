@@ -286,12 +286,13 @@ def test_split_hand_off_replicas(reps, monkeypatch):
     assert np.abs(out.cpu().numpy() - ref).max() <= gf.MOL_TOL
 
 
-def test_split_is_the_batch1_default_and_carries_time_chunks(monkeypatch):
-    """B = 1 MoL takes the role-split kernel by default; with a tiny terms budget the utterance
-    runs as several launches that carry h1 / h2 / the GRU1 terms / GH2 / x across the
-    boundaries: oracle parity, and Philox output identical to the single-launch run."""
+def test_split_carries_time_chunks(monkeypatch):
+    """The role-split kernel (forced; B = 1 MoL defaults to the XCD-resident kernel) with a tiny
+    terms budget runs the utterance as several launches that carry h1 / h2 / the GRU1 terms /
+    GH2 / x across the boundaries: oracle parity, and Philox output identical to the
+    single-launch run."""
     from oracle import oracle
-    monkeypatch.delenv("WRNN_PATH", raising=False)
+    monkeypatch.setenv("WRNN_PATH", "split")
     d = syn.DEFAULT_MOL
     L = 1500
     state = syn.make_fatchord_state(d, 71)

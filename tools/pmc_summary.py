@@ -3,7 +3,7 @@
     python tools/pmc_summary.py gpurun_out profiles/r01_v4_pmc_traffic.json
 
 Takes, per counter, the dispatch of the headline's persistent loop kernel (the longest
-fatchord_split_kernel / fatchord_loop_kernel dispatch in that pass) and stores its value (KiB per dispatch, as rocprofv3 reports these
+fatchord_xcd_kernel / fatchord_split_kernel / fatchord_loop_kernel dispatch in that pass) and stores its value (KiB per dispatch, as rocprofv3 reports these
 derived counters) and duration; bench.py reads the sum as `roofline.traffic`."""
 import csv
 import json
@@ -14,7 +14,7 @@ def loop_dispatch(path):
     best = None
     with open(path) as f:
         for r in csv.DictReader(f):
-            if "fatchord_split_kernel" not in r["Kernel_Name"] and "fatchord_loop_kernel" not in r["Kernel_Name"]:
+            if not any(k in r["Kernel_Name"] for k in ("fatchord_xcd_kernel", "fatchord_split_kernel", "fatchord_loop_kernel")):
                 continue
             dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
             if best is None or dur > best[2]:
@@ -31,8 +31,9 @@ def main(src, dst):
         "workload": "MOL rnn512 B=1 5 s (110275 steps), one persistent launch",
         "counters": counters,
         "note": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (bench.py --steps 1). "
-                "Units KiB per dispatch. Accesses are 8-byte sc1 granule polls/stores (uncalibrated width per "
-                "MI355X_MICROARCH.md; no 2x correction applied) plus 16-B LDS-DMA of the 2.4 KB/step record.",
+                "Units KiB per dispatch (no width correction applied: the XCD kernel's hand-offs are plain "
+                "8-byte stores and 16-byte sc1 polls served by the XCD's L2, its HBM traffic is the 16-byte "
+                "reads of the 640 B/step/workgroup conditioning terms).",
     }
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)

@@ -1574,6 +1574,8 @@ int wrnn_set_weights(wrnn_t *h, const wrnn_tensor *tensors, int n) {
     return WRNN_OK;
 }
 
+constexpr int kXcdDefaultRows = 48;
+
 int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed,
                   int64_t row_offset, float *out, int32_t *labels, void *stream) {
     if (!h) return WRNN_EINVAL;
@@ -1582,16 +1584,19 @@ int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise
     if (labels && h->cfg.mode == WRNN_MODE_MOL) return fail(h, WRNN_EINVAL, "labels are a RAW / DM output");
     HIP_TRY(h, hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
-    // path: one MoL row → the role-split kernel; otherwise the latency kernel while the rows
-    // fit its LDS layout in one launch, else the multi-row kernel.  WRNN_PATH=split|latency|rows
-    // forces one (tests, benchmarks)
+    // path: MoL rnn / fc 512 with few rows → the XCD-resident kernel; else one MoL row → the
+    // role-split kernel; otherwise the latency kernel while the rows fit its LDS layout in one
+    // launch, else the multi-row kernel.  WRNN_PATH=xcd|split|latency|rows forces one (tests,
+    // benchmarks)
     const char *path_env = std::getenv("WRNN_PATH");
     const std::string pe = path_env ? path_env : "";
     bool rows = h->max_rows < 1 || B > h->max_rows;
     if (pe == "rows") rows = true;
     if (pe == "latency" && h->max_rows >= 1) rows = false;
     if (rows && !h->rows_ok) rows = false;
-    const bool xcd = h->xcd_ok && pe == "xcd";
+    // MoL rnn / fc 512 up to kXcdDefaultRows rows: the XCD-resident kernel (8 rows per launch;
+    // beyond that the multi-row kernel's throughput wins)
+    const bool xcd = h->xcd_ok && (pe == "xcd" || (pe.empty() && B <= kXcdDefaultRows));
     const bool split = !xcd && h->split_ok && (pe == "split" || (pe.empty() && B == 1));
     HIP_TRY(h, hipMemsetAsync(h->d_ctl, 0, kCtlWords * sizeof(int), st));
     HIP_TRY(h, hipEventRecord(h->ev0, st));
