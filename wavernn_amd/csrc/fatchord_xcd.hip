@@ -44,6 +44,12 @@ namespace wrnn {
 #ifndef WRNN_XCD_SKIP_H2
 #define WRNN_XCD_SKIP_H2 0
 #endif
+#ifndef WRNN_XCD_FAST_EXP
+#define WRNN_XCD_FAST_EXP 1     // sampler scale e^s by v_exp_f32 (A/B vs libm expf: 3.92 -> 3.88 us/step, parity unchanged)
+#endif
+#ifndef WRNN_XCD_PRIO
+#define WRNN_XCD_PRIO 0         // s_setprio of wave 0 (the poller / sampler)
+#endif
 
 __device__ __forceinline__ unsigned xcc_id() {
     return __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 0xF;   // HW_REG_XCC_ID[3:0]
@@ -88,11 +94,15 @@ __device__ __forceinline__ float mol_sample_pairs(float la, float lb, float ua, 
     WRNN_AM_STAGE(0xB1) WRNN_AM_STAGE(0x4E) WRNN_AM_STAGE(0x141) WRNN_AM_STAGE(0x140)
 #undef WRNN_AM_STAGE
     const int k = __builtin_amdgcn_readlane(i, 0);
-    const int km = 10 + k, ks = 20 + k;
-    const float mean = (km & 1) ? lane_bcast(lb, km >> 1) : lane_bcast(la, km >> 1);
-    const float lsr = (ks & 1) ? lane_bcast(lb, ks >> 1) : lane_bcast(la, ks >> 1);
-    const float ls = fmaxf(lsr, -32.23619130191664f);
+    const int km = (10 + k) >> 1, ks = (20 + k) >> 1;     // lanes of logits 10 + k, 20 + k (same parity as k)
+    const float ma = lane_bcast(la, km), mb = lane_bcast(lb, km), sa = lane_bcast(la, ks), sb = lane_bcast(lb, ks);
+    const float mean = (k & 1) ? mb : ma;
+    const float ls = fmaxf((k & 1) ? sb : sa, -32.23619130191664f);
+#if WRNN_XCD_FAST_EXP
+    float x = mean + fast_exp(ls) * u10;
+#else
     float x = mean + expf(ls) * u10;
+#endif
     x = x < -1.0f ? -1.0f : x;
     x = x > 1.0f ? 1.0f : x;
     return x;
@@ -346,6 +356,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
     __syncthreads();
     if (*abort_flag) return;
 
+    if (WRNN_XCD_PRIO && wave == 0) __builtin_amdgcn_s_setprio(WRNN_XCD_PRIO);
     float x = xs[(a.t0 + 1) & 1];                    // x_{t-1}, wave-uniform
     f4v s4 = lds4(sg + 4 * tid);                     // GRU1 terms of unit tid for step t
     for (int t = a.t0; t < t_end; ++t) {
