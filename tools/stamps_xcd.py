@@ -37,7 +37,9 @@ def main(L=3000):
     t0 = st[:, :, 0].min(axis=0)
     rel = (st - t0[None, :, None]) * 10e-3
     period = np.diff(t0) * 10e-3
-    print(f"xcd kernel L={L}: step period median {np.median(period):.3f} us (stamped build)")
+    clk = (st[:, -1, 15] - st[:, 0, 15]) % (1 << 32) / ((st[:, -1, 0] - st[:, 0, 0]) * 10e-9) / 1e9
+    print(f"xcd kernel L={L}: step period median {np.median(period):.3f} us (stamped build), "
+          f"shader clock {np.median(clk):.3f} GHz (s_memtime / s_memrealtime)")
     print("-- median over steps of (min / median / max over the 32 workgroups), us")
     for k, lab in STAMPS:
         x = rel[:, :, k]

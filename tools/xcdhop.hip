@@ -4,18 +4,27 @@
 //   LOCAL: the 32 workgroups of ONE XCD (membership from HW_REG_XCC_ID + an arrival counter),
 //          plain stores (the line stays in that XCD's L2) + sc1 polls (L2-served);
 //   SPREAD: blocks 0..31 (four per XCD under round-robin dealing), sc1 stores + sc1 polls.
+// Poll variants (LOCAL): 8-byte loads (8 per lane) or 16-byte buffer loads (4 per lane), one or
+// two poll rounds in flight, with or without draining the own publish first, with or without
+// the other waves of the workgroup streaming LDS (the XCD kernel's off-critical dots).
 //   hipcc --offload-arch=gfx950 -O3 tools/xcdhop.hip -o tools/xcdhop && tools/xcdhop
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 
 constexpr int kN = 32, kLine = 16;
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
 
 __device__ inline unsigned xcc_id() { return __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 0xF; }
 
-template <bool LOCAL>
-__global__ __launch_bounds__(256) void hops(unsigned long long *vec, int *ctr, int nhops, unsigned long long *out) {
+__device__ __forceinline__ u4v ld16(__amdgpu_buffer_rsrc_t r, int off) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16 /* sc1 */);
+}
+
+template <bool LOCAL, int W16, int INFL, bool DRAIN, bool LDSLOAD>
+__global__ __launch_bounds__(512) void hops(unsigned long long *vec, int *ctr, int nhops, unsigned long long *out) {
     __shared__ int s_idx;
+    __shared__ float lds[8192];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (threadIdx.x == 0) {
         int idx = -1;
@@ -26,9 +35,22 @@ __global__ __launch_bounds__(256) void hops(unsigned long long *vec, int *ctr, i
         }
         s_idx = idx < kN ? idx : -1;
     }
+    for (int i = threadIdx.x; i < 8192; i += 512) lds[i] = (float)i;
     __syncthreads();
     const int me = s_idx;
-    if (me < 0 || wave != 0) return;
+    if (me < 0) return;
+    if (wave != 0) {   // background: LDS streaming by the other waves (until wave 0 is done)
+        if (!LDSLOAD) return;
+        float acc = 0.0f;
+        volatile int *flag = reinterpret_cast<volatile int *>(&s_idx);
+        for (int it = 0; ; ++it) {
+#pragma unroll 4
+            for (int k = 0; k < 16; ++k) acc += lds[(lane * 4 + k * 256 + it) & 8191];
+            if ((it & 63) == 0 && *flag < 0) break;
+        }
+        if (acc == 12345.0f) out[40] = 1;
+        return;
+    }
     const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + 200000000ull;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     bool dead = false;
@@ -39,42 +61,70 @@ __global__ __launch_bounds__(256) void hops(unsigned long long *vec, int *ctr, i
             if (LOCAL) __hip_atomic_store(v + me * kLine + lane, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             else __hip_atomic_store(v + me * kLine + lane, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        for (;;) {
-            unsigned long long x[8];
+        if (DRAIN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (W16) {
+            const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(v, 0, 0x7fffffff, 0x00020000);
+            auto check = [&](const u4v (&x)[4]) {
+                bool ok = true;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) x[k] = __hip_atomic_load(v + lane + 64 * k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            bool ok = true;
+                for (int k = 0; k < 4; ++k) ok &= (x[k].y == (unsigned)h) & (x[k].w == (unsigned)h);
+                return __all(ok);
+            };
+            u4v a[4], b[4];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) ok &= (unsigned)(x[k] >> 32) == (unsigned)h;
-            if (__all(ok)) break;
-            if (__builtin_amdgcn_s_memrealtime() > deadline) { dead = true; break; }
+            for (int k = 0; k < 4; ++k) a[k] = ld16(r, 16 * (lane + 64 * k));
+            for (;;) {
+                if (INFL == 2) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) b[k] = ld16(r, 16 * (lane + 64 * k));
+                }
+                if (check(a)) break;
+                if (INFL == 2) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) a[k] = ld16(r, 16 * (lane + 64 * k));
+                    if (check(b)) break;
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) a[k] = ld16(r, 16 * (lane + 64 * k));
+                }
+                if (__builtin_amdgcn_s_memrealtime() > deadline) { dead = true; break; }
+            }
+        } else {
+            for (;;) {
+                unsigned long long x[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) x[k] = __hip_atomic_load(v + lane + 64 * k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                bool ok = true;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) ok &= (unsigned)(x[k] >> 32) == (unsigned)h;
+                if (__all(ok)) break;
+                if (__builtin_amdgcn_s_memrealtime() > deadline) { dead = true; break; }
+            }
         }
     }
     if (lane == 0) {
         out[me] = dead ? ~0ull : __builtin_amdgcn_s_memrealtime() - t0;
+        s_idx = -1;    // stop the background waves
     }
 }
 
-template <bool LOCAL>
-void run(unsigned long long *vec, int *ctr, unsigned long long *out) {
+template <bool LOCAL, int W16, int INFL, bool DRAIN, bool LDSLOAD>
+void run(unsigned long long *vec, int *ctr, unsigned long long *out, const char *name) {
     const int nhops = 20000;
     hipMemset(vec, 0, 2 * kN * kLine * 8 + 4096);
     hipMemset(ctr, 0, 4);
     hipMemset(out, 0, kN * 8);
-    hipLaunchKernelGGL((hops<LOCAL>), dim3(256), dim3(256), 0, 0, vec, ctr, nhops, out);
+    hipLaunchKernelGGL((hops<LOCAL, W16, INFL, DRAIN, LDSLOAD>), dim3(256), dim3(512), 0, 0, vec, ctr, nhops, out);
     hipDeviceSynchronize();
     unsigned long long h[kN];
-    int c = 0;
     hipMemcpy(h, out, kN * 8, hipMemcpyDeviceToHost);
-    hipMemcpy(&c, ctr, 4, hipMemcpyDeviceToHost);
     unsigned long long mx = 0;
     bool dead = false;
     for (int i = 0; i < kN; ++i) {
         if (h[i] == ~0ull) dead = true;
         else if (h[i] > mx) mx = h[i];
     }
-    printf("%-6s (xcc0 arrivals %d): %s %.3f us per all-gather hop\n", LOCAL ? "LOCAL" : "SPREAD", c,
-           dead ? "TIMEOUT" : "", mx * 10e-3 / nhops);
+    printf("%-40s %s %.3f us per all-gather hop\n", name, dead ? "TIMEOUT" : "", mx * 10e-3 / nhops);
     fflush(stdout);
 }
 
@@ -82,11 +132,16 @@ int main() {
     unsigned long long *vec, *out;
     int *ctr;
     hipMalloc(&vec, 1 << 20);
-    hipMalloc(&out, kN * 8);
+    hipMalloc(&out, 64 * 8);
     hipMalloc(&ctr, 64);
     for (int r = 0; r < 2; ++r) {
-        run<true>(vec, ctr, out);
-        run<false>(vec, ctr, out);
+        run<true, 0, 1, false, false>(vec, ctr, out, "LOCAL 8B x8");
+        run<true, 0, 1, true, false>(vec, ctr, out, "LOCAL 8B x8 drain");
+        run<true, 1, 1, false, false>(vec, ctr, out, "LOCAL 16B x4");
+        run<true, 1, 1, true, false>(vec, ctr, out, "LOCAL 16B x4 drain");
+        run<true, 1, 2, true, false>(vec, ctr, out, "LOCAL 16B x4 drain, 2 rounds in flight");
+        run<true, 1, 1, true, true>(vec, ctr, out, "LOCAL 16B x4 drain, LDS-streaming waves");
+        run<false, 0, 1, false, false>(vec, ctr, out, "SPREAD 8B x8 (sc1 stores)");
     }
     return 0;
 }

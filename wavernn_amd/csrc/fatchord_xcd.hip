@@ -364,6 +364,19 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
         const bool more = t + 1 < a.L;
         const float *tr = RING(t);
         XSTAMP(0);
+        if (kDbg && a.dbg && wave == 0 && lane == 0 && t - a.t0 < a.dbg_steps)   // shader clock beside the 100 MHz one
+            a.dbg[((size_t)mem * a.dbg_steps + (t - a.t0)) * kStamps + 15] = (unsigned)__builtin_amdgcn_s_memtime();
+        // operands of the GRU2 gate math (engine unit ui): LDS reads issued before GRU1's
+        // transcendental chain (behind its h1 store the compiler could not move them)
+        float q2v[3], p2v[3], bi2[3], ghv[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            q2v[q] = cst[XC_Q2 + ui * 3 + q];
+            p2v[q] = tr[XT_P2 + ui * 3 + q];
+            bi2[q] = cst[XC_BIH2 + ui * 3 + q];
+            ghv[q] = gh2s[ui * 3 + q] + cst[XC_BHH2 + ui * 3 + q];
+        }
+        const float wi0v = cst[XC_WI0 + ui], civ = tr[XT_CI + ui];
         // ---- GRU1 (:208-210), unit tid
         {
             const float r = sigmoid_(fmaf(x, q1r, s4.x));
@@ -372,14 +385,10 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
             h1v = (h1v - n) * z + n;
             h1s[tid] = h1v;
         }
-        // operands of the GRU2 gate math (engine unit ui), issued before the barrier
-        float p2q[3], ghv[3];
+        float p2q[3];
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            p2q[q] = fmaf(x, cst[XC_Q2 + ui * 3 + q], tr[XT_P2 + ui * 3 + q]) + cst[XC_BIH2 + ui * 3 + q];
-            ghv[q] = gh2s[ui * 3 + q] + cst[XC_BHH2 + ui * 3 + q];
-        }
-        const float xi = fmaf(cst[XC_WI0 + ui], x, tr[XT_CI + ui]);   // x_I of unit ui
+        for (int q = 0; q < 3; ++q) p2q[q] = fmaf(x, q2v[q], p2v[q]) + bi2[q];
+        const float xi = fmaf(wi0v, x, civ);   // x_I of unit ui
         bar();
         XSTAMP(1);
         // ---- GRU2 (:212-214): pass q → gate q of unit ui (W_ih2[:, :R]·h1), all lanes of the engine
