@@ -128,13 +128,93 @@ void run(unsigned long long *vec, int *ctr, unsigned long long *out, const char 
     fflush(stdout);
 }
 
+
+// Barrier-paced variant (the XCD kernel's Y hop): per hop, __syncthreads, then PUBW waves publish
+// the workgroup's 16 granules (16 / PUBW each, by lanes 0.. of the wave), POLLW waves poll the
+// whole vector (16-byte loads, 4 per lane), XPOLL: wave 7 also publishes + polls a second vector
+// of the same shape (the h2 hand-off), then __syncthreads.
+template <int PUBW, int POLLW, bool XPOLL, int NBAR = 2>
+__global__ __launch_bounds__(512) void hops_paced(unsigned long long *vec, int *ctr, int nhops, unsigned long long *out) {
+    __shared__ int s_idx;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x == 0) {
+        int idx = -1;
+        if (xcc_id() == 0) idx = atomicAdd(ctr, 1);
+        s_idx = idx < kN ? idx : -1;
+    }
+    __syncthreads();
+    const int me = s_idx;
+    if (me < 0) return;
+    const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + 200000000ull;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    bool dead = false;
+    for (int h = 1; h <= nhops; ++h) {
+        __syncthreads();
+        unsigned long long *v = vec + (size_t)(h & 1) * kN * kLine;
+        unsigned long long *v2 = vec + 4096 + (size_t)(h & 1) * kN * kLine;
+        constexpr int per = kLine / PUBW;
+        if (wave < PUBW && lane < per) {
+            const int i = me * kLine + wave * per + lane;
+            __hip_atomic_store(v + i, ((unsigned long long)h << 32) | (unsigned)i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if (XPOLL && wave < PUBW && lane >= 32 && lane - 32 < per) {
+            const int i = me * kLine + wave * per + lane - 32;
+            __hip_atomic_store(v2 + i, ((unsigned long long)h << 32) | (unsigned)i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        const bool poller = (wave >= 1 && wave <= POLLW) || (XPOLL && wave == 7);
+        if (poller) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(wave == 7 ? v2 : v, 0, 0x7fffffff, 0x00020000);
+            for (;;) {
+                u4v a[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) a[k] = ld16(r, 16 * (lane + 64 * k));
+                bool ok = true;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) ok &= (a[k].y == (unsigned)h) & (a[k].w == (unsigned)h);
+                if (__all(ok)) break;
+                if (__builtin_amdgcn_s_memrealtime() > deadline) { dead = true; break; }
+            }
+        }
+        if (NBAR == 2) {
+            if (__syncthreads_or(dead)) break;
+        } else if (NBAR == 3) {
+            __syncthreads();
+            if (dead) break;
+        } else if (dead) {
+            break;
+        }
+    }
+    if (threadIdx.x == 64) out[me] = dead ? ~0ull : __builtin_amdgcn_s_memrealtime() - t0;
+}
+
+template <int PUBW, int POLLW, bool XPOLL, int NBAR = 2>
+void run_paced(unsigned long long *vec, int *ctr, unsigned long long *out, const char *name) {
+    const int nhops = 20000;
+    hipMemset(vec, 0, 8192 * 8 + 4096);
+    hipMemset(ctr, 0, 4);
+    hipMemset(out, 0, kN * 8);
+    hipLaunchKernelGGL((hops_paced<PUBW, POLLW, XPOLL, NBAR>), dim3(256), dim3(512), 0, 0, vec, ctr, nhops, out);
+    hipDeviceSynchronize();
+    unsigned long long h[kN];
+    hipMemcpy(h, out, kN * 8, hipMemcpyDeviceToHost);
+    unsigned long long mx = 0;
+    bool dead = false;
+    for (int i = 0; i < kN; ++i) {
+        if (h[i] == ~0ull) dead = true;
+        else if (h[i] > mx) mx = h[i];
+    }
+    printf("%-40s %s %.3f us per paced hop\n", name, dead ? "TIMEOUT" : "", mx * 10e-3 / nhops);
+    fflush(stdout);
+}
+
 int main() {
     unsigned long long *vec, *out;
     int *ctr;
-    hipMalloc(&vec, 1 << 20);
+    hipMalloc(&vec, 1 << 20);   // ≥ 8192 granules + slack
     hipMalloc(&out, 64 * 8);
     hipMalloc(&ctr, 64);
-    for (int r = 0; r < 2; ++r) {
+    for (int r = 0; r < 1; ++r) {
         run<true, 0, 1, false, false>(vec, ctr, out, "LOCAL 8B x8");
         run<true, 0, 1, true, false>(vec, ctr, out, "LOCAL 8B x8 drain");
         run<true, 1, 1, false, false>(vec, ctr, out, "LOCAL 16B x4");
@@ -142,6 +222,13 @@ int main() {
         run<true, 1, 2, true, false>(vec, ctr, out, "LOCAL 16B x4 drain, 2 rounds in flight");
         run<true, 1, 1, true, true>(vec, ctr, out, "LOCAL 16B x4 drain, LDS-streaming waves");
         run<false, 0, 1, false, false>(vec, ctr, out, "SPREAD 8B x8 (sc1 stores)");
+        run_paced<1, 1, false, 1>(vec, ctr, out, "PACED 1 pub, 1 poller, one plain barrier");
+        run_paced<1, 1, false, 3>(vec, ctr, out, "PACED 1 pub, 1 poller, two barriers");
+        run_paced<8, 1, false, 3>(vec, ctr, out, "PACED 8 publisher waves, 1 poller");
+        run_paced<1, 2, false, 3>(vec, ctr, out, "PACED 1 publisher wave, 2 pollers");
+        run_paced<8, 2, false, 3>(vec, ctr, out, "PACED 8 publisher waves, 2 pollers");
+        run_paced<8, 1, true, 3>(vec, ctr, out, "PACED 8 pub, 1 poller + h2 vector poller");
+        run_paced<8, 2, true, 3>(vec, ctr, out, "PACED 8 pub, 2 pollers + h2 vector poller");
     }
     return 0;
 }

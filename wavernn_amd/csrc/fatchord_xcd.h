@@ -11,11 +11,14 @@ constexpr int kXcdWgs = 32;         // workgroups (= CUs) per XCD, one per CU
 constexpr int kXWaves = 8;          // compute waves per workgroup (two per SIMD), no loader wave
 constexpr int kXThreads = 64 * kXWaves;
 constexpr int kXUnits = 16;         // GRU units per workgroup (R / kXcdWgs), 2 per wave
-constexpr int kXFcRows = 16;        // fc1 / fc2 rows per workgroup (F / kXcdWgs), 2 per wave
-constexpr int kXGhWaves = 7;        // waves 1..7 compute the off-critical W_hh1 / W_hh2 rows
-constexpr int kXGhRows = 7;         // rows per such wave (48 = 6·7 + 6)
-constexpr int kXH2Reg = 4;          // W_hh2 rows per wave held in VGPRs (rows 0..27) ...
-constexpr int kXH2RegRows = kXGhWaves * kXH2Reg;    // ... the other 20 live in LDS, 3 per wave
+constexpr int kXFcRows = 16;        // fc1 / fc2 rows per workgroup (F / kXcdWgs)
+// wave roles (all eight compute GRU1 and GRU2):
+//   0     samples (polls F2); W_hh1 rows 0..9; W_hh2 rows 24..27 in VGPRs
+//   1, 2  fc1 rows 8h..8h+7 (h = w − 1) from the polled y, weights in VGPRs; W_hh2 LDS rows
+//   3, 4  fc2 rows 8h..8h+7 (h = w − 3) from the polled f1 + their fc3 partials; W_hh1 rows
+//   5..7  W_hh2 rows 8(w − 5)..+7 in VGPRs; W_hh1 rows (5, 7), the h2 gather (6)
+constexpr int kXWaveFc1 = 1, kXWaveFc2 = 3;
+constexpr int kXH2RegRows = 28;     // W_hh2 rows 0..27 in VGPRs, 28..47 in LDS
 constexpr int kXRing = 4;           // steps of conditioning terms / sampler noise in LDS
 constexpr int kXNoise = 16;         // 11 MoL sampler terms, padded
 
@@ -34,11 +37,11 @@ constexpr long long kXXcdStride = kXHops * kXHopStride + 512;   // granules per 
 // Per-workgroup weight slab (floats), all rows natural (512 contiguous):
 struct XcdSlab {
     int wih2;    // [8 waves][6 rows (2q + i)][512]   W_ih2[:, :R] gate q of unit 2w + i
-    int w1;      // [8][2][512]                         fc1 rows 2w + i (y part)
-    int w2;      // [8][2][512]                         fc2 rows 2w + i (f1 part)
-    int whh2;    // [48][512]   W_hh2 rows u·3 + q: rows < 28 in VGPRs (wave 1 + r / 4), the rest LDS
+    int w1;      // [16][512]                           fc1 rows 16c + r (y part)
+    int w2;      // [16][512]                           fc2 rows 16c + r (f1 part)
+    int whh2;    // [48][512]   W_hh2 rows u·3 + q (rows < kXH2RegRows in VGPRs, the rest LDS)
     int whh1;    // [48][512]                           W_hh1 rows u·3 + q (LDS-resident)
-    int w3;      // [8][2][32]                          W3[j][16c + 2w + i]
+    int w3;      // [16][32]                            W3[j][16c + r] (j ≥ 30: 0)
     int q1a;     // [3][512]                            W_ih1·W_I[:, 0], gate-major (all units)
     int cst;     // [kXCst] small vectors, copied to LDS (XCst offsets)
     int total;
@@ -72,7 +75,7 @@ struct XcdArgs {
 };
 
 struct XcdLds {
-    int whh1, whh2, h1, y, f1, h2, sg, part, ring, nz, gh2, cst, xs, misc, total;
+    int whh1, whh2, h1, h2, sg, w3, f2x, ring, nz, gh2, cst, xs, misc, total;
 };
 
 __host__ __device__ inline XcdLds xcd_lds_layout() {
@@ -80,17 +83,17 @@ __host__ __device__ inline XcdLds xcd_lds_layout() {
     int o = 0;
     // the small per-step arrays first (offsets < 64 KiB: lane address + instruction immediate)
     l.h1 = o;    o += 512;
-    l.y = o;     o += 512;
-    l.f1 = o;    o += 512;
     l.h2 = o;    o += 512;
     l.sg = o;    o += 4 * 512;                // GRU1 terms of all units for the coming step
-    l.part = o;  o += kXWaves * 32;           // fc3 partial logits per wave
+    l.w3 = o;    o += kXFcRows * 32;          // fc3 columns of the own f2 rows (waves 3, 4)
+    l.f2x = o;   o += 32;                     // wave 4's fc3 partials, handed to wave 3
     l.ring = o;  o += kXRing * kXTerms;
     l.nz = o;    o += kXRing * kXNoise;
     l.gh2 = o;   o += 48;                     // W_hh2·h2 of the own units for the next step
     l.cst = o;   o += kXCst;
     l.xs = o;    o += 4;                      // x, by step parity
-    l.misc = o;  o += 4;                      // [0] abort flag, [1] member index
+    l.misc = o;  o += 8;                      // [0] abort flag, [1] member index, step flags (step + 1):
+                                              // [2] h2 gathered, [3] f2x ready, [4] y gathered, [5] f1 gathered
     l.whh1 = o;  o += 48 * 512;
     l.whh2 = o;  o += (48 - kXH2RegRows) * 512;
     l.total = o;

@@ -208,6 +208,63 @@ __device__ __forceinline__ void xgather16(const unsigned long long *g, uint32_t 
     }
 }
 
+// Poll NP·128 granules (pairs l + 64k) with 16-byte loads until every granule carries `tag`;
+// the pairs stay in registers (v[k].x, v[k].z).  Bounded; on abort the values are garbage.
+template <int NP>
+__device__ __forceinline__ void xpoll16(const unsigned long long *g, uint32_t tag, int *ctl, long long timeout,
+                                        int step, int hop, int *lds_abort, int lid, u4v (&v)[NP]) {
+    const __amdgpu_buffer_rsrc_t r = hop_rsrc(g);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned spins = 0;
+    for (;;) {
+#pragma unroll
+        for (int k = 0; k < NP; ++k) v[k] = ld16_sc1(r, 16 * (lid + 64 * k));
+        bool ok = true;
+#pragma unroll
+        for (int k = 0; k < NP; ++k) ok &= (v[k].y == tag) & (v[k].w == tag);
+        if (ok) return;
+        if ((++spins & 63u) == 0) {
+            const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - t0) > timeout;
+            const bool other = __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+            if (late || other) {
+                if (late) record_abort(ctl, -4, step, hop, blockIdx.x);
+                *lds_abort = 1;
+                return;
+            }
+        }
+    }
+}
+
+// 8 rows of a 512-wide layer against a vector polled into registers by ONE wave (no LDS, no
+// barrier): lane l holds the pairs k = 0..3 at granules 2(l + 64k) + {0, 1} (xk[k]) and the
+// matching weights of row r in w[2r + k/2] (.xy for even k, .zw for odd).  Packed FMAs, then a
+// reduce-scatter over the wave — permlane32 swap (row r vs r + 4), permlane16 swap (r vs r + 2),
+// DPP sum over the 16 lanes of a row — leaves in o[j] the full sum of row j + 2·(l >> 4),
+// identical bits in all 16 lanes of DPP row l >> 4.
+__device__ __forceinline__ void fc8_rows(const f4v (&w)[16], const f2v (&xk)[4], float (&o)[2]) {
+    float s[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        f2v acc = __builtin_elementwise_fma(w[2 * r].xy, xk[0], f2v{0.0f, 0.0f});
+        f2v acc2 = __builtin_elementwise_fma(w[2 * r].zw, xk[1], f2v{0.0f, 0.0f});
+        acc = __builtin_elementwise_fma(w[2 * r + 1].xy, xk[2], acc);
+        acc2 = __builtin_elementwise_fma(w[2 * r + 1].zw, xk[3], acc2);
+        const f2v t = acc + acc2;
+        s[r] = t.x + t.y;
+    }
+    float h[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {   // lanes < 32 keep row j, lanes ≥ 32 row j + 4
+        const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(s[j]), __float_as_uint(s[j + 4]), false, false);
+        h[j] = __uint_as_float(q[0]) + __uint_as_float(q[1]);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {   // even DPP rows keep h[j], odd rows h[j + 2]
+        const auto q = __builtin_amdgcn_permlane16_swap(__float_as_uint(h[j]), __float_as_uint(h[j + 2]), false, false);
+        o[j] = row_sum16(__uint_as_float(q[0]) + __uint_as_float(q[1]));
+    }
+}
+
 #define XSTAMPW(kk, w)                                                                                        \
     do {                                                                                                      \
         if (kDbg && a.dbg && wave == (w) && lane == 0 && t - a.t0 < a.dbg_steps)                              \
@@ -218,14 +275,13 @@ __device__ __forceinline__ void xgather16(const unsigned long long *g, uint32_t 
 template <bool kDbg>
 __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    constexpr int R = 512, NC = 30, TW = kXcdWgs * kXTerms;
+    constexpr int R = 512, TW = kXcdWgs * kXTerms;
     const XcdLds ll = xcd_lds_layout();
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 31, eng = lane >> 5;
-    float *whh1 = smem + ll.whh1, *whh2l = smem + ll.whh2, *h1s = smem + ll.h1, *ys = smem + ll.y;
-    float *f1s = smem + ll.f1, *h2s = smem + ll.h2, *sg = smem + ll.sg, *part = smem + ll.part;
+    float *whh1 = smem + ll.whh1, *whh2l = smem + ll.whh2, *f2x = smem + ll.f2x, *h1s = smem + ll.h1, *h2s = smem + ll.h2, *sg = smem + ll.sg, *w3s = smem + ll.w3;
     float *ring = smem + ll.ring, *nzr = smem + ll.nz, *gh2s = smem + ll.gh2, *cst = smem + ll.cst, *xs = smem + ll.xs;
     int *misc = reinterpret_cast<int *>(smem + ll.misc);
-    int *abort_flag = misc;
+    int *abort_flag = misc, *h2ready = misc + 2, *f2ready = misc + 3, *ygot = misc + 4, *f1got = misc + 5;
 
     // ---- membership: XCD k (row b0 + k) and index c within it
     if (tid == 0) {
@@ -234,6 +290,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
         if (k < a.nb) c = atomicAdd(&a.members[k], 1);
         misc[1] = (k < a.nb && c < kXcdWgs) ? k * kXcdWgs + c : -1;
         misc[0] = 0;
+        for (int i = 2; i < 8; ++i) misc[i] = 0;
     }
     __syncthreads();
     const int mem = misc[1];
@@ -250,33 +307,46 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
     const float *S = a.slab + (size_t)c * a.s.total;
     const unsigned long long prow = (unsigned long long)(a.row0 + k);
 
-    // ---- register-resident weights: engine e of wave w holds, per pass, one row's chunks li + 32m
-    //   GRU2: pass q = gate q of unit 2w + e (slab row 2q + e);  fc1 / fc2: row 2w + e;
-    //   W_hh2 (waves 1..7): pass p = row (w-1)·4 + 2p + e
-    f4v wih2[3][4], w1r[4], w2r[4], whh2r[2][4];
+    // ---- register-resident weights
+    //   wih2 (all waves): GRU2 pass q = gate q of unit ui = 2w + e, chunks li + 32m of the row
+    //   wr (one register set, contents by role):
+    //     waves 1, 2 / 3, 4: fc1 / fc2 rows 8h + r, r = 0..7, at the granules this lane polls (fc8_rows)
+    //     waves 5..7: W_hh2 rows 8(w − 5) + 2p + e, p = 0..3, at wr[4p + m] (32-lane chunks)
+    //     wave 0: wr[0..7] the F2 poll buffer, wr[8..15] W_hh2 rows 24 + 2p + e, p = 0..1
+    f4v wih2[3][4], wr[16];
     auto ldrow = [&](const float *row, int m) { return *reinterpret_cast<const f4v *>(row + 4 * (li + 32 * m)); };
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
+    for (int m = 0; m < 4; ++m)
 #pragma unroll
         for (int q = 0; q < 3; ++q) wih2[q][m] = ldrow(S + a.s.wih2 + (wave * 6 + 2 * q + eng) * R, m);
-        w1r[m] = ldrow(S + a.s.w1 + (wave * 2 + eng) * R, m);
-        w2r[m] = ldrow(S + a.s.w2 + (wave * 2 + eng) * R, m);
+    const bool fcw = wave >= kXWaveFc1 && wave < kXWaveFc2 + 2;
+    if (fcw) {
+        const int hf = (wave - kXWaveFc1) & 1;
+        const float *W = S + (wave < kXWaveFc2 ? a.s.w1 : a.s.w2) + hf * 8 * R;
 #pragma unroll
-        for (int p = 0; p < 2; ++p)
-            whh2r[p][m] = wave >= 1 ? ldrow(S + a.s.whh2 + ((wave - 1) * kXH2Reg + 2 * p + eng) * R, m)
-                                    : f4v{0.0f, 0.0f, 0.0f, 0.0f};
+        for (int r = 0; r < 8; ++r)
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                const f2v lo = *reinterpret_cast<const f2v *>(W + r * R + 2 * (lane + 64 * (2 * hh)));
+                const f2v hi = *reinterpret_cast<const f2v *>(W + r * R + 2 * (lane + 64 * (2 * hh + 1)));
+                wr[2 * r + hh] = f4v{lo.x, lo.y, hi.x, hi.y};
+            }
+    } else {
+        const int rb = wave == 0 ? 24 - 4 : 8 * (wave - 5);   // wave 0: passes 2, 3 → rows 24..27
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+                wr[4 * p + m] = (wave != 0 || p >= 2) ? ldrow(S + a.s.whh2 + (rb + 2 * p + eng) * R, m)
+                                                      : f4v{0.0f, 0.0f, 0.0f, 0.0f};
     }
-    const float w3a = S[a.s.w3 + (wave * 2 + 0) * 32 + li];
-    const float w3b = S[a.s.w3 + (wave * 2 + 1) * 32 + li];
     // GRU1 of unit tid: x-coefficients
     const float q1r = S[a.s.q1a + tid], q1z = S[a.s.q1a + R + tid], q1n = S[a.s.q1a + 2 * R + tid];
-    const int ui = wave * 2 + eng;                   // this engine's local unit and fc row
-    // W_hh1 rows (waves 1..5 and 7, eight each): gh0 + 2p + e, p = 0..3; lane li < 4 of an
-    // engine publishes the terms of its row 2·li + e
-    const bool gh1w = wave >= 1 && wave != 6;
-    const int gh0 = 8 * (wave <= 5 ? wave - 1 : 5);
-    const int h2l0 = (wave - 1) * 3;                 // W_hh2 LDS rows of waves 1..7: 28 + h2l0 + {0, 1, 2}
-
+    const int ui = wave * 2 + eng;                   // this engine's local GRU unit
+    // W_hh1 rows (waves 0, 3, 4, 5: ten each, wave 7: eight): gh0 + 2p + e, p = 0..4; lane li < 5
+    // of an engine publishes the terms of its row gh0 + 2·li + e
+    const bool gh1w = wave == 0 || wave == 3 || wave == 4 || wave == 5 || wave == 7;
+    const int gh0 = wave == 0 ? 0 : wave == 7 ? 40 : 10 * (wave - 2);
     // sampler noise of step t → NZ(t): u1 → log(-log u1) (distribution.py:107), u2 → log u2 − log(1 − u2) (:119)
     auto noise_term = [&](int t) -> float {
         float uu;
@@ -299,23 +369,53 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
             xpub(g + 2, tag, p1 + bi);
         }
     };
-    // the GRU1 terms of this wave's 8 W_hh1 rows (gh[p]: row gh0 + 2p + e), lanes li < 4
-    auto publish_terms = [&](int t, const float (&gh)[4]) {
-        if (li < 4) {
-            const float v = li == 0 ? gh[0] : li == 1 ? gh[1] : li == 2 ? gh[2] : gh[3];
-            publish_term(t, gh0 + 2 * li + eng, v);
+    // the GRU1 terms of this wave's W_hh1 rows (gh[p]: row gh0 + 2p + e), lanes li < 5
+    auto publish_terms = [&](int t, const float (&gh)[5]) {
+        const int rr = gh0 + 2 * li + eng;
+        if (li < 5 && rr < 48) {
+            const float v = li == 0 ? gh[0] : li == 1 ? gh[1] : li == 2 ? gh[2] : li == 3 ? gh[3] : gh[4];
+            publish_term(t, rr, v);
         }
     };
-    // a quarter of step t's GRU1 terms (waves 3..6: 512 granules each, one poll round)
+    // W_hh1·h1 for this wave's rows (the GRU1 terms of step t + 1, published later by
+    // publish_terms): all dots first, so LDS reads of later rows overlap earlier dots
+    auto gh1_dots = [&](float (&gh)[5]) {
+        f4v hx[4];
+        e32x(h1s, li, hx);
+#pragma unroll
+        for (int p = 0; p < 5; ++p) {
+            f4v w4[4];
+            e32x(whh1 + min(gh0 + 2 * p + eng, 47) * R, li, w4);
+            gh[p] = e32dot(w4, hx);
+        }
+    };
+    // intra-workgroup step flags in LDS (no data behind them, or the writer drained its LDS
+    // stores first): the critical waves mark "y gathered" / "f1 gathered", the others wait for
+    // them so that their own memory traffic stays out of the critical hops' windows
+    auto set_flag = [&](int *f, uint32_t tag) {
+        if (lane == 0) __hip_atomic_store(f, (int)tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto wait_flag = [&](int *f, uint32_t tag) {
+        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)tag)
+            __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");
+    };
+    // W_hh2·h2 → gh2s for the next GRU2 (after wave 6 has gathered h2): lanes li < np store the
+    // rows rb + 2·li + e
+    auto gh2_store = [&](int rb, int np, const float (&gh)[5]) {
+        const int rr = rb + 2 * li + eng;
+        if (li < np) gh2s[rr] = li == 0 ? gh[0] : li == 1 ? gh[1] : li == 2 ? gh[2] : li == 3 ? gh[3] : gh[4];
+    };
+    // a quarter of step t's GRU1 terms (waves 1, 2, 5, 6: 512 granules each, one poll round)
     auto gather_terms = [&](int t) {
-        const int qq = wave - 3;
+        const int qq = wave <= 2 ? wave - 1 : wave - 3;
         xgather16<4>(XG(XH_S0 + (t & 1)) + qq * 512, (uint32_t)t + 1u, a.ctl, a.timeout_ticks, t, XH_S0 + (t & 1),
                      abort_flag, lane, [&](int i, float v0, float v1) {
                          *reinterpret_cast<f2v *>(sg + qq * 512 + i) = f2v{v0, v1};
                      });
     };
 
-    // ---- prologue: W_hh1 and the LDS rows of W_hh2, small vectors, ring slots t0..t0+2, state
+    // ---- prologue: W_hh1, fc3 columns, small vectors, ring slots t0..t0+2, state
     {
         const f4v *src = reinterpret_cast<const f4v *>(S + a.s.whh1);
         f4v *dst = reinterpret_cast<f4v *>(whh1);
@@ -323,6 +423,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
         src = reinterpret_cast<const f4v *>(S + a.s.whh2 + kXH2RegRows * R);
         dst = reinterpret_cast<f4v *>(whh2l);
         for (int i = tid; i < (48 - kXH2RegRows) * R / 4; i += kXThreads) dst[i] = src[i];
+        for (int i = tid; i < kXFcRows * 32; i += kXThreads) w3s[i] = S[a.s.w3 + i];
         for (int i = tid; i < kXCst; i += kXThreads) cst[i] = S[a.s.cst + i];
         for (int t = a.t0; t < a.t0 + 3; ++t) {
             if (t <= t_terms)
@@ -345,10 +446,10 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
     __syncthreads();
     if (!resume) {   // GRU1 terms of step 0 (GH1 = 0), published and gathered
         if (gh1w) {
-            const float z4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-            publish_terms(0, z4);
+            const float z5[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+            publish_terms(0, z5);
         }
-        if (wave >= 3 && wave <= 6) {
+        if (wave == 1 || wave == 2 || wave == 5 || wave == 6) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             gather_terms(0);
         }
@@ -401,102 +502,37 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
             h2own = hn;
             // y = (x_I + h1) + h2 (:212, :216)
             const float y = (xi + h1j) + hn;
-            if (li == 0) {
-                xpub(XG(XH_Y) + c * kXUnits + ui, tag, y);
-                xpub(XG(XH_H2) + c * kXUnits + ui, tag, hn);
-            }
+            if (li == 0) xpub(XG(XH_Y) + c * kXUnits + ui, tag, y);   // h2: after hop Y (pub_h2)
         }
         XSTAMP(2);
-        // ---- hop Y (wave 0) ‖ W_hh1·h1 → GRU1 terms of step t+1 (waves 1..7)
+        // Off-critical memory traffic (GRU1-term and h2 publishes, the S / h2 gathers, the ring)
+        // waits for the critical waves' flags: hop Y's window (GRU2 → y gathered) carries only y,
+        // hop F1's only f1, hop F2's only the partials (a second poll stream or a burst of stores
+        // beside a critical poll costs it ≈ 0.2 µs: tools/xcdhop.hip PACED variants).
+        //   after y gathered  : publish the GRU1 terms of step t+1 and h2
+        //   after f1 gathered : gather h2 (wave 6), S (waves 1, 2, 5, 6), the ring (wave 7)
+        //   after h2 gathered : W_hh2·h2 (waves 0, 1, 2, 5, 6, 7)
+        auto pub_h2 = [&]() {
+            if (li == 0) xpub(XG(XH_H2) + c * kXUnits + ui, tag, h2own);
+        };
+        // fc waves: lane l ends fc8_rows with row 8h + j + 2·(l >> 4) in o[j]; lanes with
+        // (l & 15) < 2 publish row 8h + (l & 1) + 2·(l >> 4)
+        const int jq = lane & 1, rho = jq + 2 * (lane >> 4);
         if (wave == 0) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            xgather16<4>(XG(XH_Y), tag, a.ctl, a.timeout_ticks, t, XH_Y, abort_flag, lane,
-                         [&](int i, float v0, float v1) { *reinterpret_cast<f2v *>(ys + i) = f2v{v0, v1}; });
-            XSTAMP(3);
-        } else if (wave == 6) {
-            if (more && !WRNN_XCD_SKIP_H2) {   // h2 (published with y) for the W_hh2 dots of the next window
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                xgather16<4>(XG(XH_H2), tag, a.ctl, a.timeout_ticks, t, XH_H2, abort_flag, lane,
-                             [&](int i, float v0, float v1) { *reinterpret_cast<f2v *>(h2s + i) = f2v{v0, v1}; });
+            if (more) {
+                float gh[5];
+                gh1_dots(gh);
+                wait_flag(ygot, tag);
+                publish_terms(t + 1, gh);
+                pub_h2();
+                wait_flag(h2ready, tag);
+                f4v hx[4];
+                e32x(h2s, li, hx);
+                float g2[5] = {e32dot(*reinterpret_cast<const f4v(*)[4]>(&wr[8]), hx),
+                               e32dot(*reinterpret_cast<const f4v(*)[4]>(&wr[12]), hx), 0.0f, 0.0f, 0.0f};
+                gh2_store(24, 2, g2);
             }
-            XSTAMPW(10, 6);
-        } else if (more) {
-            // W_hh1·h1 → GRU1 terms of step t+1: the 4 dots first (LDS reads of later rows overlap
-            // earlier dots), then one publish
-            f4v hx[4];
-            e32x(h1s, li, hx);
-            float gh[4];
-#pragma unroll
-            for (int p = 0; p < 4; ++p) {
-                f4v wr[4];
-                e32x(whh1 + (gh0 + 2 * p + eng) * R, li, wr);
-                gh[p] = e32dot(wr, hx);
-            }
-            publish_terms(t + 1, gh);
-            XSTAMPW(9, 1);
-        }
-        const float v1 = tr[XT_V1 + ui], v2 = tr[XT_V2 + ui];
-        bar();
-        XSTAMPW(14, 3);
-        // ---- fc1 (:216-218), row ui → relu → hop F1
-        {
-            f4v yx[4];
-            e32x(ys, li, yx);
-            const float A = e32dot(w1r, yx) + v1;
-            if (li == 0) xpub(XG(XH_F1) + c * kXFcRows + ui, tag, A > 0.0f ? A : 0.0f);
-        }
-        XSTAMP(4);
-        if (wave == 0) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            xgather16<4>(XG(XH_F1), tag, a.ctl, a.timeout_ticks, t, XH_F1, abort_flag, lane,
-                         [&](int i, float v0, float v1) { *reinterpret_cast<f2v *>(f1s + i) = f2v{v0, v1}; });
-            XSTAMP(5);
-        } else if (more) {
-            // W_hh2·h2 → gh2s for the next GRU2: passes 0/1 the VGPR rows, 2/3 the LDS rows
-            // 28 + h2l0 + {0, 1, 2}; all dots first, then the LDS stores
-            f4v hx[4];
-            e32x(h2s, li, hx);
-            float gh[4];
-#pragma unroll
-            for (int p = 0; p < 4; ++p) {
-                if (p < 2) {
-                    gh[p] = e32dot(whh2r[p], hx);
-                } else {
-                    const int lr = h2l0 + 2 * (p - 2) + eng;     // wave 7 has LDS rows 18, 19 only
-                    f4v wr[4];
-                    e32x(whh2l + (lr < 48 - kXH2RegRows ? lr : 48 - kXH2RegRows - 1) * R, li, wr);
-                    gh[p] = e32dot(wr, hx);
-                }
-            }
-            if (li < 4) {
-                const int lr = h2l0 + 2 * (li - 2) + eng;
-                const int rr = li < 2 ? (wave - 1) * kXH2Reg + 2 * li + eng
-                                      : ((2 * (li - 2) + eng < 3 && lr < 48 - kXH2RegRows) ? kXH2RegRows + lr : -1);
-                const float v = li == 0 ? gh[0] : li == 1 ? gh[1] : li == 2 ? gh[2] : gh[3];
-                if (rr >= 0) gh2s[rr] = v;
-            }
-            XSTAMPW(13, 3);
-        }
-        bar();
-        // ---- fc2 (:220-221) → relu → fc3 partial logits of the 16 own f2 rows (:223)
-        {
-            f4v fx[4];
-            e32x(f1s, li, fx);
-            float A = e32dot(w2r, fx) + v2;
-            A = A > 0.0f ? A : 0.0f;
-            const float f20 = lane_bcast(A, 0), f21 = lane_bcast(A, 32);
-            if (lane < 32) part[wave * 32 + lane] = fmaf(w3b, f21, w3a * f20);
-        }
-        bar();
-        XSTAMP(6);
-        if (wave == 0) {
-            // Σ of the 8 waves' partials → hop F2 → Σ of the 32 workgroups' partials + b3 → sample
-            if (lane < kXF2Line) {   // all 32 granules of the line (30, 31: zero weights) for the 16-byte polls
-                float s = 0.0f;
-#pragma unroll
-                for (int w = 0; w < kXWaves; ++w) s += part[w * 32 + lane];
-                xpub(XG(XH_F2) + c * kXF2Line + lane, tag, s);
-            }
+            // ---- hop F2: Σ of the 32 workgroups' partials + b3 → sample
             // lane l: logits (2jp, 2jp+1), jp = l & 15, of producers 8·(l >> 4) + m, m = 0..7:
             // one 16-byte load each (256 B apart: immediates)
             const int jp = lane & 15, pg = lane >> 4;
@@ -509,9 +545,8 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
             unsigned spins = 0;
             float pa[8], pb[8];
             for (;;) {
-                // the polled pieces live in whh2r's registers: wave 0 holds no W_hh2 rows (one
-                // register set serves both roles, so the kernel fits 256 VGPRs)
-                u4v *v = reinterpret_cast<u4v *>(&whh2r[0][0]);
+                // the polled pieces live in wr[0..7] (wave 0 holds no weights there)
+                u4v *v = reinterpret_cast<u4v *>(&wr[0]);
 #pragma unroll
                 for (int m = 0; m < 8; ++m) v[m] = ld16_sc1(rf, goff + m * kXF2Line * 8);
                 bool ok = true;
@@ -553,21 +588,139 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
                 if (c == 0) a.out[(size_t)b * a.L + t] = x;
             }
             XSTAMP(8);
-        } else if (more) {
-            if (wave >= 3 && wave <= 6 && !WRNN_XCD_SKIP_SG) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                gather_terms(t + 1);
-                XSTAMPW(11, 5);
+        } else if (wave < kXWaveFc2) {
+            // ---- hop Y → fc1 (:216-218) rows 8h.. in registers → relu → hop F1
+            const int hf = wave - kXWaveFc1, rg = 8 * hf + rho;
+            const float v1 = tr[XT_V1 + rg];
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            u4v v[4];
+            xpoll16<4>(XG(XH_Y), tag, a.ctl, a.timeout_ticks, t, XH_Y, abort_flag, lane, v);
+            if (hf == 0) set_flag(ygot, tag);
+            XSTAMPW(3, 1);
+            f2v yk[4];
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) yk[kk] = f2v{__uint_as_float(v[kk].x), __uint_as_float(v[kk].z)};
+            float o[2];
+            fc8_rows(wr, yk, o);
+            const float A = (jq == 0 ? o[0] : o[1]) + v1;
+            if ((lane & 15) < 2) xpub(XG(XH_F1) + c * kXFcRows + rg, tag, A > 0.0f ? A : 0.0f);
+            XSTAMPW(4, 1);
+            if (more) {   // h2 out; after f1 gathered: a quarter of the next S; W_hh2 LDS rows 28 + 10h + 2p + e
+                pub_h2();
+                wait_flag(f1got, tag);
+                if (!WRNN_XCD_SKIP_SG) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    gather_terms(t + 1);
+                }
+                wait_flag(h2ready, tag);
+                f4v hx[4];
+                e32x(h2s, li, hx);
+                float gh[5];
+#pragma unroll
+                for (int p = 0; p < 5; ++p) {
+                    f4v w4[4];
+                    e32x(whh2l + (10 * hf + 2 * p + eng) * R, li, w4);
+                    gh[p] = e32dot(w4, hx);
+                }
+                gh2_store(kXH2RegRows + 10 * hf, 5, gh);
+                XSTAMPW(11, 1);
             }
-            if (wave == 7 && t + 2 >= a.t0 + 3) {
+        } else if (wave < kXWaveFc2 + 2) {
+            const int hf = wave - kXWaveFc2;
+            if (more) {   // W_hh1 rows; after y gathered their terms and h2 out
+                float gh[5];
+                gh1_dots(gh);
+                wait_flag(ygot, tag);
+                publish_terms(t + 1, gh);
+                pub_h2();
+            }
+            XSTAMPW(9, 3);
+            // ---- hop F1 → fc2 (:220-221) rows 8h.. in registers → relu → fc3 partial logits of
+            // those rows (:223); wave 4 hands its partials to wave 3 (LDS flag), wave 3 publishes
+            // the workgroup's 32 (hop F2)
+            float v2[2], w3c[8];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) v2[j] = tr[XT_V2 + 8 * hf + j + 2 * (lane >> 4)];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) w3c[r] = w3s[(8 * hf + r) * 32 + li];
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            u4v v[4];
+            xpoll16<4>(XG(XH_F1), tag, a.ctl, a.timeout_ticks, t, XH_F1, abort_flag, lane, v);
+            if (hf == 0) set_flag(f1got, tag);
+            XSTAMPW(5, 3);
+            f2v fk[4];
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) fk[kk] = f2v{__uint_as_float(v[kk].x), __uint_as_float(v[kk].z)};
+            float o[2];
+            fc8_rows(wr, fk, o);
+            float p = 0.0f;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const float f = o[j] + v2[j];
+                const float f2 = f > 0.0f ? f : 0.0f;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) p = fmaf(w3c[j + 2 * g], lane_bcast(f2, 16 * g), p);
+            }
+            if (hf == 1) {
+                if (lane < 32) f2x[lane] = p;
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                set_flag(f2ready, tag);
+            } else {
+                while (__hip_atomic_load(f2ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)tag) {
+                }
+                asm volatile("" ::: "memory");
+                if (lane < kXF2Line) xpub(XG(XH_F2) + c * kXF2Line + lane, tag, p + f2x[lane]);   // 30, 31: zero weights
+                XSTAMPW(6, 3);
+            }
+        } else if (more) {
+            // ---- waves 5..7: W_hh1 rows (5, 7) → after y gathered their terms and h2 out; after
+            // f1 gathered: h2 (wave 6, then flag), S quarters (5, 6), the ring (7); after h2
+            // gathered: W_hh2·h2 (VGPR rows)
+            if (wave != 6) {
+                float gh[5];
+                gh1_dots(gh);
+                wait_flag(ygot, tag);
+                publish_terms(t + 1, gh);
+            } else {
+                wait_flag(ygot, tag);
+            }
+            pub_h2();
+            wait_flag(f1got, tag);
+            if (wave == 6) {
+                if (!WRNN_XCD_SKIP_H2) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    xgather16<4>(XG(XH_H2), tag, a.ctl, a.timeout_ticks, t, XH_H2, abort_flag, lane,
+                                 [&](int i, float v0, float v1) { *reinterpret_cast<f2v *>(h2s + i) = f2v{v0, v1}; });
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                set_flag(h2ready, tag);
+                XSTAMPW(10, 6);
+            }
+            if (wave <= 6) {
+                if (!WRNN_XCD_SKIP_SG) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    gather_terms(t + 1);
+                }
+                XSTAMPW(14, 5);
+            } else if (t + 2 >= a.t0 + 3) {
                 // ring: step t+2's terms and sampler noise, loaded and stored within this window
-                // (the longest of the step; a load carried across steps in registers would not
-                // fit the VGPR budget, and an LDS-DMA makes hipcc wait for it before every later
-                // LDS access of the issuing wave)
+                // (a load carried across steps in registers would not fit the VGPR budget, and an
+                // LDS-DMA makes hipcc wait for it before every later LDS access of the issuing wave)
                 if (t + 2 <= t_terms && lane < kXTerms / 4)
                     reinterpret_cast<f4v *>(RING(t + 2))[lane] = reinterpret_cast<const f4v *>(TERMS(t + 2))[lane];
                 if (t + 2 < a.L && lane < 11) NZ(t + 2)[lane] = noise_term(t + 2);
                 XSTAMPW(12, 7);
+            }
+            wait_flag(h2ready, tag);
+            {
+                f4v hx[4];
+                e32x(h2s, li, hx);
+                float gh[5];
+#pragma unroll
+                for (int p = 0; p < 4; ++p) gh[p] = e32dot(*reinterpret_cast<const f4v(*)[4]>(&wr[4 * p]), hx);
+                gh[4] = 0.0f;
+                gh2_store(8 * (wave - 5), 4, gh);
+                XSTAMPW(13, 5);
             }
         }
         bar();
