@@ -11,8 +11,11 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------------------ wave-level helpers
+// (update_dpp with old = 0 and bound_ctrl: hipcc then folds the move into the consuming VALU op,
+// v_add_f32_dpp instead of v_mov_b32_dpp + v_add_f32; every pattern used here — quad_perm,
+// row mirrors, row_ror — reads a valid lane, so bound_ctrl never applies)
 #define WRNN_DPP(v, ctrl) \
-    __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, (v)), (ctrl), 0xF, 0xF, false))
+    __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, (v)), (ctrl), 0xF, 0xF, true))
 
 // Full-wave sum; every lane returns the same bits.  Row stages via DPP (xor1, xor2,
 // half-mirror, mirror), then the four row sums combined in a fixed order.
