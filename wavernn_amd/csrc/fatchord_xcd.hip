@@ -75,8 +75,21 @@ __device__ __forceinline__ float cross_rows(float v) { return perm_sum32(perm_su
 // MoL sampler (utils/distribution.py:87-123) on logits held in pairs: lane jp (of every DPP row)
 // holds logits 2jp (la) and 2jp+1 (lb); ua / ub = log(-log u1) of those mixture indices (jp < 5).
 // k = argmax over the 10 logit_probs − u (first max on ties), then the logistic draw with the
-// selected mean (logit 10 + k) and log-scale (logit 20 + k).  Result wave-uniform.
+// selected mean (logit 10 + k) and log-scale (logit 20 + k).  The draws of all ten components are
+// formed beside the argmax (lanes 5..9 hold the means of k = 2(jp − 5) + {0, 1}, row_shl:5 brings
+// the matching log-scales from lanes 10..14), so only a lane read follows it.  Result wave-uniform.
 __device__ __forceinline__ float mol_sample_pairs(float la, float lb, float ua, float ub, float u10, int jp) {
+    const float sa = fmaxf(WRNN_DPP(la, 0x105), -32.23619130191664f);   // row_shl:5: lane jp + 5
+    const float sb = fmaxf(WRNN_DPP(lb, 0x105), -32.23619130191664f);
+#if WRNN_XCD_FAST_EXP
+    float xa = la + fast_exp(sa) * u10, xb = lb + fast_exp(sb) * u10;
+#else
+    float xa = la + expf(sa) * u10, xb = lb + expf(sb) * u10;
+#endif
+    xa = xa < -1.0f ? -1.0f : xa;
+    xa = xa > 1.0f ? 1.0f : xa;
+    xb = xb < -1.0f ? -1.0f : xb;
+    xb = xb > 1.0f ? 1.0f : xb;
     float v = -INFINITY;
     int i = 64;
     if (jp < 5) {
@@ -94,18 +107,7 @@ __device__ __forceinline__ float mol_sample_pairs(float la, float lb, float ua, 
     WRNN_AM_STAGE(0xB1) WRNN_AM_STAGE(0x4E) WRNN_AM_STAGE(0x141) WRNN_AM_STAGE(0x140)
 #undef WRNN_AM_STAGE
     const int k = __builtin_amdgcn_readlane(i, 0);
-    const int km = (10 + k) >> 1, ks = (20 + k) >> 1;     // lanes of logits 10 + k, 20 + k (same parity as k)
-    const float ma = lane_bcast(la, km), mb = lane_bcast(lb, km), sa = lane_bcast(la, ks), sb = lane_bcast(lb, ks);
-    const float mean = (k & 1) ? mb : ma;
-    const float ls = fmaxf((k & 1) ? sb : sa, -32.23619130191664f);
-#if WRNN_XCD_FAST_EXP
-    float x = mean + fast_exp(ls) * u10;
-#else
-    float x = mean + expf(ls) * u10;
-#endif
-    x = x < -1.0f ? -1.0f : x;
-    x = x > 1.0f ? 1.0f : x;
-    return x;
+    return lane_bcast((k & 1) ? xb : xa, 5 + (k >> 1));
 }
 
 // 32-lane dot engine: a wave is two engines (e = lane >> 5), each computing one 512-long row per
