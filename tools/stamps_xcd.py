@@ -14,9 +14,10 @@ from wavernn_amd import synthetic as syn  # noqa: E402
 from wavernn_amd.loop import FatchordLoop  # noqa: E402
 
 STAMPS = [(0, "start (after B1)"), (1, "GRU1 done (after B2)"), (2, "Y published (GRU2)"), (3, "w1: Y gathered"),
-          (4, "w1: f1 published"), (5, "w3: F1 gathered"), (9, "w3: fc2 rows done"), (13, "w3: fc3 partials done"),
-          (14, "w3: wave 4's partials in"), (6, "w3: F2 published"), (7, "F2 gathered"), (8, "sample done"),
-          (10, "w6: h2 gathered"), (11, "w1: S quarter + GH2 done"), (12, "w7: ring done")]
+          (4, "w1: f1 published"), (5, "w3: F1 gathered"), (6, "w3: F2 published"), (7, "F2 gathered"),
+          (8, "sample done"), (9, "w3: GH1 terms published"), (10, "w6: h2 gathered"),
+          (14, "w5: S quarter gathered"), (12, "w7: ring done"), (11, "w1: S quarter + GH2 done"),
+          (13, "w5: GH2 done")]
 
 
 def main(L=3000):
