@@ -1087,7 +1087,8 @@ int generate_split(wrnn_t *h, const float *cond, int B, int L, const float *nois
     const double budget = (mb_env ? std::atof(mb_env) : 8192.0) * (1 << 20) / 4.0;   // floats
     const int Lc_max = (int)std::max(1.0, std::min((double)L, budget / (double)(N + h->KX) - 1.0));
     const char *rep_env = std::getenv("WRNN_REPLICAS");
-    // 4 replicas of every hand-off vector: 6.31 us/step vs 6.36 at 8, 6.45 at 2, 7.05 at 16 (MI355X, v8)
+    // 4 replicas of every hand-off vector (profiles/r02_split_rep_sweep.log, two rounds): 5.73/5.79 us/step
+    // vs 5.71/5.80 at 8, 5.75/5.90 at 2, 6.1-6.3 at 3, 6 and 16, 7.2 at 32; every count parity-green
     const int reps = std::max(1, std::min(32, rep_env ? std::atoi(rep_env) : 4));
     const long long vec_max = std::max<long long>({(long long)kTermsPerUnit * R, (long long)R, (long long)c.fc_dims,
                                                    (long long)(R / kSplitUnits) * kYLine,
