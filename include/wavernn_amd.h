@@ -87,8 +87,10 @@ typedef struct {
                                                   the GRU weights are block-sparse, else 0 */
     int32_t split_grid;      /* batch-1 MoL role-split kernel: GRU + FC workgroups (0: unavailable) */
     int32_t last_path;       /* kernel of the last wrnn_generate: 1 latency, 2 multi-row,
-                                3 deepmind, 4 role-split, 5 XCD-resident (0: none yet) */
-    int32_t xcd_rows;        /* XCD-resident kernel: rows per launch (0: unavailable)          */
+                                3 deepmind, 4 role-split, 5 XCD-resident, 6 XCD-resident
+                                block-sparse rnn 896 (0: none yet) */
+    int32_t xcd_rows;        /* XCD-resident kernel (dense rnn 512, or rnn 896 with block-sparse
+                                GRU weights once they are set): rows per launch (0: unavailable) */
 } wrnn_info;
 
 /* Create a handle on `device` (replaces WaveRNN.__init__ for the loop's dims,

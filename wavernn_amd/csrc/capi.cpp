@@ -20,6 +20,7 @@
 #include "deepmind_rows.h"
 #include "fatchord_split.h"
 #include "fatchord_xcd.h"
+#include "fatchord_xcds.h"
 
 namespace wrnn {
 hipError_t launch_ci_gemm(const float *cond, int CD, int Bt, int b0, int Bc, int t0, int L, const float *W, int ldw,
@@ -43,6 +44,9 @@ bool split_has_kernel(int R, int F);
 hipError_t launch_xcd(const XcdArgs &a, hipStream_t st);
 hipError_t prepare_xcd_kernel(int max_lds_bytes);
 hipError_t xcd_occupancy(int *blocks_per_cu);
+hipError_t launch_xcds(const XcdsArgs &a, hipStream_t st);
+hipError_t prepare_xcds_kernel(int max_lds_bytes);
+hipError_t xcds_occupancy(int *blocks_per_cu);
 }  // namespace wrnn
 
 using namespace wrnn;
@@ -101,7 +105,7 @@ struct wrnn_ctx {
     // r* fields above while in use
     RowsPart g2{};
     rocblas_handle blas = nullptr;
-    int last_path = 0;                              // 1 = latency, 2 = rows, 3 = deepmind, 4 = split, 5 = xcd
+    int last_path = 0;                              // 1 = latency, 2 = rows, 3 = deepmind, 4 = split, 5 = xcd, 6 = xcd sparse
     // deepmind_version (WRNN_MODE_DM): deepmind_rows.hip
     DmSlab ds{};
     int dmU = 0, dmUO = 0, dmUO2 = 0;
@@ -124,6 +128,11 @@ struct wrnn_ctx {
     size_t xstate_cap = 0;
     unsigned long long *d_xgx = nullptr;
     int *d_members = nullptr;
+    // XCD-resident MoL kernel for rnn 896 with 4x4 block-sparse GRU weights: fatchord_xcds.hip
+    // (shares the d_x* buffers: the dense one needs rnn 512); cap = dims and device fit, ok =
+    // the loaded weights are block-sparse with <= kSNB nonzero blocks per gate block-row
+    bool xcds_cap = false, xcds_ok = false;
+    XcdsSlab xss{};
 };
 
 namespace {
@@ -802,6 +811,125 @@ void pack_xcd_terms_weights(const wrnn_ctx &h, std::vector<float> &Wt) {
     }
 }
 
+
+// ---- XCD-resident block-sparse kernel (fatchord_xcds.h): workgroup c of an XCD owns units
+// 28c..28c+27 (block-rows ub = 0..6 of each gate) and fc rows 16c..16c+15
+void make_xcds_slab(wrnn_ctx &h) {
+    int o = 0;
+    auto take = [&](int n) { int at = o; o += round4(n); return at; };
+    XcdsSlab &x = h.xss;
+    x.wih2b = take(kSBR * kSNB * 16);
+    x.whh1b = take(kSBR * kSNB * 16);
+    x.whh2b = take(kSBR * kSNB * 16);
+    x.wih2c = take(kSBR * kSNB);
+    x.whh1c = take(kSBR * kSNB);
+    x.whh2c = take(kSBR * kSNB);
+    x.w1 = take(kXFcRows * kSR);
+    x.w2 = take(kXFcRows * 512);
+    x.w3 = take(kXFcRows * 32);
+    x.q1a = take(3 * kSR);
+    x.cst = take(kSCst);
+    x.total = o;
+}
+
+// nonzero 4x4 blocks of the gate block-row (q, 4-unit group u4) of a loop matrix
+std::vector<int> xcds_blocks(const LoopMat &m, int q, int u4) {
+    std::vector<int> cols;
+    for (int cb = 0; cb < kSR; cb += 4)
+        if (block_nonzero(m.w, m.ld, q * kSR + 4 * u4, cb)) cols.push_back(cb / 4);
+    return cols;
+}
+
+// largest nonzero-block count over every gate block-row of W_ih2[:, :R], W_hh1, W_hh2
+int xcds_nbmax(const wrnn_ctx &h) {
+    LoopMat m[3];
+    loop_mats(h, m);
+    int mx = 0;
+    for (int k = 0; k < 3; ++k)
+        for (int q = 0; q < 3; ++q)
+            for (int u4 = 0; u4 < kSR / 4; ++u4) mx = std::max(mx, (int)xcds_blocks(m[k], q, u4).size());
+    return mx;
+}
+
+void pack_xcds_slab(const wrnn_ctx &h, std::vector<float> &slab) {
+    const int R = kSR, F = h.cfg.fc_dims, A = h.cfg.aux_dims, NC = h.cfg.n_classes;
+    auto W = [&](const char *n) { return h.w.at(n).data(); };
+    const float *IW = W("I.weight");
+    const int nin = 1 + h.cfg.feat_dims + A;
+    const XcdsSlab &x = h.xss;
+    slab.assign((size_t)kXcdWgs * x.total, 0.0f);
+    std::vector<float> q1a(3 * R);
+    for (int r = 0; r < 3 * R; ++r) q1a[r] = xcol_dot(W("rnn1.weight_ih_l0") + (size_t)r * R, IW, nin, R);
+    LoopMat m[3];
+    loop_mats(h, m);
+    const int boff[3] = {x.wih2b, x.whh1b, x.whh2b}, coff[3] = {x.wih2c, x.whh1c, x.whh2c};
+    for (int c = 0; c < kXcdWgs; ++c) {
+        float *out = slab.data() + (size_t)c * x.total;
+        std::memcpy(out + x.q1a, q1a.data(), (size_t)3 * R * 4);
+        for (int k = 0; k < 3; ++k)
+            for (int q = 0; q < 3; ++q)
+                for (int ub = 0; ub < kSUB; ++ub) {
+                    const int br = q * kSUB + ub, u4 = c * kSUB + ub, r0 = q * R + 4 * u4;
+                    const std::vector<int> cols = xcds_blocks(m[k], q, u4);
+                    int *cc = reinterpret_cast<int *>(out + coff[k]) + br * kSNB;
+                    for (size_t n = 0; n < cols.size() && n < (size_t)kSNB; ++n) {
+                        float *blk = out + boff[k] + ((size_t)br * kSNB + n) * 16;
+                        for (int r = 0; r < 4; ++r)
+                            for (int cc4 = 0; cc4 < 4; ++cc4)
+                                blk[r * 4 + cc4] = m[k].w[(size_t)(r0 + r) * m[k].ld + 4 * cols[n] + cc4];
+                        cc[n] = cols[n];
+                    }
+                }
+        for (int r = 0; r < kXFcRows; ++r) {
+            const int j = c * kXFcRows + r;
+            std::memcpy(out + x.w1 + (size_t)r * R, W("fc1.weight") + (size_t)j * (R + A), R * 4);
+            std::memcpy(out + x.w2 + (size_t)r * F, W("fc2.weight") + (size_t)j * (F + A), F * 4);
+            for (int kk = 0; kk < NC; ++kk) out[x.w3 + r * 32 + kk] = W("fc3.weight")[(size_t)kk * F + j];
+        }
+        for (int u = 0; u < kSU; ++u) {
+            const int j = c * kSU + u;
+            out[x.cst + SC_WI0 + u] = IW[(size_t)j * nin];
+            for (int q = 0; q < 3; ++q) {
+                const int src = q * R + j, rr = u * 3 + q;
+                out[x.cst + SC_Q2 + rr] = xcol_dot(W("rnn2.weight_ih_l0") + (size_t)src * (R + A), IW, nin, R);
+                out[x.cst + SC_BIH1 + rr] = W("rnn1.bias_ih_l0")[src];
+                out[x.cst + SC_BHH1 + rr] = W("rnn1.bias_hh_l0")[src];
+                out[x.cst + SC_BIH2 + rr] = W("rnn2.bias_ih_l0")[src];
+                out[x.cst + SC_BHH2 + rr] = W("rnn2.bias_hh_l0")[src];
+            }
+        }
+        for (int kk = 0; kk < NC; ++kk) out[x.cst + SC_B3 + kk] = W("fc3.bias")[kk];
+    }
+}
+
+// Terms-GEMM weights [kXcdWgs·kSTerms][KX] against X = [cI | a2 a3 a4 | 1 0 0 0] (SXTerm slots)
+void pack_xcds_terms_weights(const wrnn_ctx &h, std::vector<float> &Wt) {
+    const int R = kSR, F = h.cfg.fc_dims, A = h.cfg.aux_dims, KX = h.KX;
+    auto W = [&](const char *n) { return h.w.at(n).data(); };
+    Wt.assign((size_t)kXcdWgs * kSTerms * KX, 0.0f);
+    for (int c = 0; c < kXcdWgs; ++c) {
+        auto row = [&](int slot) { return Wt.data() + ((size_t)c * kSTerms + slot) * KX; };
+        for (int u = 0; u < kSU; ++u) {
+            const int j = c * kSU + u;
+            for (int q = 0; q < 3; ++q) {
+                const int src = q * R + j;
+                std::memcpy(row(SX_P1 + u * 3 + q), W("rnn1.weight_ih_l0") + (size_t)src * R, R * 4);
+                const float *ih2 = W("rnn2.weight_ih_l0") + (size_t)src * (R + A);
+                std::memcpy(row(SX_P2 + u * 3 + q), ih2, R * 4);
+                std::memcpy(row(SX_P2 + u * 3 + q) + R, ih2 + R, A * 4);          // a2
+            }
+            row(SX_CI + u)[j] = 1.0f;                                            // cI_j itself
+        }
+        for (int r = 0; r < kXFcRows; ++r) {
+            const int j = c * kXFcRows + r;
+            float *v1 = row(SX_V1 + r), *v2 = row(SX_V2 + r);
+            std::memcpy(v1 + R + A, W("fc1.weight") + (size_t)j * (R + A) + R, A * 4);       // a3
+            v1[R + 3 * A] = W("fc1.bias")[j];
+            std::memcpy(v2 + R + 2 * A, W("fc2.weight") + (size_t)j * (F + A) + F, A * 4);   // a4
+            v2[R + 3 * A] = W("fc2.bias")[j];
+        }
+    }
+}
 }  // namespace
 
 namespace {
@@ -1224,6 +1352,77 @@ int generate_xcd(wrnn_t *h, const float *cond, int B, int L, const float *noise,
     return WRNN_OK;
 }
 
+// MoL rows (rnn 896, block-sparse GRU) through the XCD-resident sparse kernel: as generate_xcd.
+int generate_xcds(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed, int64_t row_offset,
+                  float *out, hipStream_t st) {
+    const wrnn_config &c = h->cfg;
+    const int R = c.rnn_dims, A = c.aux_dims, N = kXcdWgs * kSTerms;
+    if (!h->blas && rocblas_create_handle(&h->blas) != rocblas_status_success)
+        return fail(h, WRNN_EHIP, "rocblas_create_handle failed");
+    if (rocblas_set_stream(h->blas, st) != rocblas_status_success) return fail(h, WRNN_EHIP, "rocblas_set_stream failed");
+    const char *mb_env = std::getenv("WRNN_TERMS_MB");
+    const double budget = (mb_env ? std::atof(mb_env) : 8192.0) * (1 << 20) / 4.0;   // floats
+    const size_t xg_words = (size_t)kXcds * kXXcdStride;
+    if (!h->d_members) {
+        HIP_TRY(h, hipMalloc(&h->d_members, kXcds * sizeof(int)));
+        HIP_TRY(h, hipMalloc(&h->d_xgx, xg_words * 8));
+    }
+    const char *dbg_env = std::getenv("WRNN_DEBUG_STAMPS");
+    const int dbg_steps = dbg_env ? std::min(L, std::atoi(dbg_env)) : 0;
+    unsigned *d_dbg = nullptr;
+    int dbg_G = 0;
+    const float one = 1.0f, zero = 0.0f;
+    for (int b0 = 0; b0 < B; b0 += kXcds) {
+        const int nb = std::min(kXcds, B - b0);
+        const int Lc_max = (int)std::max(1.0, std::min((double)L, budget / ((double)nb * (N + h->KX)) - 1.0));
+        if (grow(h, h->d_X, h->X_cap, (size_t)(Lc_max + 1) * nb * h->KX) ||
+            grow(h, h->d_T, h->T_cap, (size_t)(Lc_max + 1) * nb * N) ||
+            grow(h, h->d_xstate, h->xstate_cap, (size_t)nb * kXcdWgs * kSStateW))
+            return WRNN_EHIP;
+        if (dbg_steps > 0 && !d_dbg) {
+            dbg_G = nb * kXcdWgs;
+            HIP_TRY(h, hipMalloc(&d_dbg, (size_t)dbg_G * dbg_steps * kStamps * 4));
+            HIP_TRY(h, hipMemsetAsync(d_dbg, 0, (size_t)dbg_G * dbg_steps * kStamps * 4, st));
+        }
+        HIP_TRY(h, hipMemsetAsync(h->d_xgx, 0, (size_t)nb * kXXcdStride * 8, st));   // tags restart at 1
+        for (int t0 = 0; t0 < L; t0 += Lc_max) {
+            const int Lc = std::min(Lc_max, L - t0);
+            const int rows = std::min(Lc + 1, L - t0);     // terms rows: steps [t0, t0 + rows)
+            HIP_TRY(h, launch_ci_gemm(cond, h->CD, B, b0, nb, t0, rows, h->d_IW, 1 + c.feat_dims + A, h->d_Ib, R,
+                                      c.feat_dims + A, h->d_X, h->KX, st));
+            HIP_TRY(h, launch_pack_terms_input(cond, h->CD, B, b0, nb, t0, rows, c.feat_dims, A, R, h->KX, h->d_X, st));
+            if (rocblas_sgemm(h->blas, rocblas_operation_transpose, rocblas_operation_none, N, rows * nb, h->KX, &one,
+                              h->d_xWt, h->KX, h->d_X, h->KX, &zero, h->d_T, N) != rocblas_status_success)
+                return fail(h, WRNN_EHIP, "rocblas_sgemm (conditioning terms) failed");
+            HIP_TRY(h, hipMemsetAsync(h->d_members, 0, kXcds * sizeof(int), st));
+            XcdsArgs a{};
+            a.slab = h->d_xslab;
+            a.terms = h->d_T;
+            a.noise = noise;
+            a.out = out;
+            a.state = h->d_xstate;
+            a.xg = h->d_xgx;
+            a.members = h->d_members;
+            a.ctl = h->d_ctl;
+            a.seed = seed;
+            a.row0 = row_offset + b0;
+            a.timeout_ticks = h->timeout_ticks;
+            a.L = L;
+            a.t0 = t0;
+            a.Lc = Lc;
+            a.Bt = B;
+            a.b0 = b0;
+            a.nb = nb;
+            a.s = h->xss;
+            a.dbg = (b0 == 0 && t0 == 0) ? d_dbg : nullptr;
+            a.dbg_steps = std::min(dbg_steps, Lc);
+            HIP_TRY(h, launch_xcds(a, st));
+        }
+    }
+    if (d_dbg) return dump_stamps(h, d_dbg, dbg_steps, st, dbg_G);
+    return WRNN_OK;
+}
+
 int generate_latency(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed,
                      int64_t row_offset, float *out, int32_t *labels, hipStream_t st) {
     const wrnn_config &c = h->cfg;
@@ -1447,6 +1646,15 @@ int wrnn_create(const wrnn_config *cfg, int device, wrnn_t **out) {
         HIP_TRY(h, xcd_occupancy(&per_cu));
         h->xcd_ok = per_cu >= 1;
     }
+    // MoL rnn 896 / fc 512: the XCD-resident block-sparse kernel, if the weights turn out
+    // block-sparse (decided at wrnn_set_weights)
+    if (mol && c.grid <= 0 && R == kSR && F == 512 && c.aux_dims == 32 && h->num_cus == kXcds * kXcdWgs &&
+        xcds_lds_layout().total * sizeof(float) <= (size_t)h->max_lds) {
+        make_xcds_slab(*h);
+        HIP_TRY(h, prepare_xcds_kernel(h->max_lds));
+        HIP_TRY(h, xcds_occupancy(&per_cu));
+        h->xcds_cap = per_cu >= 1;
+    }
     h->timeout_ticks = (long long)(c.timeout_ms > 0 ? c.timeout_ms : 2000) * 100000LL;   // 100 MHz
     HIP_TRY(h, hipMalloc(&h->d_ctl, kCtlWords * sizeof(int)));
     HIP_TRY(h, hipMemset(h->d_ctl, 0, kCtlWords * sizeof(int)));
@@ -1571,6 +1779,23 @@ int wrnn_set_weights(wrnn_t *h, const wrnn_tensor *tensors, int n) {
             HIP_TRY(h, hipMemcpy(*pr.first, pr.second->data(), pr.second->size() * 4, hipMemcpyHostToDevice));
         }
     }
+    h->xcds_ok = false;
+    if (h->xcds_cap) {
+        const char *sp_env = std::getenv("WRNN_SPARSE");
+        const int nbmax = (sp_env && std::string(sp_env) == "0") ? kSNB + 1 : xcds_nbmax(*h);
+        if (h->sparse && nbmax <= kSNB) {
+            std::vector<float> slab, Wt;
+            pack_xcds_slab(*h, slab);
+            pack_xcds_terms_weights(*h, Wt);
+            for (auto pr : {std::make_pair(&h->d_xslab, &slab), std::make_pair(&h->d_xWt, &Wt)}) {
+                if (*pr.first) HIP_TRY(h, hipFree(*pr.first));
+                *pr.first = nullptr;
+                HIP_TRY(h, hipMalloc(pr.first, pr.second->size() * 4));
+                HIP_TRY(h, hipMemcpy(*pr.first, pr.second->data(), pr.second->size() * 4, hipMemcpyHostToDevice));
+            }
+            h->xcds_ok = true;
+        }
+    }
     h->ready = true;
     return WRNN_OK;
 }
@@ -1598,12 +1823,15 @@ int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise
     // MoL rnn / fc 512 up to kXcdDefaultRows rows: the XCD-resident kernel (8 rows per launch;
     // beyond that the multi-row kernel's throughput wins)
     const bool xcd = h->xcd_ok && (pe == "xcd" || (pe.empty() && B <= kXcdDefaultRows));
-    const bool split = !xcd && h->split_ok && (pe == "split" || (pe.empty() && B == 1));
+    // MoL rnn 896 with block-sparse GRU weights likewise: the XCD-resident sparse kernel
+    const bool xcds = !xcd && h->xcds_ok && (pe == "xcd" || (pe.empty() && B <= kXcdDefaultRows));
+    const bool split = !xcd && !xcds && h->split_ok && (pe == "split" || (pe.empty() && B == 1));
     HIP_TRY(h, hipMemsetAsync(h->d_ctl, 0, kCtlWords * sizeof(int), st));
     HIP_TRY(h, hipEventRecord(h->ev0, st));
-    h->last_path = h->dm ? 3 : xcd ? 5 : split ? 4 : rows ? 2 : 1;
+    h->last_path = h->dm ? 3 : xcd ? 5 : xcds ? 6 : split ? 4 : rows ? 2 : 1;
     const int rc = h->dm    ? generate_dm(h, B, L, noise, seed, row_offset, out, labels, st)
                    : xcd   ? generate_xcd(h, cond, B, L, noise, seed, row_offset, out, st)
+                   : xcds  ? generate_xcds(h, cond, B, L, noise, seed, row_offset, out, st)
                    : split ? generate_split(h, cond, B, L, noise, seed, row_offset, out, st)
                    : rows  ? generate_rows(h, cond, B, L, noise, seed, row_offset, out, labels, st)
                            : generate_latency(h, cond, B, L, noise, seed, row_offset, out, labels, st);
@@ -1627,7 +1855,7 @@ int wrnn_check(wrnn_t *h, void *stream) {
                                         "coarse label", "fine label"};
         static const char *split_hops[] = {"y", "f1", "f2", "h2", "h2", "gru1-terms", "gru1-terms"};
         static const char *xcd_hops[] = {"y", "f1", "f2", "h2", "gru1-terms", "gru1-terms"};
-        const char *name = h->last_path == 5   ? (hop >= 0 && hop < 6 ? xcd_hops[hop] : "?")
+        const char *name = h->last_path >= 5   ? (hop >= 0 && hop < 6 ? xcd_hops[hop] : "?")
                            : h->last_path == 4 ? (hop >= 0 && hop < 7 ? split_hops[hop] : "?")
                            : h->last_path == 3 ? (hop >= 0 && hop < 8 ? dm_hops[hop] : "?")
                            : h->last_path == 2 ? (hop >= 0 && hop < 6 ? row_hops[hop] : "?")
@@ -1678,7 +1906,7 @@ int wrnn_query(const wrnn_t *h, wrnn_info *info) {
     info->num_cus = h->num_cus;
     info->split_grid = h->split_ok ? h->sGg + h->sGf : 0;
     info->last_path = h->last_path;
-    info->xcd_rows = h->xcd_ok ? kXcds : 0;
+    info->xcd_rows = (h->xcd_ok || h->xcds_ok) ? kXcds : 0;
     return WRNN_OK;
 }
 

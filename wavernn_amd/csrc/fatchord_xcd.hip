@@ -34,6 +34,7 @@
 #include "fatchord_loop.h"
 #include "fatchord_xcd.h"
 #include "wrnn_device.h"
+#include "xcd_device.h"
 
 namespace wrnn {
 
@@ -44,228 +45,9 @@ namespace wrnn {
 #ifndef WRNN_XCD_SKIP_H2
 #define WRNN_XCD_SKIP_H2 0
 #endif
-#ifndef WRNN_XCD_FAST_EXP
-#define WRNN_XCD_FAST_EXP 1     // sampler scale e^s by v_exp_f32 (A/B vs libm expf: 3.92 -> 3.88 us/step, parity unchanged)
-#endif
 #ifndef WRNN_XCD_PRIO
 #define WRNN_XCD_PRIO 0         // s_setprio of wave 0 (the poller / sampler)
 #endif
-
-__device__ __forceinline__ unsigned xcc_id() {
-    return __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 0xF;   // HW_REG_XCC_ID[3:0]
-}
-
-// XCD-local publish: a plain (workgroup-scope) 8-byte store keeps the line in this XCD's L2
-__device__ __forceinline__ void xpub(unsigned long long *g, uint32_t tag, float v) {
-    const unsigned long long x = ((unsigned long long)tag << 32) | __float_as_uint(v);
-    __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-__device__ __forceinline__ float perm_sum16(float v) {   // + the same lane of the paired 16-lane row
-    const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return __uint_as_float(s[0]) + __uint_as_float(s[1]);
-}
-__device__ __forceinline__ float perm_sum32(float v) {   // + the same lane of the other wave half
-    const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return __uint_as_float(s[0]) + __uint_as_float(s[1]);
-}
-// Σ over the 4 DPP rows of a wave (identical bits in the lanes it pairs)
-__device__ __forceinline__ float cross_rows(float v) { return perm_sum32(perm_sum16(v)); }
-
-// MoL sampler (utils/distribution.py:87-123) on logits held in pairs: lane jp (of every DPP row)
-// holds logits 2jp (la) and 2jp+1 (lb); ua / ub = log(-log u1) of those mixture indices (jp < 5).
-// k = argmax over the 10 logit_probs − u (first max on ties), then the logistic draw with the
-// selected mean (logit 10 + k) and log-scale (logit 20 + k).  The draws of all ten components are
-// formed beside the argmax (lanes 5..9 hold the means of k = 2(jp − 5) + {0, 1}, row_shl:5 brings
-// the matching log-scales from lanes 10..14), so only a lane read follows it.  Result wave-uniform.
-__device__ __forceinline__ float mol_sample_pairs(float la, float lb, float ua, float ub, float u10, int jp) {
-    const float sa = fmaxf(WRNN_DPP(la, 0x105), -32.23619130191664f);   // row_shl:5: lane jp + 5
-    const float sb = fmaxf(WRNN_DPP(lb, 0x105), -32.23619130191664f);
-#if WRNN_XCD_FAST_EXP
-    float xa = la + fast_exp(sa) * u10, xb = lb + fast_exp(sb) * u10;
-#else
-    float xa = la + expf(sa) * u10, xb = lb + expf(sb) * u10;
-#endif
-    xa = xa < -1.0f ? -1.0f : xa;
-    xa = xa > 1.0f ? 1.0f : xa;
-    xb = xb < -1.0f ? -1.0f : xb;
-    xb = xb > 1.0f ? 1.0f : xb;
-    float v = -INFINITY;
-    int i = 64;
-    if (jp < 5) {
-        const float va = la - ua, vb = lb - ub;
-        const bool hi = vb > va;                    // tie → the smaller index
-        v = hi ? vb : va;
-        i = 2 * jp + (hi ? 1 : 0);
-    }
-#define WRNN_AM_STAGE(ctrl)                                                           \
-    {                                                                                 \
-        float ov = WRNN_DPP(v, ctrl);                                                 \
-        int oi = __builtin_amdgcn_mov_dpp(i, (ctrl), 0xF, 0xF, false);                \
-        am_merge(v, i, ov, oi);                                                       \
-    }
-    WRNN_AM_STAGE(0xB1) WRNN_AM_STAGE(0x4E) WRNN_AM_STAGE(0x141) WRNN_AM_STAGE(0x140)
-#undef WRNN_AM_STAGE
-    const int k = __builtin_amdgcn_readlane(i, 0);
-    return lane_bcast((k & 1) ? xb : xa, 5 + (k >> 1));
-}
-
-// 32-lane dot engine: a wave is two engines (e = lane >> 5), each computing one 512-long row per
-// pass; lane li = lane & 31 of an engine holds the float4 chunks li + 32m (m = 0..3) of its row
-// (16 weights) and reads the same chunks of x.  Packed FMAs, then Σ over the engine's 32 lanes:
-// row_sum16 (DPP, identical bits in its 16 lanes) + the paired DPP row (permlane16 swap).
-__device__ __forceinline__ float e32dot(const f4v (&w)[4], const f4v (&x)[4]) {
-    f2v a = __builtin_elementwise_fma(w[0].xy, x[0].xy, f2v{0.0f, 0.0f});
-    f2v b = __builtin_elementwise_fma(w[1].xy, x[1].xy, f2v{0.0f, 0.0f});
-    a = __builtin_elementwise_fma(w[0].zw, x[0].zw, a);
-    b = __builtin_elementwise_fma(w[1].zw, x[1].zw, b);
-    a = __builtin_elementwise_fma(w[2].xy, x[2].xy, a);
-    b = __builtin_elementwise_fma(w[3].xy, x[3].xy, b);
-    a = __builtin_elementwise_fma(w[2].zw, x[2].zw, a);
-    b = __builtin_elementwise_fma(w[3].zw, x[3].zw, b);
-    const f2v s = a + b;
-    return perm_sum16(row_sum16(s.x + s.y));
-}
-
-__device__ __forceinline__ f4v lds4(const float *p) { return *reinterpret_cast<const f4v *>(p); }
-
-// x chunks of an engine lane (li = lane & 31) from a 512-float LDS vector
-__device__ __forceinline__ void e32x(const float *v, int li, f4v (&x)[4]) {
-#pragma unroll
-    for (int m = 0; m < 4; ++m) x[m] = lds4(v + 4 * (li + 32 * m));
-}
-
-// Poll NG granules per lane (indices lid + 64·k: one address per call site, instruction
-// immediates for k) until all carry `tag`, then store(i, value).  Bounded like wrnn_device.h:gather (timeout / another workgroup's abort).
-template <int NG, typename Store>
-__device__ __forceinline__ void xgather(const unsigned long long *g, uint32_t tag, int *ctl, long long timeout,
-                                        int step, int hop, int *lds_abort, int lid, Store store) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    unsigned spins = 0;
-    for (;;) {
-        unsigned long long v[NG];
-#pragma unroll
-        for (int k = 0; k < NG; ++k) v[k] = __hip_atomic_load(g + lid + 64 * k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        bool ok = true;
-#pragma unroll
-        for (int k = 0; k < NG; ++k) ok &= (uint32_t)(v[k] >> 32) == tag;
-        if (ok) {
-#pragma unroll
-            for (int k = 0; k < NG; ++k) store(lid + 64 * k, __uint_as_float((uint32_t)v[k]));
-            return;
-        }
-        if ((++spins & 63u) == 0) {
-            const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - t0) > timeout;
-            const bool other = __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-            if (late || other) {
-                if (late) record_abort(ctl, -4, step, hop, blockIdx.x);
-                *lds_abort = 1;
-                return;
-            }
-        }
-    }
-}
-
-
-typedef unsigned u4v __attribute__((ext_vector_type(4)));
-
-// A hop vector as a raw buffer: 16-byte sc1 loads (two granules each, every 8-byte half untorn:
-// MI355X_MICROARCH.md hand-off table), lane offset + instruction immediate
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t hop_rsrc(const unsigned long long *g) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned long long *>(g), 0, 0x7fffffff, 0x00020000);
-}
-__device__ __forceinline__ u4v ld16_sc1(__amdgpu_buffer_rsrc_t r, int off) {
-    return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16 /* sc1 */);
-}
-
-// Poll NP·128 granules (pairs l + 64k, k < NP) with 16-byte loads until every granule carries
-// `tag`, then store2(i, v_i, v_i+1) for each pair's first granule index i.  Bounded.
-template <int NP, typename Store2>
-__device__ __forceinline__ void xgather16(const unsigned long long *g, uint32_t tag, int *ctl, long long timeout,
-                                          int step, int hop, int *lds_abort, int lid, Store2 store2) {
-    const __amdgpu_buffer_rsrc_t r = hop_rsrc(g);
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    unsigned spins = 0;
-    for (;;) {
-        u4v v[NP];
-#pragma unroll
-        for (int k = 0; k < NP; ++k) v[k] = ld16_sc1(r, 16 * (lid + 64 * k));
-        bool ok = true;
-#pragma unroll
-        for (int k = 0; k < NP; ++k) ok &= (v[k].y == tag) & (v[k].w == tag);
-        if (ok) {
-#pragma unroll
-            for (int k = 0; k < NP; ++k) store2(2 * (lid + 64 * k), __uint_as_float(v[k].x), __uint_as_float(v[k].z));
-            return;
-        }
-        if ((++spins & 63u) == 0) {
-            const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - t0) > timeout;
-            const bool other = __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-            if (late || other) {
-                if (late) record_abort(ctl, -4, step, hop, blockIdx.x);
-                *lds_abort = 1;
-                return;
-            }
-        }
-    }
-}
-
-// Poll NP·128 granules (pairs l + 64k) with 16-byte loads until every granule carries `tag`;
-// the pairs stay in registers (v[k].x, v[k].z).  Bounded; on abort the values are garbage.
-template <int NP>
-__device__ __forceinline__ void xpoll16(const unsigned long long *g, uint32_t tag, int *ctl, long long timeout,
-                                        int step, int hop, int *lds_abort, int lid, u4v (&v)[NP]) {
-    const __amdgpu_buffer_rsrc_t r = hop_rsrc(g);
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    unsigned spins = 0;
-    for (;;) {
-#pragma unroll
-        for (int k = 0; k < NP; ++k) v[k] = ld16_sc1(r, 16 * (lid + 64 * k));
-        bool ok = true;
-#pragma unroll
-        for (int k = 0; k < NP; ++k) ok &= (v[k].y == tag) & (v[k].w == tag);
-        if (ok) return;
-        if ((++spins & 63u) == 0) {
-            const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - t0) > timeout;
-            const bool other = __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-            if (late || other) {
-                if (late) record_abort(ctl, -4, step, hop, blockIdx.x);
-                *lds_abort = 1;
-                return;
-            }
-        }
-    }
-}
-
-// 8 rows of a 512-wide layer against a vector polled into registers by ONE wave (no LDS, no
-// barrier): lane l holds the pairs k = 0..3 at granules 2(l + 64k) + {0, 1} (xk[k]) and the
-// matching weights of row r in w[2r + k/2] (.xy for even k, .zw for odd).  Packed FMAs, then a
-// reduce-scatter over the wave — permlane32 swap (row r vs r + 4), permlane16 swap (r vs r + 2),
-// DPP sum over the 16 lanes of a row — leaves in o[j] the full sum of row j + 2·(l >> 4),
-// identical bits in all 16 lanes of DPP row l >> 4.
-__device__ __forceinline__ void fc8_rows(const f4v (&w)[16], const f2v (&xk)[4], float (&o)[2]) {
-    float s[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-        f2v acc = __builtin_elementwise_fma(w[2 * r].xy, xk[0], f2v{0.0f, 0.0f});
-        f2v acc2 = __builtin_elementwise_fma(w[2 * r].zw, xk[1], f2v{0.0f, 0.0f});
-        acc = __builtin_elementwise_fma(w[2 * r + 1].xy, xk[2], acc);
-        acc2 = __builtin_elementwise_fma(w[2 * r + 1].zw, xk[3], acc2);
-        const f2v t = acc + acc2;
-        s[r] = t.x + t.y;
-    }
-    float h[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {   // lanes < 32 keep row j, lanes ≥ 32 row j + 4
-        const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(s[j]), __float_as_uint(s[j + 4]), false, false);
-        h[j] = __uint_as_float(q[0]) + __uint_as_float(q[1]);
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {   // even DPP rows keep h[j], odd rows h[j + 2]
-        const auto q = __builtin_amdgcn_permlane16_swap(__float_as_uint(h[j]), __float_as_uint(h[j + 2]), false, false);
-        o[j] = row_sum16(__uint_as_float(q[0]) + __uint_as_float(q[1]));
-    }
-}
 
 #define XSTAMPW(kk, w)                                                                                        \
     do {                                                                                                      \
