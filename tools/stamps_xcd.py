@@ -2,7 +2,7 @@
 (s_memrealtime, 100 MHz, wave 0 of every workgroup).  For each step, times are relative to the
 earliest step start over the XCD's 32 workgroups; the table gives the median over steps of the
 min / median / max over the workgroups.
-    python tools/stamps_xcd.py [L]"""
+    python tools/stamps_xcd.py [L] [sparse]     (sparse: the rnn-896 block-sparse kernel, fatchord_xcds.hip)"""
 import os
 import sys
 
@@ -13,6 +13,10 @@ import torch  # noqa: E402
 from wavernn_amd import synthetic as syn  # noqa: E402
 from wavernn_amd.loop import FatchordLoop  # noqa: E402
 
+SPARSE_STAMPS = [(0, "start (after B1)"), (1, "GRU1 done (after B2)"), (2, "Y published (GRU2)"),
+                 (3, "w6: Y gathered"), (4, "w6: f1 published"), (5, "w4: F1 gathered"), (6, "w4: F2 published"),
+                 (7, "F2 gathered"), (8, "sample done"), (9, "w1: GH1 terms + h2 published"),
+                 (10, "w7: h2 gathered"), (11, "w1: S quarter gathered"), (12, "w7: ring done"), (13, "w1: GH2 done")]
 STAMPS = [(0, "start (after B1)"), (1, "GRU1 done (after B2)"), (2, "Y published (GRU2)"), (3, "w1: Y gathered"),
           (4, "w1: f1 published"), (5, "w3: F1 gathered"), (6, "w3: F2 published"), (7, "F2 gathered"),
           (8, "sample done"), (9, "w3: GH1 terms published"), (10, "w6: h2 gathered"),
@@ -20,15 +24,19 @@ STAMPS = [(0, "start (after B1)"), (1, "GRU1 done (after B2)"), (2, "Y published
           (13, "w5: GH2 done")]
 
 
-def main(L=3000):
+def main(L=3000, sparse=0):
     os.makedirs("gpurun_out", exist_ok=True)
     path = "gpurun_out/stamps_xcd.bin"
     os.environ["WRNN_DEBUG_STAMPS"] = str(L)
     os.environ["WRNN_DEBUG_FILE"] = path
     os.environ["WRNN_PATH"] = "xcd"
-    d = syn.DEFAULT_MOL
+    d = syn.SPARSE896_MOL if sparse else syn.DEFAULT_MOL
     loop = FatchordLoop(d.mode, d.rnn_dims, d.fc_dims, d.aux_dims, d.feat_dims, d.n_classes)
-    loop.set_weights(syn.make_fatchord_state(d, 0))
+    state = syn.make_fatchord_state(d, 0)
+    if sparse:
+        from wavernn_amd.pruning import prune_state
+        state = prune_state(state, 0.95)
+    loop.set_weights(state)
     mels, aux = syn.make_conditioning(1, L, d.feat_dims, d.res_out_dims, 5)
     cond = torch.from_numpy(np.concatenate([mels, aux], 2).transpose(1, 0, 2).copy()).cuda()
     loop.generate(cond, seed=1)
@@ -42,7 +50,7 @@ def main(L=3000):
     print(f"xcd kernel L={L}: step period median {np.median(period):.3f} us (stamped build), "
           f"shader clock {np.median(clk):.3f} GHz (s_memtime / s_memrealtime)")
     print("-- median over steps of (min / median / max over the 32 workgroups), us")
-    for k, lab in STAMPS:
+    for k, lab in (SPARSE_STAMPS if sparse else STAMPS):
         x = rel[:, :, k]
         print(f"   {lab:28s} {np.median(x.min(0)):6.2f} {np.median(np.median(x, 0)):6.2f} {np.median(x.max(0)):6.2f}")
 

@@ -25,6 +25,8 @@
 namespace wrnn {
 hipError_t launch_ci_gemm(const float *cond, int CD, int Bt, int b0, int Bc, int t0, int L, const float *W, int ldw,
                           const float *bias, int N, int K, float *cI, int ldc, hipStream_t st);
+hipError_t launch_pack_cond_input(const float *cond, int CD, int Bt, int b0, int B, int t0, int Lc, int KX, float *X,
+                                  hipStream_t st);
 hipError_t launch_pack_terms_input(const float *cond, int CD, int Bt, int b0, int B, int t0, int Lc, int feat, int A,
                                    int R, int KX, float *X, hipStream_t st);
 hipError_t launch_rows(const RowsArgs &a, const RowsGroup *g1, size_t lds_bytes, hipStream_t st);
@@ -92,6 +94,7 @@ struct wrnn_ctx {
     int rU = 0, rG = 0, rUF = 0, rUC = 0;           // rows-kernel partition (U = 4 when sparse)
     bool sparse = false;                            // GRU weights stored as nonzero 4x4 blocks
     int NT = 0, KX = 0, KA = 0;
+    int KXc = 0;                                    // XCD kernels' terms-GEMM depth: [cond record | 1 0 0 0]
     bool rows_ok = false;                           // weights fit LDS with at least one row
     float *d_rslab = nullptr, *d_Wt = nullptr;      // per-workgroup slabs, terms-GEMM weights [G·NT][KX]
     float *d_X = nullptr, *d_T = nullptr, *d_act = nullptr, *d_state = nullptr;
@@ -785,32 +788,66 @@ void pack_xcd_slab(const wrnn_ctx &h, std::vector<float> &slab) {
     }
 }
 
-// Terms-GEMM weights [kXcdWgs·kXTerms][KX] against X = [cI | a2 a3 a4 | 1 0 0 0] (XTerm slots)
-void pack_xcd_terms_weights(const wrnn_ctx &h, std::vector<float> &Wt) {
-    const int R = h.cfg.rnn_dims, F = h.cfg.fc_dims, A = h.cfg.aux_dims, KX = h.KX;
+// The XCD kernels' terms-GEMM rows against X' = [mel | a1 | a2 | a3 | a4 | 1 0 0 0] (KXc = CD + 4):
+// the I layer (fatchord_version.py:208, cI = W_I·[mel; a1] + b_I; the x column is folded
+// separately, q1a / q2) is composed into the W_ih1 / W_ih2 rows in fp64 here, so the GEMM runs on
+// the 208-wide conditioning record instead of a 900-wide cI (4.7x less work at rnn 896).
+void fold_ci_row(const wrnn_ctx &h, const float *w, float *dst) {
+    const int R = h.cfg.rnn_dims, M = h.cfg.feat_dims, A = h.cfg.aux_dims, nin = 1 + M + A;
+    const float *IW = h.w.at("I.weight").data(), *Ib = h.w.at("I.bias").data();
+    std::vector<double> acc(M + A + 1, 0.0);
+    for (int k = 0; k < R; ++k) {
+        const double wk = w[k];
+        if (wk == 0.0) continue;
+        const float *iw = IW + (size_t)k * nin + 1;
+        for (int m = 0; m < M + A; ++m) acc[m] += wk * iw[m];
+        acc[M + A] += wk * Ib[k];
+    }
+    for (int m = 0; m < M + A; ++m) dst[m] += (float)acc[m];
+    dst[h.CD] += (float)acc[M + A];
+}
+
+// slot rows of one unit j (gates q = 0..2: p1q[q], p2q[q]; its cI: ci) and of one fc row r
+// (v1, v2) for the composed input X'
+void pack_xcd_unit_terms(const wrnn_ctx &h, int j, float *const p1q[3], float *const p2q[3], float *ci) {
+    const int R = h.cfg.rnn_dims, M = h.cfg.feat_dims, A = h.cfg.aux_dims, nin = 1 + M + A;
     auto W = [&](const char *n) { return h.w.at(n).data(); };
+    for (int q = 0; q < 3; ++q) {
+        const int src = q * R + j;
+        fold_ci_row(h, W("rnn1.weight_ih_l0") + (size_t)src * R, p1q[q]);
+        const float *ih2 = W("rnn2.weight_ih_l0") + (size_t)src * (R + A);
+        fold_ci_row(h, ih2, p2q[q]);
+        for (int a = 0; a < A; ++a) p2q[q][M + A + a] += ih2[R + a];                      // a2
+    }
+    const float *iw = W("I.weight") + (size_t)j * nin + 1;
+    for (int m = 0; m < M + A; ++m) ci[m] = iw[m];                                         // cI_j
+    ci[h.CD] = W("I.bias")[j];
+}
+void pack_xcd_fc_terms(const wrnn_ctx &h, int r, float *v1, float *v2) {
+    const int R = h.cfg.rnn_dims, F = h.cfg.fc_dims, M = h.cfg.feat_dims, A = h.cfg.aux_dims;
+    auto W = [&](const char *n) { return h.w.at(n).data(); };
+    for (int a = 0; a < A; ++a) {
+        v1[M + 2 * A + a] = W("fc1.weight")[(size_t)r * (R + A) + R + a];                 // a3
+        v2[M + 3 * A + a] = W("fc2.weight")[(size_t)r * (F + A) + F + a];                 // a4
+    }
+    v1[h.CD] = W("fc1.bias")[r];
+    v2[h.CD] = W("fc2.bias")[r];
+}
+
+// Terms-GEMM weights [kXcdWgs·kXTerms][KXc] (XTerm slots) against X'
+void pack_xcd_terms_weights(const wrnn_ctx &h, std::vector<float> &Wt) {
+    const int KX = h.KXc;
     Wt.assign((size_t)kXcdWgs * kXTerms * KX, 0.0f);
     for (int c = 0; c < kXcdWgs; ++c) {
         auto row = [&](int slot) { return Wt.data() + ((size_t)c * kXTerms + slot) * KX; };
         for (int u = 0; u < kXUnits; ++u) {
-            const int j = c * kXUnits + u;
-            for (int q = 0; q < 3; ++q) {
-                const int src = q * R + j;
-                std::memcpy(row(XT_P1 + u * 3 + q), W("rnn1.weight_ih_l0") + (size_t)src * R, R * 4);
-                const float *ih2 = W("rnn2.weight_ih_l0") + (size_t)src * (R + A);
-                std::memcpy(row(XT_P2 + u * 3 + q), ih2, R * 4);
-                std::memcpy(row(XT_P2 + u * 3 + q) + R, ih2 + R, A * 4);          // a2
-            }
-            row(XT_CI + u)[j] = 1.0f;                                            // cI_j itself
-            float *v1 = row(XT_V1 + u), *v2 = row(XT_V2 + u);
-            std::memcpy(v1 + R + A, W("fc1.weight") + (size_t)j * (R + A) + R, A * 4);       // a3
-            v1[R + 3 * A] = W("fc1.bias")[j];
-            std::memcpy(v2 + R + 2 * A, W("fc2.weight") + (size_t)j * (F + A) + F, A * 4);   // a4
-            v2[R + 3 * A] = W("fc2.bias")[j];
+            float *const p1q[3] = {row(XT_P1 + u * 3), row(XT_P1 + u * 3 + 1), row(XT_P1 + u * 3 + 2)};
+            float *const p2q[3] = {row(XT_P2 + u * 3), row(XT_P2 + u * 3 + 1), row(XT_P2 + u * 3 + 2)};
+            pack_xcd_unit_terms(h, c * kXUnits + u, p1q, p2q, row(XT_CI + u));
+            pack_xcd_fc_terms(h, c * kXUnits + u, row(XT_V1 + u), row(XT_V2 + u));
         }
     }
 }
-
 
 // ---- XCD-resident block-sparse kernel (fatchord_xcds.h): workgroup c of an XCD owns units
 // 28c..28c+27 (block-rows ub = 0..6 of each gate) and fc rows 16c..16c+15
@@ -902,34 +939,21 @@ void pack_xcds_slab(const wrnn_ctx &h, std::vector<float> &slab) {
     }
 }
 
-// Terms-GEMM weights [kXcdWgs·kSTerms][KX] against X = [cI | a2 a3 a4 | 1 0 0 0] (SXTerm slots)
+// Terms-GEMM weights [kXcdWgs·kSTerms][KXc] (SXTerm slots) against X' (pack_xcd_terms_weights)
 void pack_xcds_terms_weights(const wrnn_ctx &h, std::vector<float> &Wt) {
-    const int R = kSR, F = h.cfg.fc_dims, A = h.cfg.aux_dims, KX = h.KX;
-    auto W = [&](const char *n) { return h.w.at(n).data(); };
+    const int KX = h.KXc;
     Wt.assign((size_t)kXcdWgs * kSTerms * KX, 0.0f);
     for (int c = 0; c < kXcdWgs; ++c) {
         auto row = [&](int slot) { return Wt.data() + ((size_t)c * kSTerms + slot) * KX; };
         for (int u = 0; u < kSU; ++u) {
-            const int j = c * kSU + u;
-            for (int q = 0; q < 3; ++q) {
-                const int src = q * R + j;
-                std::memcpy(row(SX_P1 + u * 3 + q), W("rnn1.weight_ih_l0") + (size_t)src * R, R * 4);
-                const float *ih2 = W("rnn2.weight_ih_l0") + (size_t)src * (R + A);
-                std::memcpy(row(SX_P2 + u * 3 + q), ih2, R * 4);
-                std::memcpy(row(SX_P2 + u * 3 + q) + R, ih2 + R, A * 4);          // a2
-            }
-            row(SX_CI + u)[j] = 1.0f;                                            // cI_j itself
+            float *const p1q[3] = {row(SX_P1 + u * 3), row(SX_P1 + u * 3 + 1), row(SX_P1 + u * 3 + 2)};
+            float *const p2q[3] = {row(SX_P2 + u * 3), row(SX_P2 + u * 3 + 1), row(SX_P2 + u * 3 + 2)};
+            pack_xcd_unit_terms(h, c * kSU + u, p1q, p2q, row(SX_CI + u));
         }
-        for (int r = 0; r < kXFcRows; ++r) {
-            const int j = c * kXFcRows + r;
-            float *v1 = row(SX_V1 + r), *v2 = row(SX_V2 + r);
-            std::memcpy(v1 + R + A, W("fc1.weight") + (size_t)j * (R + A) + R, A * 4);       // a3
-            v1[R + 3 * A] = W("fc1.bias")[j];
-            std::memcpy(v2 + R + 2 * A, W("fc2.weight") + (size_t)j * (F + A) + F, A * 4);   // a4
-            v2[R + 3 * A] = W("fc2.bias")[j];
-        }
+        for (int r = 0; r < kXFcRows; ++r) pack_xcd_fc_terms(h, c * kXFcRows + r, row(SX_V1 + r), row(SX_V2 + r));
     }
 }
+
 }  // namespace
 
 namespace {
@@ -1303,8 +1327,8 @@ int generate_xcd(wrnn_t *h, const float *cond, int B, int L, const float *noise,
     const float one = 1.0f, zero = 0.0f;
     for (int b0 = 0; b0 < B; b0 += kXcds) {
         const int nb = std::min(kXcds, B - b0);
-        const int Lc_max = (int)std::max(1.0, std::min((double)L, budget / ((double)nb * (N + h->KX)) - 1.0));
-        if (grow(h, h->d_X, h->X_cap, (size_t)(Lc_max + 1) * nb * h->KX) ||
+        const int Lc_max = (int)std::max(1.0, std::min((double)L, budget / ((double)nb * (N + h->KXc)) - 1.0));
+        if (grow(h, h->d_X, h->X_cap, (size_t)(Lc_max + 1) * nb * h->KXc) ||
             grow(h, h->d_T, h->T_cap, (size_t)(Lc_max + 1) * nb * N) ||
             grow(h, h->d_xstate, h->xstate_cap, (size_t)nb * kXcdWgs * kXStateW))
             return WRNN_EHIP;
@@ -1317,11 +1341,9 @@ int generate_xcd(wrnn_t *h, const float *cond, int B, int L, const float *noise,
         for (int t0 = 0; t0 < L; t0 += Lc_max) {
             const int Lc = std::min(Lc_max, L - t0);
             const int rows = std::min(Lc + 1, L - t0);     // terms rows: steps [t0, t0 + rows)
-            HIP_TRY(h, launch_ci_gemm(cond, h->CD, B, b0, nb, t0, rows, h->d_IW, 1 + c.feat_dims + A, h->d_Ib, R,
-                                      c.feat_dims + A, h->d_X, h->KX, st));
-            HIP_TRY(h, launch_pack_terms_input(cond, h->CD, B, b0, nb, t0, rows, c.feat_dims, A, R, h->KX, h->d_X, st));
-            if (rocblas_sgemm(h->blas, rocblas_operation_transpose, rocblas_operation_none, N, rows * nb, h->KX, &one,
-                              h->d_xWt, h->KX, h->d_X, h->KX, &zero, h->d_T, N) != rocblas_status_success)
+            HIP_TRY(h, launch_pack_cond_input(cond, h->CD, B, b0, nb, t0, rows, h->KXc, h->d_X, st));
+            if (rocblas_sgemm(h->blas, rocblas_operation_transpose, rocblas_operation_none, N, rows * nb, h->KXc, &one,
+                              h->d_xWt, h->KXc, h->d_X, h->KXc, &zero, h->d_T, N) != rocblas_status_success)
                 return fail(h, WRNN_EHIP, "rocblas_sgemm (conditioning terms) failed");
             HIP_TRY(h, hipMemsetAsync(h->d_members, 0, kXcds * sizeof(int), st));
             XcdArgs a{};
@@ -1374,8 +1396,8 @@ int generate_xcds(wrnn_t *h, const float *cond, int B, int L, const float *noise
     const float one = 1.0f, zero = 0.0f;
     for (int b0 = 0; b0 < B; b0 += kXcds) {
         const int nb = std::min(kXcds, B - b0);
-        const int Lc_max = (int)std::max(1.0, std::min((double)L, budget / ((double)nb * (N + h->KX)) - 1.0));
-        if (grow(h, h->d_X, h->X_cap, (size_t)(Lc_max + 1) * nb * h->KX) ||
+        const int Lc_max = (int)std::max(1.0, std::min((double)L, budget / ((double)nb * (N + h->KXc)) - 1.0));
+        if (grow(h, h->d_X, h->X_cap, (size_t)(Lc_max + 1) * nb * h->KXc) ||
             grow(h, h->d_T, h->T_cap, (size_t)(Lc_max + 1) * nb * N) ||
             grow(h, h->d_xstate, h->xstate_cap, (size_t)nb * kXcdWgs * kSStateW))
             return WRNN_EHIP;
@@ -1388,11 +1410,9 @@ int generate_xcds(wrnn_t *h, const float *cond, int B, int L, const float *noise
         for (int t0 = 0; t0 < L; t0 += Lc_max) {
             const int Lc = std::min(Lc_max, L - t0);
             const int rows = std::min(Lc + 1, L - t0);     // terms rows: steps [t0, t0 + rows)
-            HIP_TRY(h, launch_ci_gemm(cond, h->CD, B, b0, nb, t0, rows, h->d_IW, 1 + c.feat_dims + A, h->d_Ib, R,
-                                      c.feat_dims + A, h->d_X, h->KX, st));
-            HIP_TRY(h, launch_pack_terms_input(cond, h->CD, B, b0, nb, t0, rows, c.feat_dims, A, R, h->KX, h->d_X, st));
-            if (rocblas_sgemm(h->blas, rocblas_operation_transpose, rocblas_operation_none, N, rows * nb, h->KX, &one,
-                              h->d_xWt, h->KX, h->d_X, h->KX, &zero, h->d_T, N) != rocblas_status_success)
+            HIP_TRY(h, launch_pack_cond_input(cond, h->CD, B, b0, nb, t0, rows, h->KXc, h->d_X, st));
+            if (rocblas_sgemm(h->blas, rocblas_operation_transpose, rocblas_operation_none, N, rows * nb, h->KXc, &one,
+                              h->d_xWt, h->KXc, h->d_X, h->KXc, &zero, h->d_T, N) != rocblas_status_success)
                 return fail(h, WRNN_EHIP, "rocblas_sgemm (conditioning terms) failed");
             HIP_TRY(h, hipMemsetAsync(h->d_members, 0, kXcds * sizeof(int), st));
             XcdsArgs a{};
@@ -1589,6 +1609,7 @@ int wrnn_create(const wrnn_config *cfg, int device, wrnn_t **out) {
     h->s = make_slab_layout(*h);
     // rows per launch: LDS, and the per-thread gather register budget
     h->KX = R + 3 * c.aux_dims + 4;
+    h->KXc = h->CD + 4;
     h->KA = round4(std::max(R, std::max(F, c.n_classes)));
     set_rows_partition(*h, 0);
     // dims whose dense weights fit neither kernel may still run with block-sparse GRU weights

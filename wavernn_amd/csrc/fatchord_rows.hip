@@ -547,6 +547,25 @@ __global__ void pack_terms_input_kernel(const float *__restrict__ cond, int CD, 
     for (int k = threadIdx.x & 63; k < KX - R; k += 64) dst[k] = k < 3 * A ? src[k] : (k == 3 * A ? 1.0f : 0.0f);
 }
 
+// XCD kernels' terms input: X'[m] = [cond record (CD: mel, a1, a2, a3, a4) | 1 | 0 0 0] — the
+// GEMM weights fold I = W_I·[x; mel; a1] + b_I into the W_ih1 / W_ih2 rows (capi.cpp), so no cI.
+__global__ void pack_cond_input_kernel(const float *__restrict__ cond, int CD, int Bt, int b0, int B, int t0, int M,
+                                       int KX, float *__restrict__ X) {
+    const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (m >= M) return;
+    const int tl = m / B, b = m - tl * B;
+    const float *src = cond + ((size_t)(t0 + tl) * Bt + b0 + b) * CD;
+    float *dst = X + (size_t)m * KX;
+    for (int k = threadIdx.x & 63; k < KX; k += 64) dst[k] = k < CD ? src[k] : (k == CD ? 1.0f : 0.0f);
+}
+
+hipError_t launch_pack_cond_input(const float *cond, int CD, int Bt, int b0, int B, int t0, int Lc, int KX, float *X,
+                                  hipStream_t st) {
+    const int M = Lc * B;
+    hipLaunchKernelGGL(pack_cond_input_kernel, dim3((M + 3) / 4), dim3(256), 0, st, cond, CD, Bt, b0, B, t0, M, KX, X);
+    return hipGetLastError();
+}
+
 hipError_t launch_pack_terms_input(const float *cond, int CD, int Bt, int b0, int B, int t0, int Lc, int feat, int A,
                                    int R, int KX, float *X, hipStream_t st) {
     const int M = Lc * B;

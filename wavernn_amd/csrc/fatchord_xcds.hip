@@ -20,7 +20,7 @@
 //   wave 0 polls the 32 × 32 partials → Σ + b3 → MoL sample (redundant, bit-identical) → x_t
 // Off the critical path: W_hh1·h1 (LDS blocks; waves 0..5, one engine per gate block-row) → the
 // GRU1 terms of step t+1, published after "y gathered"; h2 likewise; after "f1 gathered": h2
-// gathered by wave 1, S by waves 1, 2, 3, 6, the ring by wave 7; after "h2 gathered": W_hh2·h2
+// gathered by wave 7 (then the ring), S by waves 1, 2, 3, 6; after "h2 gathered": W_hh2·h2
 // (LDS blocks; waves 1, 2, 3, 5, 6, 7).  fp32, sums re-associated (tolerance-checked).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -31,6 +31,10 @@
 #include "xcd_device.h"
 
 namespace wrnn {
+
+#ifndef WRNN_XCDS_DIAG
+#define WRNN_XCDS_DIAG 0   // timing diagnostics (wrong results): 1 skip the S gathers, 2 skip the h2 gather
+#endif
 
 // 8 rows of an (NK·128)-wide layer against a vector polled into registers by ONE wave: lane l
 // holds the pairs k = 0..NK-1 at granules 2(l + 64k) + {0, 1} (xk[k]) and the matching weights
@@ -122,6 +126,8 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
     const int t_terms = min(t_end, a.L - 1);
     unsigned long long *xg = a.xg + (size_t)k * kXXcdStride;
     auto XG = [&](int hop) { return xg + (size_t)hop * kXHopStride; };
+    const __amdgpu_buffer_rsrc_t xgr = __builtin_amdgcn_make_buffer_rsrc(xg, 0, 0x7fffffff, 0x00020000);   // publishes
+    auto XGI = [&](int hop) { return hop * (int)kXHopStride; };                                          // granule index
     auto RING = [&](int t) { return ring + (t & (kXRing - 1)) * kSTerms; };
     auto NZ = [&](int t) { return nzr + (t & (kXRing - 1)) * kXNoise; };
     auto TERMS = [&](int t) { return a.terms + ((size_t)(t - a.t0) * a.nb + k) * TW + (size_t)c * kSTerms; };
@@ -190,13 +196,13 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
     auto publish_term = [&](int t, int rr, float gh) {
         const int u = rr / 3, q = rr - 3 * u;
         const float p1 = RING(t)[SX_P1 + rr], bh = cst[SC_BHH1 + rr], bi = cst[SC_BIH1 + rr];
-        unsigned long long *g = XG(XH_S0 + (t & 1)) + (size_t)(c * kSU + u) * 4;
+        const int g = XGI(XH_S0 + (t & 1)) + (c * kSU + u) * 4;
         const uint32_t tag = (uint32_t)t + 1u;
         if (q < 2) {
-            xpub(g + q, tag, (gh + bh) + (p1 + bi));
+            xpub_b(xgr, g + q, tag, (gh + bh) + (p1 + bi));
         } else {
-            xpub(g + 3, tag, gh + bh);
-            xpub(g + 2, tag, p1 + bi);
+            xpub_b(xgr, g + 3, tag, gh + bh);
+            xpub_b(xgr, g + 2, tag, p1 + bi);
         }
     };
     // a gate block-row of W_hh1 / W_hh2 from LDS (block-row br of this engine)
@@ -234,6 +240,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
     };
     // a quarter of step t's GRU1 terms (waves 1, 2, 3, 6: 896 granules each, one poll round)
     auto gather_terms = [&](int t) {
+        if (WRNN_XCDS_DIAG & 1) return;
         const int qq = wave == 6 ? 3 : wave - 1;
         xgather16<kSPairs>(XG(XH_S0 + (t & 1)) + qq * R, (uint32_t)t + 1u, a.ctl, a.timeout_ticks, t,
                            XH_S0 + (t & 1), abort_flag, lane, [&](int i, float v0, float v1) {
@@ -270,6 +277,13 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
             if (wave == 1 && lane < 11 && t < a.L) NZ(t)[lane] = noise_term(t);
         }
     }
+    // wave 7 stages the ring entries of a step in wg (its GRU2 registers, unused by wave 7):
+    // conditioning terms (lanes < 57, one float4 each) and the injected sampler noise (lanes < 11)
+    auto stage_ring = [&](int t) {
+        if (t <= t_terms && lane < kSTerms / 4) wg[0] = reinterpret_cast<const f4v *>(TERMS(t))[lane];
+        if (a.noise && t < a.L && lane < 11) wg[1].x = a.noise[((size_t)t * a.Bt + b) * 11 + lane];
+    };
+    if (wave == 7) stage_ring(a.t0 + 3);
     const bool resume = a.t0 > 0;
     float *st = a.state + ((size_t)k * kXcdWgs + c) * kSStateW;
     constexpr int oSG = kSR, oGH2 = kSR + 4 * kSR, oH2 = oGH2 + 84, oX = oH2 + kSU;
@@ -355,11 +369,11 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
             h2own = hn;
             // y = (x_I + h1) + h2 (:212, :216)
             const float y = (xi + h1j) + hn;
-            if (lane < 4) xpub(XG(XH_Y) + c * kSU + ul, tag, y);
+            if (lane < 4) xpub_b(xgr, XGI(XH_Y) + c * kSU + ul, tag, y);
         }
         XSTAMP(2);
         auto pub_h2 = [&]() {
-            if (wave < kSUB && lane < 4) xpub(XG(XH_H2) + c * kSU + ul, tag, h2own);
+            if (wave < kSUB && lane < 4) xpub_b(xgr, XGI(XH_H2) + c * kSU + ul, tag, h2own);
         };
         // fc waves: lane l ends fc8_rows_k with row 8h + j + 2·(l >> 4) in o[j]; lanes with
         // (l & 15) < 2 publish row 8h + (l & 1) + 2·(l >> 4)
@@ -439,7 +453,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
             float o[2];
             fc8_rows_k<kSPairs>(wr, yk, o);
             const float A = (jq == 0 ? o[0] : o[1]) + v1;
-            if ((lane & 15) < 2) xpub(XG(XH_F1) + c * kXFcRows + rg, tag, A > 0.0f ? A : 0.0f);
+            if ((lane & 15) < 2) xpub_b(xgr, XGI(XH_F1) + c * kXFcRows + rg, tag, A > 0.0f ? A : 0.0f);
             XSTAMPW(4, 6);
             if (more) {
                 if (wave == 6) {
@@ -447,13 +461,21 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
                     wait_flag(f1got, tag);
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     gather_terms(t + 1);
-                } else {   // wave 7: the ring entries of step t+2 (terms, sampler noise) after f1 gathered
+                } else {   // wave 7 after f1 gathered: h2 (then flag), the ring entries of step t+3
                     wait_flag(f1got, tag);
-                    if (t + 2 >= a.t0 + 3) {
-                        if (t + 2 <= t_terms && lane < kSTerms / 4)
-                            reinterpret_cast<f4v *>(RING(t + 2))[lane] = reinterpret_cast<const f4v *>(TERMS(t + 2))[lane];
-                        if (t + 2 < a.L && lane < 11) NZ(t + 2)[lane] = noise_term(t + 2);
-                    }
+                    if (!(WRNN_XCDS_DIAG & 2))
+                    xgather16<kSPairs>(XG(XH_H2), tag, a.ctl, a.timeout_ticks, t, XH_H2, abort_flag, lane,
+                                       [&](int i, float v0, float v1) { *reinterpret_cast<f2v *>(h2s + i) = f2v{v0, v1}; });
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    set_flag(h2ready, tag);
+                    XSTAMPW(10, 7);
+                    // the ring entries of step t+3 from the registers loaded a step ago, then the
+                    // load for t+4 (lands during the next step, before this wave's next poll)
+                    if (t + 3 <= t_terms && lane < kSTerms / 4) reinterpret_cast<f4v *>(RING(t + 3))[lane] = wg[0];
+                    if (t + 3 < a.L && lane < 11)
+                        NZ(t + 3)[lane] = mol_noise_term(a.noise ? wg[1].x : philox_noise(a.seed, prow, (uint32_t)(t + 3), (uint32_t)lane, 1), lane);
+                    stage_ring(t + 4);
+                    XSTAMPW(12, 7);
                 }
                 wait_flag(h2ready, tag);
                 gh2_dots();
@@ -504,30 +526,25 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
                 while (__hip_atomic_load(f2ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)tag) {
                 }
                 asm volatile("" ::: "memory");
-                if (lane < kXF2Line) xpub(XG(XH_F2) + c * kXF2Line + lane, tag, p + f2x[lane]);   // 30, 31: zero weights
+                if (lane < kXF2Line) xpub_b(xgr, XGI(XH_F2) + c * kXF2Line + lane, tag, p + f2x[lane]);   // 30, 31: zero weights
                 XSTAMPW(6, 4);
             }
         } else if (more) {
             // ---- waves 1..3: W_hh1 block-rows → after y gathered their terms and h2 out; after f1
-            // gathered: h2 (wave 1, then flag), S quarters; after h2 gathered: W_hh2·h2
+            // gathered: S quarters; after h2 gathered: W_hh2·h2
             float g[4];
             gh1_dots(g);
             wait_flag(ygot, tag);
             publish_terms(t + 1, g);
             pub_h2();
+            XSTAMPW(9, 1);
             wait_flag(f1got, tag);
-            if (wave == 1) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                xgather16<kSPairs>(XG(XH_H2), tag, a.ctl, a.timeout_ticks, t, XH_H2, abort_flag, lane,
-                                   [&](int i, float v0, float v1) { *reinterpret_cast<f2v *>(h2s + i) = f2v{v0, v1}; });
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                set_flag(h2ready, tag);
-                XSTAMPW(10, 1);
-            }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             gather_terms(t + 1);
+            XSTAMPW(11, 1);
             wait_flag(h2ready, tag);
             gh2_dots();
+            XSTAMPW(13, 1);
         }
         bar();
         // next step's x, GRU1 terms and the abort word: one LDS round trip

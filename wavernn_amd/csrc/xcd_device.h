@@ -23,6 +23,14 @@ __device__ __forceinline__ void xpub(unsigned long long *g, uint32_t tag, float 
     __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// The same publish through a buffer resource over the XCD's hop area (one wave-uniform
+// descriptor; the per-lane part is a 32-bit granule index instead of a 64-bit address — fewer
+// VGPRs live across the step loop).  Plain buffer store: no cache bits, as xpub.
+typedef unsigned u2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void xpub_b(__amdgpu_buffer_rsrc_t r, int granule, uint32_t tag, float v) {
+    __builtin_amdgcn_raw_buffer_store_b64(u2v{__float_as_uint(v), tag}, r, granule * 8, 0, 0);
+}
+
 __device__ __forceinline__ float perm_sum16(float v) {   // + the same lane of the paired 16-lane row
     const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
     return __uint_as_float(s[0]) + __uint_as_float(s[1]);
