@@ -98,7 +98,10 @@ def other_configs(dev) -> dict:
     res["config4_sparse896_8utt"] = {"samples_per_s": B4 * L4 / ms * 1e3, "rtf": B4 * L4 / ms * 1e3 / d4.sample_rate,
                                      "rows": B4, "loop_steps": L4, "device_ms": ms, "us_per_loop_step": ms * 1e3 / L4,
                                      "sparse_blocks_per_gate_row": loop.info["sparse_blocks"],
-                                     "note": "loop launch from upsampled conditioning (upsample excluded)"}
+                                     "kernel_path": loop.info["last_path"],
+                                     "note": "loop launch from upsampled conditioning (upsample excluded); path 6 = "
+                                             "fatchord_xcds_kernel (one utterance per XCD, block-sparse GRU blocks), "
+                                             "incl. the conditioning-terms GEMM"}
     loop.close()
     # config 5
     dm = syn.DEFAULT_DM

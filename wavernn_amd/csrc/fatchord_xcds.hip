@@ -19,9 +19,9 @@
 //   waves 4, 5 poll f1 → fc2 rows 8h.. → relu → fc3 partials; wave 5 → wave 4     [hop F2]
 //   wave 0 polls the 32 × 32 partials → Σ + b3 → MoL sample (redundant, bit-identical) → x_t
 // Off the critical path: W_hh1·h1 (LDS blocks; waves 0..5, one engine per gate block-row) → the
-// GRU1 terms of step t+1, published after "y gathered"; h2 likewise; after "f1 gathered": h2
-// gathered by wave 7 (then the ring), S by waves 1, 2, 3, 6; after "h2 gathered": W_hh2·h2
-// (LDS blocks; waves 1, 2, 3, 5, 6, 7).  fp32, sums re-associated (tolerance-checked).
+// GRU1 terms of step t+1, published after "y gathered"; h2 likewise and gathered by wave 3 right
+// away; after "h2 gathered": W_hh2·h2 (LDS blocks; waves 0, 3, then 4, 5 after hop F2's publish,
+// 1, 2 after their S quarter); after "f1 gathered": S by waves 1, 2, 6, 7, then the ring (wave 7).  fp32, sums re-associated (tolerance-checked).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -226,10 +226,10 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
             publish_term(t, (4 * ub + li) * 3 + q, sel4(g, li));
         }
     };
-    // W_hh2·h2 → gh2s: engines E = 4·gidx + e < 21 of waves 1, 2, 3, 6, 7, 5
-    const int gidx = wave == 1 ? 0 : wave == 2 ? 1 : wave == 3 ? 2 : wave == 6 ? 3 : wave == 7 ? 4 : 5;
+    // W_hh2·h2 → gh2s: engines E = 4·gidx + e < 21 of waves 0, 3, 4, 5, 1, 2
+    const int gidx = wave == 0 ? 0 : wave == 3 ? 1 : wave == 4 ? 2 : wave == 5 ? 3 : wave == 1 ? 4 : 5;
     const int gh2_br = 4 * gidx + eng;
-    const bool gh2w = wave != 0 && wave != 4 && gh2_br < kSBR;
+    const bool gh2w = wave <= 5 && gh2_br < kSBR;
     auto gh2_dots = [&]() {
         float g[4];
         lds_block_row(whh2b, whh2c, gh2w ? gh2_br : 0, h2s, g);
@@ -238,10 +238,10 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
             gh2s[(4 * ub + li) * 3 + q] = sel4(g, li);
         }
     };
-    // a quarter of step t's GRU1 terms (waves 1, 2, 3, 6: 896 granules each, one poll round)
+    // a quarter of step t's GRU1 terms (waves 1, 2, 6, 7: 896 granules each, one poll round)
     auto gather_terms = [&](int t) {
         if (WRNN_XCDS_DIAG & 1) return;
-        const int qq = wave == 6 ? 3 : wave - 1;
+        const int qq = wave <= 2 ? wave - 1 : wave - 4;   // waves 1, 2, 6, 7
         xgather16<kSPairs>(XG(XH_S0 + (t & 1)) + qq * R, (uint32_t)t + 1u, a.ctl, a.timeout_ticks, t,
                            XH_S0 + (t & 1), abort_flag, lane, [&](int i, float v0, float v1) {
                                *reinterpret_cast<f2v *>(sg + qq * R + i) = f2v{v0, v1};
@@ -302,7 +302,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
     if (!resume) {   // GRU1 terms of step 0 (GH1 = 0), published and gathered
         const float z4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
         publish_terms(0, z4);
-        if (wave == 1 || wave == 2 || wave == 3 || wave == 6) {
+        if (wave == 1 || wave == 2 || wave == 6 || wave == 7) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             gather_terms(0);
         }
@@ -385,6 +385,8 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
                 wait_flag(ygot, tag);
                 publish_terms(t + 1, g);
                 pub_h2();
+                wait_flag(h2ready, tag);
+                gh2_dots();
             }
             // ---- hop F2: Σ of the 32 workgroups' partials + b3 → sample
             const int jp = lane & 15, pg = lane >> 4;
@@ -445,7 +447,10 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
             if (wave == 6) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             u4v v[kSPairs];
             xpoll16<kSPairs>(XG(XH_Y), tag, a.ctl, a.timeout_ticks, t, XH_Y, abort_flag, lane, v);
-            if (hf == 0) set_flag(ygot, tag);
+            if (hf == 0) {
+                set_flag(ygot, tag);
+                if (more) pub_h2();   // before fc1: the early h2 gather (wave 3) waits for every h2
+            }
             XSTAMPW(3, 6);
             f2v yk[kSPairs];
 #pragma unroll
@@ -456,29 +461,19 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
             if ((lane & 15) < 2) xpub_b(xgr, XGI(XH_F1) + c * kXFcRows + rg, tag, A > 0.0f ? A : 0.0f);
             XSTAMPW(4, 6);
             if (more) {
-                if (wave == 6) {
-                    pub_h2();
-                    wait_flag(f1got, tag);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    gather_terms(t + 1);
-                } else {   // wave 7 after f1 gathered: h2 (then flag), the ring entries of step t+3
-                    wait_flag(f1got, tag);
-                    if (!(WRNN_XCDS_DIAG & 2))
-                    xgather16<kSPairs>(XG(XH_H2), tag, a.ctl, a.timeout_ticks, t, XH_H2, abort_flag, lane,
-                                       [&](int i, float v0, float v1) { *reinterpret_cast<f2v *>(h2s + i) = f2v{v0, v1}; });
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    set_flag(h2ready, tag);
-                    XSTAMPW(10, 7);
-                    // the ring entries of step t+3 from the registers loaded a step ago, then the
-                    // load for t+4 (lands during the next step, before this wave's next poll)
+                // after f1 gathered: a quarter of the next S; wave 7 then the ring entries of step
+                // t+3 from the registers loaded a step ago and the load for t+4 (lands during the
+                // next step, before this wave's next poll)
+                wait_flag(f1got, tag);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                gather_terms(t + 1);
+                if (wave == 7) {
                     if (t + 3 <= t_terms && lane < kSTerms / 4) reinterpret_cast<f4v *>(RING(t + 3))[lane] = wg[0];
                     if (t + 3 < a.L && lane < 11)
                         NZ(t + 3)[lane] = mol_noise_term(a.noise ? wg[1].x : philox_noise(a.seed, prow, (uint32_t)(t + 3), (uint32_t)lane, 1), lane);
                     stage_ring(t + 4);
                     XSTAMPW(12, 7);
                 }
-                wait_flag(h2ready, tag);
-                gh2_dots();
             }
         } else if (wave >= 4) {
             const int hf = wave - 4;
@@ -528,20 +523,35 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
                 asm volatile("" ::: "memory");
                 if (lane < kXF2Line) xpub_b(xgr, XGI(XH_F2) + c * kXF2Line + lane, tag, p + f2x[lane]);   // 30, 31: zero weights
                 XSTAMPW(6, 4);
+                if (more) {
+                    wait_flag(h2ready, tag);
+                    gh2_dots();
+                }
             }
         } else if (more) {
-            // ---- waves 1..3: W_hh1 block-rows → after y gathered their terms and h2 out; after f1
-            // gathered: S quarters; after h2 gathered: W_hh2·h2
+            // ---- waves 1..3: W_hh1 block-rows → after y gathered their terms and h2 out; wave 3
+            // gathers h2; waves 1, 2 after f1 gathered S quarters; then W_hh2·h2
             float g[4];
             gh1_dots(g);
             wait_flag(ygot, tag);
             publish_terms(t + 1, g);
             pub_h2();
             XSTAMPW(9, 1);
-            wait_flag(f1got, tag);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            gather_terms(t + 1);
-            XSTAMPW(11, 1);
+            if (wave == 3) {   // h2 right after y (every workgroup publishes it on "y gathered")
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (!(WRNN_XCDS_DIAG & 2))
+                    xgather16<kSPairs>(XG(XH_H2), tag, a.ctl, a.timeout_ticks, t, XH_H2, abort_flag, lane,
+                                       [&](int i, float v0, float v1) { *reinterpret_cast<f2v *>(h2s + i) = f2v{v0, v1}; });
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                set_flag(h2ready, tag);
+                XSTAMPW(10, 3);
+            }
+            if (wave != 3) {   // waves 1, 2: after f1 gathered a quarter of the next S
+                wait_flag(f1got, tag);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                gather_terms(t + 1);
+                XSTAMPW(11, 1);
+            }
             wait_flag(h2ready, tag);
             gh2_dots();
             XSTAMPW(13, 1);
