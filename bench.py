@@ -31,7 +31,9 @@ from wavernn_amd import synthetic as syn  # noqa: E402
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak (dense)
 MOL_MACS_PER_ROW_STEP = 3825152   # loop MACs per row-step, MoL rnn 512
-PMC_PROFILE = os.environ.get("WRNN_PMC_PROFILE", os.path.join(REPO, "profiles", "r01_v13_pmc_traffic.json"))
+PMC_PROFILE = os.environ.get("WRNN_PMC_PROFILE", os.path.join(REPO, "profiles", "r02_v3_pmc_traffic.json"))
+SPARSE896_BYTES_PER_STEP = 5536598   # config 4 sparse values + int16 block indices, fp32
+DM_BYTES_PER_STEP = 12200196         # config 5 deepmind weights, fp32
 
 
 def pmc_traffic_bytes(mode: str, batched: bool, seconds: float):
@@ -52,15 +54,43 @@ def loop_weight_bytes(d: syn.FatchordDims) -> int:
     return 4 * n
 
 
+def hbm_roofline(bytes_per_step: float, us_per_step: float, note: str) -> dict:
+    achieved = bytes_per_step / (us_per_step * 1e-6) / 1e9
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "note": note}
+
+
 def other_configs(dev) -> dict:
     """BASELINE configs 3-5 on one GPU (synthetic inputs, random weights of each architecture):
       3: MoL fold-batched generate() of one 60 s utterance (115 folds x 12 100 steps);
       4: rnn 896 with 95 % 4x4 block-sparse GRU weights, 8 utterances of 5 s (8 rows) per GPU;
-      5: deepmind dual softmax, 32 utterances of 1 s at 16 kHz (32 rows) per GPU."""
+      5: deepmind dual softmax, 32 utterances of 1 s at 16 kHz (32 rows) per GPU;
+    plus the headline architecture serving 8 independent batch-1 streams at once (one per XCD)."""
     from wavernn_amd.fatchord_version import WaveRNN
     from wavernn_amd.loop import DeepmindLoop, FatchordLoop
     from wavernn_amd.pruning import prune_state
     res = {}
+    # config 2 architecture, 8 concurrent unbatched utterances (per-stream latency unchanged)
+    d = syn.DEFAULT_MOL
+    L2, B2 = syn.frames_for_seconds(5.0, d.sample_rate, d.hop_length) * d.hop_length, 8
+    loop = FatchordLoop(d.mode, d.rnn_dims, d.fc_dims, d.aux_dims, d.feat_dims, d.n_classes)
+    loop.set_weights(syn.make_fatchord_state(d, 0))
+    mels, aux = syn.make_conditioning(B2, L2, d.feat_dims, d.res_out_dims, 4)
+    cond = torch.from_numpy(np.concatenate([mels, aux], 2).transpose(1, 0, 2).copy()).to(dev)
+    loop.generate(cond[:100].contiguous(), seed=1)
+    loop.generate(cond, seed=2)
+    ms = loop.elapsed_ms()
+    res["config2_8_streams"] = {"samples_per_s": B2 * L2 / ms * 1e3, "rtf_per_stream": L2 / ms * 1e3 / d.sample_rate,
+                                "rows": B2, "loop_steps": L2, "device_ms": ms, "us_per_loop_step": ms * 1e3 / L2,
+                                "kernel_path": loop.info["last_path"],
+                                "roofline": hbm_roofline(loop_weight_bytes(d) + B2 * COND_BYTES_PER_ROW_STEP, ms * 1e3 / L2,
+                                                         "algorithmic bytes per step (all loop weights once + 836 B "
+                                                         "per row) / step time; weights resident, latency-bound"),
+                                "note": "8 independent 5 s utterances, unbatched, one per XCD in one launch of "
+                                        "fatchord_xcd_kernel (path 5), from upsampled conditioning (upsample "
+                                        "excluded), incl. the conditioning-terms GEMM"}
+    del cond
+    loop.close()
     # config 3
     d = syn.DEFAULT_MOL
     model = WaveRNN(**d.ctor_kwargs()).to(dev)
@@ -99,6 +129,11 @@ def other_configs(dev) -> dict:
                                      "rows": B4, "loop_steps": L4, "device_ms": ms, "us_per_loop_step": ms * 1e3 / L4,
                                      "sparse_blocks_per_gate_row": loop.info["sparse_blocks"],
                                      "kernel_path": loop.info["last_path"],
+                                     "roofline": hbm_roofline(SPARSE896_BYTES_PER_STEP + B4 * COND_BYTES_PER_ROW_STEP,
+                                                              ms * 1e3 / L4,
+                                                              "SURVEY.md 8(d) bytes per step (sparse weights + int16 "
+                                                              "block indices once + 836 B per row) / step time; "
+                                                              "blocks resident, latency-bound"),
                                      "note": "loop launch from upsampled conditioning (upsample excluded); path 6 = "
                                              "fatchord_xcds_kernel (one utterance per XCD, block-sparse GRU blocks), "
                                              "incl. the conditioning-terms GEMM"}
@@ -112,7 +147,10 @@ def other_configs(dev) -> dict:
     loop5.generate(B5, L5, seed=2)
     ms = loop5.elapsed_ms()
     res["config5_deepmind_32utt"] = {"samples_per_s": B5 * L5 / ms * 1e3, "rtf": B5 * L5 / ms * 1e3 / 16000.0,
-                                     "rows": B5, "loop_steps": L5, "device_ms": ms, "us_per_loop_step": ms * 1e3 / L5}
+                                     "rows": B5, "loop_steps": L5, "device_ms": ms, "us_per_loop_step": ms * 1e3 / L5,
+                                     "roofline": hbm_roofline(DM_BYTES_PER_STEP + 4 * B5, ms * 1e3 / L5,
+                                                              "SURVEY.md 8(d) bytes per step (weights once + 4 B per "
+                                                              "row) / step time; weights LDS-resident, latency-bound")}
     loop5.close()
     return res
 
