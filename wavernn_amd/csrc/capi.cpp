@@ -438,6 +438,49 @@ void pack_terms_weights(const wrnn_ctx &h, float *Wt) {
         }
 }
 
+void fold_ci_row(const wrnn_ctx &h, const float *w, float *dst);
+
+// MoL: the same slots against the composed input X' = [mel | a1 | a2 | a3 | a4 | 1 0 0 0]
+// (KXc = CD + 4) — the I layer folded into the W_ih1 / W_ih2 / fc1 rows in fp64 (fold_ci_row,
+// as the XCD kernels' terms), so the GEMM needs no cI and runs at depth 212 instead of R + 3A + 4
+// (2.9x less work at rnn 512).  RAW keeps the cI GEMM (its labels are checked bit-exact).
+bool rows_terms_composed(const wrnn_ctx &h) { return h.cfg.mode == WRNN_MODE_MOL; }
+int rows_terms_kx(const wrnn_ctx &h) { return rows_terms_composed(h) ? h.KXc : h.KX; }
+
+void pack_terms_weights_composed(const wrnn_ctx &h, float *Wt) {
+    const int R = h.cfg.rnn_dims, F = h.cfg.fc_dims, M = h.cfg.feat_dims, A = h.cfg.aux_dims, U = h.rU, UF = h.rUF;
+    const int KX = h.KXc;
+    auto W = [&](const char *n) { return h.w.at(n).data(); };
+    std::fill(Wt, Wt + (size_t)h.rG * h.NT * KX, 0.0f);
+    for (int w = 0; w < h.rG; ++w)
+        for (int k = 0; k < 6 * U + 2 * UF; ++k) {
+            float *row = Wt + ((size_t)w * h.NT + k) * KX;
+            if (k < 6 * U) {
+                const int kk = k % (3 * U), g = kk / U, j = w * U + kk % U;
+                if (j >= R) continue;
+                if (k < 3 * U) {
+                    fold_ci_row(h, W("rnn1.weight_ih_l0") + (size_t)(g * R + j) * R, row);
+                } else {
+                    const float *ih2 = W("rnn2.weight_ih_l0") + (size_t)(g * R + j) * (R + A);
+                    fold_ci_row(h, ih2, row);
+                    for (int a = 0; a < A; ++a) row[M + A + a] += ih2[R + a];                   // a2
+                }
+            } else if (k < 6 * U + UF) {
+                const int r = w * UF + (k - 6 * U);
+                if (r >= F) continue;
+                const float *w1 = W("fc1.weight") + (size_t)r * (R + A);
+                fold_ci_row(h, w1, row);
+                for (int a = 0; a < A; ++a) row[M + 2 * A + a] += w1[R + a];                    // a3
+                row[h.CD] += W("fc1.bias")[r];
+            } else {
+                const int r = w * UF + (k - 6 * U - UF);
+                if (r >= F) continue;
+                for (int a = 0; a < A; ++a) row[M + 3 * A + a] = W("fc2.weight")[(size_t)r * (F + A) + F + a];   // a4
+                row[h.CD] = W("fc2.bias")[r];
+            }
+        }
+}
+
 size_t rows_lds_bytes(const wrnn_ctx &h, int B, int TB, bool head_lds = true) {
     return (size_t)rows_lds_layout(head_lds ? h.rs.total : h.rs.body, B, TB, h.cfg.rnn_dims, h.cfg.fc_dims,
                                    h.cfg.n_classes, h.NK, h.rU, h.rUF, h.rG)
@@ -1073,11 +1116,16 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
             // every workgroup's terms
             for (int g = 0; g < ng; ++g) {
                 const int bg0 = b0 + (g ? Bg : 0), nb = group_rows(Bl, g);
-                HIP_TRY(h, launch_ci_gemm(cond, h->CD, B, bg0, nb, t0, Lc, h->d_IW, 1 + c.feat_dims + A, h->d_Ib, R,
-                                          c.feat_dims + A, h->d_X, h->KX, st));
-                HIP_TRY(h, launch_pack_terms_input(cond, h->CD, B, bg0, nb, t0, Lc, c.feat_dims, A, R, h->KX, h->d_X, st));
-                if (rocblas_sgemm(h->blas, rocblas_operation_transpose, rocblas_operation_none, N, Lc * nb, h->KX, &one,
-                                  h->d_Wt, h->KX, h->d_X, h->KX, &zero, h->d_T + g * T_grp, N) != rocblas_status_success)
+                const int KXg = rows_terms_kx(*h);
+                if (rows_terms_composed(*h)) {
+                    HIP_TRY(h, launch_pack_cond_input(cond, h->CD, B, bg0, nb, t0, Lc, KXg, h->d_X, st));
+                } else {
+                    HIP_TRY(h, launch_ci_gemm(cond, h->CD, B, bg0, nb, t0, Lc, h->d_IW, 1 + c.feat_dims + A, h->d_Ib, R,
+                                              c.feat_dims + A, h->d_X, h->KX, st));
+                    HIP_TRY(h, launch_pack_terms_input(cond, h->CD, B, bg0, nb, t0, Lc, c.feat_dims, A, R, h->KX, h->d_X, st));
+                }
+                if (rocblas_sgemm(h->blas, rocblas_operation_transpose, rocblas_operation_none, N, Lc * nb, KXg, &one,
+                                  h->d_Wt, KXg, h->d_X, KXg, &zero, h->d_T + g * T_grp, N) != rocblas_status_success)
                     return fail(h, WRNN_EHIP, "rocblas_sgemm (conditioning terms) failed");
             }
             RowsArgs a{};
@@ -1756,8 +1804,9 @@ int wrnn_set_weights(wrnn_t *h, const wrnn_tensor *tensors, int n) {
         if (h->d_rslab) HIP_TRY(h, hipFree(h->d_rslab));
         HIP_TRY(h, hipMalloc(&h->d_rslab, rslab.size() * 4));
         HIP_TRY(h, hipMemcpy(h->d_rslab, rslab.data(), rslab.size() * 4, hipMemcpyHostToDevice));
-        std::vector<float> Wt((size_t)h->rG * h->NT * h->KX);
-        pack_terms_weights(*h, Wt.data());
+        std::vector<float> Wt((size_t)h->rG * h->NT * rows_terms_kx(*h));
+        if (rows_terms_composed(*h)) pack_terms_weights_composed(*h, Wt.data());
+        else pack_terms_weights(*h, Wt.data());
         if (h->d_Wt) HIP_TRY(h, hipFree(h->d_Wt));
         HIP_TRY(h, hipMalloc(&h->d_Wt, Wt.size() * 4));
         HIP_TRY(h, hipMemcpy(h->d_Wt, Wt.data(), Wt.size() * 4, hipMemcpyHostToDevice));
@@ -1770,8 +1819,9 @@ int wrnn_set_weights(wrnn_t *h, const wrnn_tensor *tensors, int n) {
         h->d_rslab = nullptr;
         HIP_TRY(h, hipMalloc(&h->d_rslab, rslab.size() * 4));
         HIP_TRY(h, hipMemcpy(h->d_rslab, rslab.data(), rslab.size() * 4, hipMemcpyHostToDevice));
-        std::vector<float> Wt((size_t)h->rG * h->NT * h->KX);
-        pack_terms_weights(*h, Wt.data());
+        std::vector<float> Wt((size_t)h->rG * h->NT * rows_terms_kx(*h));
+        if (rows_terms_composed(*h)) pack_terms_weights_composed(*h, Wt.data());
+        else pack_terms_weights(*h, Wt.data());
         if (h->d_Wt) HIP_TRY(h, hipFree(h->d_Wt));
         h->d_Wt = nullptr;
         HIP_TRY(h, hipMalloc(&h->d_Wt, Wt.size() * 4));
