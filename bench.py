@@ -38,11 +38,20 @@ DM_BYTES_PER_STEP = 12200196         # config 5 deepmind weigh
 
 def pmc_traffic_bytes(mode: str, batched: bool, seconds: float):
     """HBM-side bytes per launch from the committed rocprofv3 PMC passes (FETCH_SIZE +
-    WRITE_SIZE, separate passes) for this exact workload, or None."""
+    WRITE_SIZE, separate passes) for this exact workload, or None.  gfx950 correction
+    (MI355X_MICROARCH.md): FETCH_SIZE counts half the bytes of 16-B-per-lane reads."""
     if mode != "MOL" or batched or abs(seconds - 5.0) > 1e-9 or not os.path.exists(PMC_PROFILE):
         return None
     c = json.load(open(PMC_PROFILE))["counters"]
-    return 1024.0 * (c["FETCH_SIZE"]["value_kib"] + c["WRITE_SIZE"]["value_kib"])
+    return 1024.0 * (2.0 * c["FETCH_SIZE"]["value_kib"] + c["WRITE_SIZE"]["value_kib"])
+
+
+def pmc_config_traffic(key: str):
+    """HBM bytes per loop step of another config's loop kernel from the same PMC passes, or None."""
+    if not os.path.exists(PMC_PROFILE):
+        return None
+    c = json.load(open(PMC_PROFILE)).get("other_configs", {}).get(key)
+    return c["bytes_per_step"] if c else None
 COND_BYTES_PER_ROW_STEP = 836  # 208 fp32 conditioning + 1 fp32 output (SURVEY.md §8(d))
 
 
@@ -260,8 +269,8 @@ def main():
                 "note": "achieved = algorithmic bytes (all loop weights fp32 per step + 836 B/row-step) per launch "
                         "/ launch time (HIP events); the weights are LDS/VGPR-resident on one XCD's 32 CUs "
                         "(fatchord_xcd_kernel), the kernel is hand-off-latency bound. "
-                        f"traffic = FETCH_SIZE+WRITE_SIZE bytes per launch from profiles/{os.path.basename(PMC_PROFILE)}: "
-                        "conditioning-terms reads; the hand-offs stay in the XCD's L2",
+                        f"traffic = 2 x FETCH_SIZE + WRITE_SIZE bytes per launch (gfx950 read correction) from "
+                        f"{os.path.basename(PMC_PROFILE)}: conditioning-terms reads; the hand-offs stay in the XCD's L2",
             },
         }
         if not args.batched and args.mode == "MOL":
@@ -285,6 +294,10 @@ def main():
             }
         if args.other_configs and world == 1 and args.mode == "MOL":
             rec["other_configs"] = other_configs(dev)
+            for key, v in rec["other_configs"].items():
+                tr = pmc_config_traffic(key)
+                if tr is not None and "roofline" in v:
+                    v["roofline"]["traffic_per_step"] = tr   # HBM bytes per loop step (PMC, corrected)
         if args.cpu_steps > 0 and world == 1:
             from oracle import oracle
             cpu = cond.transpose(0, 1).cpu().numpy()

@@ -1,39 +1,81 @@
 """Summarise the FETCH_SIZE / WRITE_SIZE passes of tools/gpu_round.sh into profiles/<name>.json.
 
-    python tools/pmc_summary.py gpurun_out profiles/r01_v4_pmc_traffic.json
+    python tools/pmc_summary.py gpurun_out profiles/r02_v5_pmc_traffic.json
 
-Takes, per counter, the dispatch of the headline's persistent loop kernel (the longest
-fatchord_xcd_kernel / fatchord_split_kernel / fatchord_loop_kernel dispatch in that pass) and stores its value (KiB per dispatch, as rocprofv3 reports these
-derived counters) and duration; bench.py reads the sum as `roofline.traffic`."""
+Headline: per counter, the dispatch of the headline's persistent loop kernel (the longest
+fatchord_xcd_kernel / fatchord_split_kernel / fatchord_loop_kernel dispatch in that pass), its
+value (KiB per dispatch, as rocprofv3 reports these derived counters) and duration.  Other
+configs (present when the passes ran bench.py --other-configs 1): per loop kernel, the summed
+KiB over all its dispatches and the loop steps those dispatches covered.
+
+gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports exactly half the bytes of
+a wide coalesced read (16 B per lane, global_load and buffer_load ... lds alike), WRITE_SIZE the
+exact bytes of 16-B-per-lane stores.  Every HBM read of these kernels is such a read (float4 loads
+of the conditioning terms, the activation-tile LDS-DMA, the slab prologue), so `bytes` = 2 x
+FETCH + WRITE; bench.py reads `bytes` as `roofline.traffic`."""
 import csv
 import json
 import sys
 
+HEADLINE = ("fatchord_xcd_kernel", "fatchord_split_kernel", "fatchord_loop_kernel")
+# loop kernel -> (config key in bench.py's other_configs, loop steps of its dispatches in one
+# bench.py --steps 1 --other-configs 1 run: warm-up + timed generate of that config)
+OTHER = {"fatchord_rows_kernel": ("config3_mol_fold_60s", 2 * 12100),
+         "fatchord_xcds_kernel": ("config4_sparse896_8utt", 100 + 110275),
+         "deepmind_rows_kernel": ("config5_deepmind_32utt", 100 + 16000)}
+
+
+def rows(path):
+    with open(path) as f:
+        yield from csv.DictReader(f)
+
 
 def loop_dispatch(path):
     best = None
-    with open(path) as f:
-        for r in csv.DictReader(f):
-            if not any(k in r["Kernel_Name"] for k in ("fatchord_xcd_kernel", "fatchord_split_kernel", "fatchord_loop_kernel")):
-                continue
-            dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-            if best is None or dur > best[2]:
-                best = (r["Kernel_Name"], float(r["Counter_Value"]), dur)
+    for r in rows(path):
+        if not any(k in r["Kernel_Name"] for k in HEADLINE):
+            continue
+        dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        if best is None or dur > best[2]:
+            best = (r["Kernel_Name"], float(r["Counter_Value"]), dur)
     return best
 
 
+def other_sums(path):
+    out = {}
+    for r in rows(path):
+        for k in OTHER:
+            if k in r["Kernel_Name"]:
+                out[k] = out.get(k, 0.0) + float(r["Counter_Value"])
+    return out
+
+
 def main(src, dst):
-    counters = {}
+    counters, others = {}, {}
     for c in ("FETCH_SIZE", "WRITE_SIZE"):
-        name, kib, dur = loop_dispatch(f"{src}/pmc_{c}/pmc_counter_collection.csv")
+        path = f"{src}/pmc_{c}/pmc_counter_collection.csv"
+        name, kib, dur = loop_dispatch(path)
         counters[c] = {"kernel": name, "value_kib": kib, "duration_ns": dur}
+        for k, v in other_sums(path).items():
+            others.setdefault(k, {})[c] = v
+    headline_bytes = 1024.0 * (2.0 * counters["FETCH_SIZE"]["value_kib"] + counters["WRITE_SIZE"]["value_kib"])
+    cfg = {}
+    for k, v in others.items():
+        if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+            key, steps = OTHER[k]
+            b = 1024.0 * (2.0 * v["FETCH_SIZE"] + v["WRITE_SIZE"])
+            cfg[key] = {"kernel": k, "fetch_kib": v["FETCH_SIZE"], "write_kib": v["WRITE_SIZE"], "loop_steps": steps,
+                        "bytes_per_step": b / steps}
     out = {
         "workload": "MOL rnn512 B=1 5 s (110275 steps), one persistent launch",
         "counters": counters,
-        "note": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (bench.py --steps 1). "
-                "Units KiB per dispatch (no width correction applied: the XCD kernel's hand-offs are plain "
-                "8-byte stores and 16-byte sc1 polls served by the XCD's L2, its HBM traffic is the 16-byte "
-                "reads of the 640 B/step/workgroup conditioning terms).",
+        "bytes": headline_bytes,
+        "other_configs": cfg,
+        "note": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (bench.py --steps 1). Counter "
+                "values in KiB per dispatch; bytes = 1024 x (2 x FETCH_SIZE + WRITE_SIZE), the gfx950 correction for "
+                "16-B-per-lane reads (MI355X_MICROARCH.md). The XCD kernel's hand-offs are plain 8-byte stores and "
+                "16-byte sc1 polls served by the XCD's L2; its HBM traffic is the float4 reads of the 640 B/step/"
+                "workgroup conditioning terms (32 x 640 = 20 480 B per step).",
     }
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)
