@@ -10,9 +10,10 @@ KiB over all its dispatches and the loop steps those dispatches covered.
 
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports exactly half the bytes of
 a wide coalesced read (16 B per lane, global_load and buffer_load ... lds alike), WRITE_SIZE the
-exact bytes of 16-B-per-lane stores.  Every HBM read of these kernels is such a read (float4 loads
-of the conditioning terms, the activation-tile LDS-DMA, the slab prologue), so `bytes` = 2 x
-FETCH + WRITE; bench.py reads `bytes` as `roofline.traffic`."""
+exact bytes of 16-B-per-lane stores.  The XCD kernels' HBM reads are all such reads (float4 loads
+of the conditioning terms, the slab prologue), so `bytes` = 2 x FETCH + WRITE; bench.py reads
+`bytes` as `roofline.traffic`.  The rows kernels add 4-byte flag and 8-byte granule polls
+(uncalibrated widths) beside their 16-B tile LDS-DMA: their per-step figures are approximate."""
 import csv
 import json
 import sys
@@ -75,7 +76,9 @@ def main(src, dst):
                 "values in KiB per dispatch; bytes = 1024 x (2 x FETCH_SIZE + WRITE_SIZE), the gfx950 correction for "
                 "16-B-per-lane reads (MI355X_MICROARCH.md). The XCD kernel's hand-offs are plain 8-byte stores and "
                 "16-byte sc1 polls served by the XCD's L2; its HBM traffic is the float4 reads of the 640 B/step/"
-                "workgroup conditioning terms (32 x 640 = 20 480 B per step).",
+                "workgroup conditioning terms (32 x 640 = 20 480 B per step). The rows kernels (configs 3, 5) also "
+                "poll 4-byte flags and 8-byte granules, widths the guide leaves uncalibrated, so their bytes_per_step "
+                "are approximate; their HBM traffic is dominated by the sc1 activation-tile LDS-DMA (16 B per lane).",
     }
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)
