@@ -127,3 +127,20 @@ def test_large_batches_keep_the_rows_kernel(monkeypatch):
     loop.set_weights(state)
     loop.generate(_cond(mels, aux), seed=1)
     assert loop.info["last_path"] == 2
+
+
+def test_xcd_full_headline_length(monkeypatch):
+    """The headline workload's full length (BASELINE config 2: 5 s = 110 275 loop steps, one
+    row) against the C oracle under injected noise: no drift of the fp32 re-associations over the
+    whole utterance (|Δ| <= MOL_TOL at every sample; the oracle takes ~30 s on one core)."""
+    monkeypatch.setenv("WRNN_PATH", "xcd")
+    L = syn.frames_for_seconds(5.0, syn.DEFAULT_MOL.sample_rate, syn.DEFAULT_MOL.hop_length) * syn.DEFAULT_MOL.hop_length
+    assert L == 110275
+    d, state, mels, aux, noise, ref = _oracle_case(1, L, 150)
+    loop = _loop(d)
+    loop.set_weights(state)
+    out, _ = loop.generate(_cond(mels, aux), noise=torch.from_numpy(noise).to(DEV))
+    assert loop.info["last_path"] == 5
+    err = np.abs(out.cpu().numpy() - ref)
+    print(f"full-length (110 275 steps) max |Δ| {err.max():.3g}, mean {err.mean():.3g}")
+    assert err.max() <= gf.MOL_TOL, f"max |Δ| {err.max()} at {np.unravel_index(err.argmax(), err.shape)}"
