@@ -106,3 +106,19 @@ def test_dense_896_weights_are_refused(monkeypatch):
     loop = _loop(d)
     with pytest.raises(WrnnError, match="block-sparse"):
         loop.set_weights(syn.make_fatchord_state(d, 660))
+
+
+def test_xcds_one_second_vs_oracle(monkeypatch):
+    """A full 1 s utterance (22 275 loop steps, one row) of config 4's sparse rnn-896 model against
+    the C oracle under injected noise: no drift over the utterance."""
+    monkeypatch.delenv("WRNN_PATH", raising=False)
+    L = syn.frames_for_seconds(1.0) * 275
+    assert L == 22275
+    d, state, mels, aux, noise, ref = _oracle_case(1, L, 640)
+    loop = _loop(d)
+    loop.set_weights(state)
+    out, _ = loop.generate(_cond(mels, aux), noise=torch.from_numpy(noise).to(DEV))
+    assert loop.info["last_path"] == 6
+    err = np.abs(out.cpu().numpy() - ref)
+    print(f"sparse 1 s (22 275 steps) max |Δ| {err.max():.3g}, mean {err.mean():.3g}")
+    assert err.max() <= gf.MOL_TOL, f"max |Δ| {err.max()} at {np.unravel_index(err.argmax(), err.shape)}"
