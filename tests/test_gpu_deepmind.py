@@ -100,3 +100,21 @@ def test_dm_granule_and_bulk_handoffs(B, monkeypatch):
         res[g] = loop.generate(B, 300, seed=7)[1]
         loop.close()
     assert torch.equal(res["0"], res["1"])
+
+
+def test_dm_full_second_bit_exact():
+    """Config 5's full utterance length (1 s at 16 kHz = 16 000 steps), 2 rows, H = 896: every
+    coarse/fine label and combined sample bit-exact vs the oracle under injected noise."""
+    from oracle import oracle
+    from wavernn_amd.loop import DeepmindLoop
+    d, B, L = syn.DEFAULT_DM, 2, 16000
+    state = syn.make_deepmind_state(d, 21)
+    noise = syn.make_dm_noise(B, L, d.quantisation, 22)
+    _, _, ref = oracle.deepmind_loop(state, B, L, noise)
+    loop = DeepmindLoop(d.hidden_size, d.quantisation)
+    loop.set_weights(state)
+    _, comb = loop.generate(B, L, noise=torch.from_numpy(noise).to(DEV))
+    got = comb.cpu().numpy().astype(np.int64)
+    eq = got == ref
+    assert eq.all(), f"{eq.mean():.6f} equal, first mismatch {np.argwhere(~eq)[0].tolist()}"
+    loop.close()
