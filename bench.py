@@ -174,6 +174,7 @@ def main():
     ap.add_argument("--batched", action="store_true", help="fold-batched generate (target 11000, overlap 550)")
     ap.add_argument("--cpu-steps", type=int, default=50000, help="oracle steps timed for cpu_baseline (0: skip)")
     ap.add_argument("--other-configs", type=int, default=1, help="also time BASELINE configs 3/4/5 on this GPU (N=1)")
+    ap.add_argument("--fold-batched", type=int, default=1, help="also time the same utterance through generate(batched=True)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -273,7 +274,7 @@ def main():
                         f"{os.path.basename(PMC_PROFILE)}: conditioning-terms reads; the hand-offs stay in the XCD's L2",
             },
         }
-        if not args.batched and args.mode == "MOL":
+        if args.fold_batched and not args.batched and args.mode == "MOL":
             # the same utterance through the reference's default generate() mode
             # (hparams voc_gen_batched = True: 11000/550 folds, one multi-row launch)
             model.generate(mel, None, True, target, overlap, True, seed=7, verbose=False)

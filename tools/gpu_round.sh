@@ -24,3 +24,9 @@ tail -1 gpurun_out/bench.log | cut -c1-300
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o bench --output-format csv -- \
     python "$R/bench.py" --steps 2 --warmup 1 --cpu-steps 0 > gpurun_out/prof.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || exit $rc
+# the headline alone (no fold-batched line, no other configs): the XCD kernel's average dispatch
+# in this summary is the headline launch that roofline.achieved is computed from
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_headline" -o bench --output-format csv -- \
+    python "$R/bench.py" --steps 2 --warmup 1 --cpu-steps 0 --other-configs 0 --fold-batched 0 > gpurun_out/prof_headline.log 2>&1
+rc=$?; echo "rocprof headline rc=$rc"; [ $rc -eq 0 ] || exit $rc
+tail -1 gpurun_out/prof_headline.log | cut -c1-200
