@@ -4,6 +4,7 @@ from __future__ import annotations
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
@@ -38,20 +39,28 @@ EXTRA_FLAGS = {"fatchord_rows.hip": ["-fno-slp-vectorize"], "fatchord_split.hip"
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
+    """Compile the sources whose object is older than the source or any header (all of them in
+    parallel, one hipcc each), then link."""
     if not force and up_to_date():
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     objdir = os.path.join(os.path.dirname(OUT), "obj")
     os.makedirs(objdir, exist_ok=True)
     common = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-I" + os.path.join(REPO, "include")]
-    objs = []
+    newest_header = max(os.path.getmtime(h) for h in HEADERS)
+    objs, cmds = [], []
     for src in SOURCES:
         obj = os.path.join(objdir, os.path.basename(src) + ".o")
-        cmd = common + EXTRA_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj]
-        if verbose:
-            print(" ".join(cmd), flush=True)
-        subprocess.run(cmd, check=True)
         objs.append(obj)
+        if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), newest_header):
+            cmds.append(common + EXTRA_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj])
+    jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1)), 8))
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        for cmd in cmds:
+            if verbose:
+                print(" ".join(cmd), flush=True)
+        for f in [ex.submit(subprocess.run, cmd, check=True) for cmd in cmds]:
+            f.result()
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-lrocblas", "-o", OUT + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)

@@ -1090,10 +1090,13 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
         const int TB = head_lds ? tb_in : rows_tile_for(*h, Bg, false);
         if (TB == 0) return fail(h, WRNN_EUNSUPPORTED, "rows kernel: one row of state does not fit LDS");
         const int SW = rows_state_width(h->rU, h->rUF);
-        const int Lc_max = (int)std::max(1.0, std::min((double)L, budget / ((double)Bl * (N + h->KX))));
+        // GEMM input width: the composed MoL record (KXc = CD + 4) or [cI | a2 a3 a4 | 1 0 0 0]
+        // (KX); either may be the larger one (tiny dims: KXc 100 > KX 80)
+        const int KXg = rows_terms_kx(*h);
+        const int Lc_max = (int)std::max(1.0, std::min((double)L, budget / ((double)Bl * (N + KXg))));
         const size_t T_grp = (size_t)Lc_max * Bg * N, act_grp = (size_t)kRowsHops * 2 * Bg * h->KA;
         const size_t state_grp = (size_t)h->rG * Bg * SW + Bg;
-        if (grow(h, h->d_X, h->X_cap, (size_t)Lc_max * Bg * h->KX) || grow(h, h->d_T, h->T_cap, ng * T_grp) ||
+        if (grow(h, h->d_X, h->X_cap, (size_t)Lc_max * Bg * KXg) || grow(h, h->d_T, h->T_cap, ng * T_grp) ||
             grow(h, h->d_act, h->act_cap, ng * act_grp) || grow(h, h->d_state, h->state_cap, ng * state_grp))
             return WRNN_EHIP;
         HIP_TRY(h, hipMemsetAsync(h->d_flags, 0, ng * flag_words * 4, st));
@@ -1116,7 +1119,7 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
             // every workgroup's terms
             for (int g = 0; g < ng; ++g) {
                 const int bg0 = b0 + (g ? Bg : 0), nb = group_rows(Bl, g);
-                const int KXg = rows_terms_kx(*h);
+                if ((size_t)Lc * nb * KXg > h->X_cap) return fail(h, WRNN_EINVAL, "terms-GEMM input exceeds its workspace");
                 if (rows_terms_composed(*h)) {
                     HIP_TRY(h, launch_pack_cond_input(cond, h->CD, B, bg0, nb, t0, Lc, KXg, h->d_X, st));
                 } else {

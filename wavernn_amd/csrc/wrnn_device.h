@@ -12,8 +12,10 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------------------ wave-level helpers
 // (update_dpp with old = 0 and bound_ctrl: hipcc then folds the move into the consuming VALU op,
-// v_add_f32_dpp instead of v_mov_b32_dpp + v_add_f32; every pattern used here — quad_perm,
-// row mirrors, row_ror — reads a valid lane, so bound_ctrl never applies)
+// v_add_f32_dpp instead of v_mov_b32_dpp + v_add_f32).  quad_perm, the row mirrors and row_ror
+// always read a valid lane; the row shifts (row_shl / row_shr, e.g. xcd_device.h's row_shl:5)
+// do not: their out-of-row lanes read 0 here, not their old value — callers must not select
+// those lanes)
 #define WRNN_DPP(v, ctrl) \
     __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, (v)), (ctrl), 0xF, 0xF, true))
 
