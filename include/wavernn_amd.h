@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define WRNN_ABI_VERSION 4
+#define WRNN_ABI_VERSION 5
 
 enum wrnn_status {
     WRNN_OK = 0,
@@ -69,7 +69,8 @@ typedef struct {
 } wrnn_tensor;
 
 /* Launch geometry chosen for the handle (read-only).  Kernels: the XCD-resident kernel (MoL
- * rnn/fc 512, up to 8 rows per launch, one row on each XCD's 32 CUs), the role-split kernel
+ * rnn/fc 512, up to 8 rows per launch, one row on each XCD's 32 CUs), its many-row form (up to
+ * 16 rows per XCD on the matrix cores, 128 per launch), the role-split kernel
  * (one MoL row), the per-row latency kernel (rows in LDS, used while B <= max_rows) and the
  * multi-row kernel (rows through HBM). */
 typedef struct {
@@ -88,9 +89,11 @@ typedef struct {
     int32_t split_grid;      /* batch-1 MoL role-split kernel: GRU + FC workgroups (0: unavailable) */
     int32_t last_path;       /* kernel of the last wrnn_generate: 1 latency, 2 multi-row,
                                 3 deepmind, 4 role-split, 5 XCD-resident, 6 XCD-resident
-                                block-sparse rnn 896 (0: none yet) */
+                                block-sparse rnn 896, 7 XCD-resident many-row (0: none yet) */
     int32_t xcd_rows;        /* XCD-resident kernel (dense rnn 512, or rnn 896 with block-sparse
                                 GRU weights once they are set): rows per launch (0: unavailable) */
+    int32_t xcdm_rows;       /* XCD-resident many-row kernel (MoL rnn/fc 512): rows per launch
+                                (0: unavailable)                                           (ABI 5) */
 } wrnn_info;
 
 /* Create a handle on `device` (replaces WaveRNN.__init__ for the loop's dims,

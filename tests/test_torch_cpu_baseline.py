@@ -1,0 +1,49 @@
+"""The PyTorch-CPU eager restatement bench.py times as `cpu_baseline` (oracle/torch_cpu.py) computes
+what the pinned C/numpy oracle computes: loop samples (MoL within MOL_TOL, RAW labels exact under
+injected noise), the upsampled conditioning, and a whole generate()."""
+import numpy as np
+import torch
+
+from oracle import oracle, torch_cpu
+from tests.golden import fixtures as gf
+from wavernn_amd import synthetic as syn
+
+
+def test_loop_matches_c_oracle():
+    for d in (syn.TINY_MOL, syn.TINY_RAW):
+        B, L = 3, 200
+        state = syn.make_fatchord_state(d, 5)
+        mels, aux = syn.make_conditioning(B, L, d.feat_dims, d.res_out_dims, 6)
+        noise = syn.make_noise(d.mode, B, L, d.n_classes, 7)
+        ref, _ = oracle.fatchord_loop(state, d.mode, mels, aux, noise)
+        got = torch_cpu.loop(state, d.mode, torch.from_numpy(mels), torch.from_numpy(aux), noise)
+        if d.mode == "RAW":
+            assert np.array_equal(got, ref)
+        else:
+            assert np.abs(got - ref).max() <= gf.MOL_TOL
+
+
+def test_upsample_matches_numpy_oracle():
+    d = syn.TINY_MOL
+    state = syn.make_fatchord_state(d, 8)
+    mel = syn.make_mel(d.feat_dims, 12, 9)
+    m, a = torch_cpu.upsample(state, d, torch.from_numpy(mel)[None])
+    mp = oracle.pad_tensor(mel.T[None].astype(np.float32), d.pad)[0].T
+    rm, ra = oracle.upsample(mp, state, d.upsample_factors, d.res_blocks, d.pad)
+    assert np.abs(m[0].numpy() - rm).max() <= 1e-5
+    assert np.abs(a[0].numpy() - ra).max() <= 1e-4 * max(1.0, float(np.abs(ra).max()))
+
+
+def test_timed_generate_matches_oracle_generate():
+    d = syn.TINY_MOL
+    state = syn.make_fatchord_state(d, 10)
+    T = 24
+    mel = syn.make_mel(d.feat_dims, T, 11)
+    L = T * d.hop_length
+    target, overlap = 1000, 50
+    folds = oracle.fold_with_overlap(np.zeros((1, L, 1), np.float32), target, overlap).shape
+    noise = syn.make_noise(d.mode, folds[0], folds[1], d.n_classes, 12)
+    ref = oracle.generate(state, d, mel, True, target, overlap, False, noise)
+    r = torch_cpu.timed_generate(state, d, mel, True, target, overlap, False, noise)
+    assert r["loop_steps"] == folds[1] and r["rows"] == folds[0]
+    assert np.abs(r["wave"] - ref).max() <= 2 * gf.MOL_TOL

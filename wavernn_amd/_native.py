@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_lib", "libwavernn_amd.so")
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 MODE_RAW, MODE_MOL, MODE_DM = 0, 1, 2
 STATUS = {0: "WRNN_OK", -1: "WRNN_EINVAL", -2: "WRNN_EHIP", -3: "WRNN_ENOWEIGHTS", -4: "WRNN_ETIMEOUT",
           -5: "WRNN_ENOMEM", -6: "WRNN_EUNSUPPORTED"}
@@ -41,7 +41,7 @@ class Info(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in ("grid", "units_rnn", "units_fc", "units_cls", "max_rows",
                                               "lds_bytes", "slab_floats", "num_cus", "rows_grid",
                                               "rows_units_rnn", "sparse_blocks", "split_grid", "last_path",
-                                              "xcd_rows")]
+                                              "xcd_rows", "xcdm_rows")]
 
 
 class UpsampleCfg(ctypes.Structure):

@@ -21,6 +21,7 @@
 #include "fatchord_split.h"
 #include "fatchord_xcd.h"
 #include "fatchord_xcds.h"
+#include "fatchord_xcdm.h"
 
 namespace wrnn {
 hipError_t launch_ci_gemm(const float *cond, int CD, int Bt, int b0, int Bc, int t0, int L, const float *W, int ldw,
@@ -49,6 +50,9 @@ hipError_t xcd_occupancy(int *blocks_per_cu);
 hipError_t launch_xcds(const XcdsArgs &a, hipStream_t st);
 hipError_t prepare_xcds_kernel(int max_lds_bytes);
 hipError_t xcds_occupancy(int *blocks_per_cu);
+hipError_t launch_xcdm(const XcdmArgs &a, int nq, hipStream_t st);
+hipError_t prepare_xcdm_kernel(int max_lds_bytes);
+hipError_t xcdm_max_quads(int max_lds_bytes, int *nq_max);
 }  // namespace wrnn
 
 using namespace wrnn;
@@ -136,6 +140,13 @@ struct wrnn_ctx {
     // the loaded weights are block-sparse with <= kSNB nonzero blocks per gate block-row
     bool xcds_cap = false, xcds_ok = false;
     XcdsSlab xss{};
+    // XCD-resident many-row MoL kernel (rnn / fc 512, MFMA): fatchord_xcdm.hip; shares the XCD
+    // kernel's terms-GEMM weights (d_xWt)
+    bool xcdm_ok = false;
+    int xcdm_nq = 0;                                // largest co-resident quad count (rows per XCD / 4)
+    XcdmSlab xms{};
+    float *d_xmslab = nullptr, *d_xmstate = nullptr;
+    unsigned long long *d_xmxg = nullptr;
 };
 
 namespace {
@@ -997,6 +1008,63 @@ void pack_xcds_terms_weights(const wrnn_ctx &h, std::vector<float> &Wt) {
     }
 }
 
+// ---- XCD-resident many-row kernel (fatchord_xcdm.h): per workgroup c the MFMA A operands of the
+// eleven 16-row sets (wave w: K window [kMK·w, kMK·(w + 1))), the fc3 columns of its f2 rows and
+// the small vectors
+void make_xcdm_slab(wrnn_ctx &h) {
+    int o = 0;
+    auto take = [&](int n) { int at = o; o += round4(n); return at; };
+    XcdmSlab &x = h.xms;
+    x.a = take(kMWaves * kMSets * kMJ * 64);
+    x.w3 = take(32 * 16);
+    x.cst = take(kMCst);
+    x.total = o;
+}
+
+void pack_xcdm_slab(const wrnn_ctx &h, std::vector<float> &slab) {
+    const int R = h.cfg.rnn_dims, F = h.cfg.fc_dims, A = h.cfg.aux_dims, NC = h.cfg.n_classes;
+    auto W = [&](const char *n) { return h.w.at(n).data(); };
+    const float *IW = W("I.weight");
+    const int nin = 1 + h.cfg.feat_dims + A;
+    const XcdmSlab &x = h.xms;
+    slab.assign((size_t)kXcdWgs * x.total, 0.0f);
+    // row r (0..15) of set s of workgroup c: (matrix, row index, row stride)
+    auto set_row = [&](int s, int c, int r) -> const float * {
+        if (s < MS_FC1) return W("rnn2.weight_ih_l0") + (size_t)(s * R + 16 * c + r) * (R + A);
+        if (s == MS_FC1) return W("fc1.weight") + (size_t)(16 * c + r) * (R + A);
+        if (s == MS_FC2) return W("fc2.weight") + (size_t)(16 * c + r) * (F + A);
+        if (s < MS_HH1) return W("rnn2.weight_hh_l0") + (size_t)((s - MS_HH2) * R + 16 * c + r) * R;
+        return W("rnn1.weight_hh_l0") + (size_t)((s - MS_HH1) * R + 16 * c + r) * R;
+    };
+    for (int c = 0; c < kXcdWgs; ++c) {
+        float *out = slab.data() + (size_t)c * x.total;
+        for (int w = 0; w < kMWaves; ++w)
+            for (int s = 0; s < kMSets; ++s)
+                for (int j = 0; j < kMJ; ++j)
+                    for (int l = 0; l < 64; ++l) {
+                        const int g = (l >> 2) & 3, sp = l >> 4, j4 = l & 3;
+                        out[x.a + (((size_t)w * kMSets + s) * kMJ + j) * 64 + l] =
+                            set_row(s, c, 4 * g + j4)[kMK * w + kMJ * sp + j];
+                    }
+        for (int jj = 0; jj < NC; ++jj)
+            for (int r = 0; r < 16; ++r) out[x.w3 + jj * 16 + r] = W("fc3.weight")[(size_t)jj * F + 16 * c + r];
+        for (int u = 0; u < 16; ++u) {
+            const int j = 16 * c + u;
+            out[x.cst + MC_WI0 + u] = IW[(size_t)j * nin];
+            for (int q = 0; q < 3; ++q) {
+                const int src = q * R + j, i = q * 16 + u;
+                out[x.cst + MC_Q1 + i] = xcol_dot(W("rnn1.weight_ih_l0") + (size_t)src * R, IW, nin, R);
+                out[x.cst + MC_Q2 + i] = xcol_dot(W("rnn2.weight_ih_l0") + (size_t)src * (R + A), IW, nin, R);
+                out[x.cst + MC_BIH1 + i] = W("rnn1.bias_ih_l0")[src];
+                out[x.cst + MC_BHH1 + i] = W("rnn1.bias_hh_l0")[src];
+                out[x.cst + MC_BIH2 + i] = W("rnn2.bias_ih_l0")[src];
+                out[x.cst + MC_BHH2 + i] = W("rnn2.bias_hh_l0")[src];
+            }
+        }
+        for (int jj = 0; jj < NC; ++jj) out[x.cst + MC_B3 + jj] = W("fc3.bias")[jj];
+    }
+}
+
 }  // namespace
 
 namespace {
@@ -1494,6 +1562,89 @@ int generate_xcds(wrnn_t *h, const float *cond, int B, int L, const float *noise
     return WRNN_OK;
 }
 
+// MoL rows through the XCD-resident many-row kernel: up to kMRowsMax rows per launch (launch row
+// r on XCD r % 8, its row r / 8 there), time chunks sized so terms + GEMM input stay within
+// WRNN_TERMS_MB (default 8192 MiB); the recurrent state is carried per workgroup in d_xmstate.
+int generate_xcdm(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed, int64_t row_offset,
+                  float *out, hipStream_t st) {
+    const int N = kXcdWgs * kXTerms;
+    if (!h->blas && rocblas_create_handle(&h->blas) != rocblas_status_success)
+        return fail(h, WRNN_EHIP, "rocblas_create_handle failed");
+    if (rocblas_set_stream(h->blas, st) != rocblas_status_success) return fail(h, WRNN_EHIP, "rocblas_set_stream failed");
+    const char *mb_env = std::getenv("WRNN_TERMS_MB");
+    const double budget = (mb_env ? std::atof(mb_env) : 8192.0) * (1 << 20) / 4.0;   // floats
+    const size_t xg_words = (size_t)kXcds * kMXcdStride;
+    if (!h->d_members) HIP_TRY(h, hipMalloc(&h->d_members, kXcds * sizeof(int)));
+    if (!h->d_xmxg) HIP_TRY(h, hipMalloc(&h->d_xmxg, xg_words * 8));
+    if (!h->d_xmstate) HIP_TRY(h, hipMalloc(&h->d_xmstate, (size_t)kXcds * kXcdWgs * kMStateW * sizeof(float)));
+    const int rows_max = kXcds * 4 * h->xcdm_nq;
+    const float one = 1.0f, zero = 0.0f;
+    // diagnostics: WRNN_DEBUG_STAMPS=<steps> WRNN_DEBUG_FILE=<path>: per-wave phase stamps of
+    // the first launch ([256 · kMWaves][steps][kMStamps] shader clocks, int32 header)
+    const char *dbg_env = std::getenv("WRNN_DEBUG_STAMPS");
+    const int dbg_steps = dbg_env ? std::min(L, std::atoi(dbg_env)) : 0;
+    const size_t dbg_n = (size_t)kXcds * kXcdWgs * kMWaves * dbg_steps * kMStamps;
+    unsigned *d_dbg = nullptr;
+    if (dbg_steps > 0) {
+        HIP_TRY(h, hipMalloc(&d_dbg, dbg_n * 4));
+        HIP_TRY(h, hipMemsetAsync(d_dbg, 0, dbg_n * 4, st));
+    }
+    for (int b0 = 0; b0 < B; b0 += rows_max) {
+        const int nb = std::min(rows_max, B - b0);
+        const int nq = (((nb + kXcds - 1) / kXcds) + 3) / 4;   // quads on the fullest XCD
+        const int Lc_max = (int)std::max(1.0, std::min((double)L, budget / ((double)nb * (N + h->KXc))));
+        if (grow(h, h->d_X, h->X_cap, (size_t)Lc_max * nb * h->KXc) || grow(h, h->d_T, h->T_cap, (size_t)Lc_max * nb * N))
+            return WRNN_EHIP;
+        HIP_TRY(h, hipMemsetAsync(h->d_xmxg, 0, xg_words * 8, st));   // tags restart at 1
+        for (int t0 = 0; t0 < L; t0 += Lc_max) {
+            const int Lc = std::min(Lc_max, L - t0);
+            if ((size_t)Lc * nb * h->KXc > h->X_cap || (size_t)Lc * nb * N > h->T_cap)
+                return fail(h, WRNN_EINVAL, "xcdm: terms workspace too small");
+            HIP_TRY(h, launch_pack_cond_input(cond, h->CD, B, b0, nb, t0, Lc, h->KXc, h->d_X, st));
+            if (rocblas_sgemm(h->blas, rocblas_operation_transpose, rocblas_operation_none, N, Lc * nb, h->KXc, &one,
+                              h->d_xWt, h->KXc, h->d_X, h->KXc, &zero, h->d_T, N) != rocblas_status_success)
+                return fail(h, WRNN_EHIP, "rocblas_sgemm (conditioning terms) failed");
+            HIP_TRY(h, hipMemsetAsync(h->d_members, 0, kXcds * sizeof(int), st));
+            XcdmArgs a{};
+            a.slab = h->d_xmslab;
+            a.terms = h->d_T;
+            a.noise = noise;
+            a.out = out;
+            a.state = h->d_xmstate;
+            a.xg = h->d_xmxg;
+            a.members = h->d_members;
+            a.ctl = h->d_ctl;
+            a.seed = seed;
+            a.row0 = row_offset + b0;
+            a.timeout_ticks = h->timeout_ticks;
+            a.L = L;
+            a.t0 = t0;
+            a.Lc = Lc;
+            a.Bt = B;
+            a.b0 = b0;
+            a.nb = nb;
+            a.s = h->xms;
+            a.dbg = (b0 == 0 && t0 == 0) ? d_dbg : nullptr;
+            a.dbg_steps = std::min(dbg_steps, Lc);
+            HIP_TRY(h, launch_xcdm(a, nq, st));
+        }
+    }
+    if (d_dbg) {
+        std::vector<unsigned> host(dbg_n);
+        HIP_TRY(h, hipStreamSynchronize(st));
+        HIP_TRY(h, hipMemcpy(host.data(), d_dbg, dbg_n * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(h, hipFree(d_dbg));
+        const char *path = std::getenv("WRNN_DEBUG_FILE");
+        if (FILE *f = std::fopen(path ? path : "wrnn_stamps.bin", "wb")) {
+            int hdr[3] = {kXcds * kXcdWgs * kMWaves, dbg_steps, kMStamps};
+            std::fwrite(hdr, sizeof(hdr), 1, f);
+            std::fwrite(host.data(), 4, host.size(), f);
+            std::fclose(f);
+        }
+    }
+    return WRNN_OK;
+}
+
 int generate_latency(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed,
                      int64_t row_offset, float *out, int32_t *labels, hipStream_t st) {
     const wrnn_config &c = h->cfg;
@@ -1717,6 +1868,13 @@ int wrnn_create(const wrnn_config *cfg, int device, wrnn_t **out) {
         HIP_TRY(h, prepare_xcd_kernel(h->max_lds));
         HIP_TRY(h, xcd_occupancy(&per_cu));
         h->xcd_ok = per_cu >= 1;
+        // its many-row form (same terms GEMM)
+        if (h->xcd_ok) {
+            make_xcdm_slab(*h);
+            HIP_TRY(h, prepare_xcdm_kernel(h->max_lds));
+            HIP_TRY(h, xcdm_max_quads(h->max_lds, &h->xcdm_nq));
+            h->xcdm_ok = h->xcdm_nq >= 1;
+        }
     }
     // MoL rnn 896 / fc 512: the XCD-resident block-sparse kernel, if the weights turn out
     // block-sparse (decided at wrnn_set_weights)
@@ -1853,6 +2011,14 @@ int wrnn_set_weights(wrnn_t *h, const wrnn_tensor *tensors, int n) {
             HIP_TRY(h, hipMemcpy(*pr.first, pr.second->data(), pr.second->size() * 4, hipMemcpyHostToDevice));
         }
     }
+    if (h->xcdm_ok) {
+        std::vector<float> slab;
+        pack_xcdm_slab(*h, slab);
+        if (h->d_xmslab) HIP_TRY(h, hipFree(h->d_xmslab));
+        h->d_xmslab = nullptr;
+        HIP_TRY(h, hipMalloc(&h->d_xmslab, slab.size() * 4));
+        HIP_TRY(h, hipMemcpy(h->d_xmslab, slab.data(), slab.size() * 4, hipMemcpyHostToDevice));
+    }
     h->xcds_ok = false;
     if (h->xcds_cap) {
         const char *sp_env = std::getenv("WRNN_SPARSE");
@@ -1875,6 +2041,7 @@ int wrnn_set_weights(wrnn_t *h, const wrnn_tensor *tensors, int n) {
 }
 
 constexpr int kXcdDefaultRows = 48;
+constexpr int kXcdmMinRows = 9;
 
 int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed,
                   int64_t row_offset, float *out, int32_t *labels, void *stream) {
@@ -1896,14 +2063,17 @@ int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise
     if (rows && !h->rows_ok) rows = false;
     // MoL rnn / fc 512 up to kXcdDefaultRows rows: the XCD-resident kernel (8 rows per launch;
     // beyond that the multi-row kernel's throughput wins)
-    const bool xcd = h->xcd_ok && (pe == "xcd" || (pe.empty() && B <= kXcdDefaultRows));
+    // MoL rnn / fc 512, more than kXcdmMinRows rows: the many-row XCD-resident kernel (MFMA)
+    const bool xcdm = h->xcdm_ok && (pe == "xcdm" || (pe.empty() && B >= kXcdmMinRows));
+    const bool xcd = !xcdm && h->xcd_ok && (pe == "xcd" || (pe.empty() && B <= kXcdDefaultRows));
     // MoL rnn 896 with block-sparse GRU weights likewise: the XCD-resident sparse kernel
     const bool xcds = !xcd && h->xcds_ok && (pe == "xcd" || (pe.empty() && B <= kXcdDefaultRows));
     const bool split = !xcd && !xcds && h->split_ok && (pe == "split" || (pe.empty() && B == 1));
     HIP_TRY(h, hipMemsetAsync(h->d_ctl, 0, kCtlWords * sizeof(int), st));
     HIP_TRY(h, hipEventRecord(h->ev0, st));
-    h->last_path = h->dm ? 3 : xcd ? 5 : xcds ? 6 : split ? 4 : rows ? 2 : 1;
+    h->last_path = h->dm ? 3 : xcdm ? 7 : xcd ? 5 : xcds ? 6 : split ? 4 : rows ? 2 : 1;
     const int rc = h->dm    ? generate_dm(h, B, L, noise, seed, row_offset, out, labels, st)
+                   : xcdm  ? generate_xcdm(h, cond, B, L, noise, seed, row_offset, out, st)
                    : xcd   ? generate_xcd(h, cond, B, L, noise, seed, row_offset, out, st)
                    : xcds  ? generate_xcds(h, cond, B, L, noise, seed, row_offset, out, st)
                    : split ? generate_split(h, cond, B, L, noise, seed, row_offset, out, st)
@@ -1929,7 +2099,9 @@ int wrnn_check(wrnn_t *h, void *stream) {
                                         "coarse label", "fine label"};
         static const char *split_hops[] = {"y", "f1", "f2", "h2", "h2", "gru1-terms", "gru1-terms"};
         static const char *xcd_hops[] = {"y", "f1", "f2", "h2", "gru1-terms", "gru1-terms"};
-        const char *name = h->last_path >= 5   ? (hop >= 0 && hop < 6 ? xcd_hops[hop] : "?")
+        static const char *xcdm_hops[] = {"h1", "y", "h2", "f1", "f2 (partial logits)", "x"};
+        const char *name = h->last_path == 7   ? (hop >= 0 && hop < 6 ? xcdm_hops[hop] : "?")
+                           : h->last_path >= 5 ? (hop >= 0 && hop < 6 ? xcd_hops[hop] : "?")
                            : h->last_path == 4 ? (hop >= 0 && hop < 7 ? split_hops[hop] : "?")
                            : h->last_path == 3 ? (hop >= 0 && hop < 8 ? dm_hops[hop] : "?")
                            : h->last_path == 2 ? (hop >= 0 && hop < 6 ? row_hops[hop] : "?")
@@ -1981,6 +2153,7 @@ int wrnn_query(const wrnn_t *h, wrnn_info *info) {
     info->split_grid = h->split_ok ? h->sGg + h->sGf : 0;
     info->last_path = h->last_path;
     info->xcd_rows = (h->xcd_ok || h->xcds_ok) ? kXcds : 0;
+    info->xcdm_rows = h->xcdm_ok ? kXcds * 4 * h->xcdm_nq : 0;
     return WRNN_OK;
 }
 
@@ -1997,7 +2170,7 @@ void wrnn_destroy(wrnn_t *h) {
                     (void *)h->d_dmflags, (void *)h->d_dmxg, (void *)h->d_sgslab, (void *)h->d_sfslab,
                     (void *)h->d_sWt, (void *)h->g2.d_slab, (void *)h->g2.d_Wt, (void *)h->dm2.d_slab,
                     (void *)h->d_gact, (void *)h->d_xslab, (void *)h->d_xWt, (void *)h->d_xstate, (void *)h->d_xgx,
-                    (void *)h->d_members})
+                    (void *)h->d_members, (void *)h->d_xmslab, (void *)h->d_xmstate, (void *)h->d_xmxg})
         if (p) (void)hipFree(p);
     if (h->blas) (void)rocblas_destroy_handle(h->blas);
     delete h;

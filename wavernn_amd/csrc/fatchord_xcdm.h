@@ -1,0 +1,127 @@
+// Shared between the host launcher (capi.cpp) and fatchord_xcdm.hip: the XCD-resident MoL kernel
+// for MANY rows — up to 16 rows (utterances or folds) on each XCD, all of them stepping together
+// through one copy of the weights held in the XCD's 32 CUs, the matvecs on the matrix cores
+// (v_mfma_f32_4x4x1_16b_f32: 16 blocks of 4 weight rows × 4 rows of the batch), every hand-off
+// kept in the XCD's L2.
+//
+// Shapes: rnn 512, fc 512, aux 32, MoL (30 classes) — BASELINE configs 2 (fold-batched) and 3.
+#pragma once
+#include <stdint.h>
+
+#include "fatchord_xcd.h"
+
+namespace wrnn {
+
+#ifndef WRNN_XCDM_WAVES
+#define WRNN_XCDM_WAVES 4
+#endif
+constexpr int kMWaves = WRNN_XCDM_WAVES;   // waves per workgroup (one per SIMD)
+constexpr int kMThreads = 64 * kMWaves;
+constexpr int kMQuadMax = 4;               // batch quads (4 rows) per XCD
+constexpr int kMRowsXcd = 4 * kMQuadMax;   // rows per XCD
+constexpr int kMRowsMax = kXcds * kMRowsXcd;   // rows per launch (128 ≥ config 3's 115 folds)
+constexpr int kMK = 512 / kMWaves;         // K window of a wave: wave w multiplies columns [kMK·w, kMK·(w + 1))
+constexpr int kMJ = kMK / 4;               // MFMAs per set and quad (4 k-slices of kMJ columns)
+constexpr int kMPL = kMK / 32;             // 16-byte poll loads per lane and quad (4 rows × kMK granules)
+
+// The eleven 16-row weight sets a workgroup c multiplies (rows of its units 16c..16c+15 / fc rows
+// 16c..16c+15), register-resident as MFMA A operands (16 per set and wave: kMK / 4 k-slices)
+enum MSet { MS_IH2 = 0, MS_FC1 = 3, MS_FC2 = 4, MS_HH2 = 5, MS_HH1 = 8, kMSets = 11 };
+//   MS_IH2 + q: W_ih2[q·512 + 16c + u][:512]   MS_HH2 + q / MS_HH1 + q: W_hh2 / W_hh1 rows likewise
+//   MS_FC1: fc1.weight[16c + r][:512]          MS_FC2: fc2.weight[16c + r][:512]
+// A operand of set s, MFMA j (0..kMJ-1), lane l = 4b + j4 (block b = 4s' + g: row group g = b & 3,
+// k-slice s' = b >> 2): W_s[row 4g + j4][kMK·w + kMJ·s' + j]  (slab [kMWaves][11][kMJ][64 lanes])
+
+// Hand-off vectors of one XCD.  Row n (0..15) of the XCD = launch row k + 8n.  Granules
+// {tag = step + 1, value}: H1 / Y / H2 / F1 at n·512 + j (unit or fc row j); F2 (partial logits
+// of producer c) at (n·32 + c)·32 + j, j < 32 (30, 31 zero); X (two-level sampler) at n.
+enum MHop { MH_H1 = 0, MH_Y = 1, MH_H2 = 2, MH_F1 = 3, MH_F2 = 4, MH_X = 5, kMHops = 6 };
+constexpr long long kMVec = (long long)kMRowsXcd * 512;
+constexpr long long kMF2 = (long long)kMRowsXcd * kXcdWgs * 32;
+constexpr long long kMHopOff[kMHops] = {0, kMVec, 2 * kMVec, 3 * kMVec, 4 * kMVec, 4 * kMVec + kMF2};
+constexpr long long kMXcdStride = 4 * kMVec + kMF2 + 64;   // granules per XCD
+
+// Per-workgroup constants (LDS), gate-major: index q·16 + u
+enum MCst { MC_Q1 = 0, MC_Q2 = 48, MC_BIH1 = 96, MC_BHH1 = 144, MC_BIH2 = 192, MC_BHH2 = 240, MC_WI0 = 288,
+            MC_B3 = 304, kMCst = 336 };
+//   q1 / q2: W_ih1 / W_ih2[:, :R] · W_I[:, 0] (the x column of the I layer folded into the gates),
+//   biases of both GRUs, W_I[:, 0] of the own units, b3 (padded to 32)
+
+struct XcdmSlab {
+    int a;       // [kMWaves][kMSets][16][64]   MFMA A operands
+    int w3;      // [32][16]                     W3[j][16c + r] (j >= 30: 0)
+    int cst;     // [kMCst]
+    int total;
+};
+
+// Terms of one step for one row (the XCD kernels' terms GEMM, XTerm slots): P1 [0,48), P2 [48,96),
+// cI [96,112), V1 [112,128), V2 [128,144) — the first kMRing floats of the 160-float record
+constexpr int kMRing = 144;
+constexpr int kMNoise = 12;                // 11 MoL sampler terms per row and step, padded
+
+// Per-workgroup state carried between time chunks: h1 / h2 of the own units [16][16 rows],
+// W_hh1·h1 / W_hh2·h2 [3][16][16], x [16]
+constexpr int kMStateW = 256 + 256 + 768 + 768 + 16;
+
+struct XcdmArgs {
+    const float *slab;            // [kXcdWgs][slab.total]
+    const float *terms;           // [Lc][nb][kXcdWgs·kXTerms], row (t - t0)·nb + launch row
+    const float *noise;           // [L][Bt][11] or nullptr (Philox)
+    float *out;                   // [Bt][L]
+    float *state;                 // [kXcds][kXcdWgs][kMStateW]
+    unsigned long long *xg;       // [kXcds][kMXcdStride] granules
+    int *members;                 // [kXcds] arrival counters (zeroed before the launch)
+    int *ctl;                     // [0] abort, [1] code, [2] step, [3] hop, [4] wg
+    unsigned long long seed;
+    long long row0;               // global row id of launch row 0 (Philox key: row0 + launch row)
+    long long timeout_ticks;
+    int L, t0, Lc, Bt, b0, nb;    // launch rows b0 .. b0 + nb - 1 of the call's Bt; nb <= kMRowsMax
+    XcdmSlab s;
+    unsigned *dbg;                // WRNN_DEBUG_STAMPS: [256 wg][kMWaves][dbg_steps][kMStamps] s_memtime, or nullptr
+    int dbg_steps;
+};
+constexpr int kMStamps = 24;
+
+struct XcdmLds {
+    int stg_h1, stg, pbig, phh1, pfc1, pfc2, gh1, gh2, f2, ring, nz, cst, w3, xs, misc, total;
+};
+
+// staging of a polled vector slice, per wave: [quad][4 rows][64], value k of row j4 at
+// j4·64 + (k ^ 4·j4) (the XOR keeps the B-operand reads of the four rows on distinct banks)
+constexpr int kMStg = 4 * kMK;
+// lane l's pair i (of kMPL·NQ): quad i / kMPL; pairs p = l + 64·(i % kMPL) cover the 4 rows of the
+// quad row-major (kMK / 2 pairs per row)
+__host__ __device__ constexpr int mpoll_row(int i) { return 4 * (i / kMPL) + (((i % kMPL) * 64) / (kMK / 2)); }
+__host__ __device__ inline int mpoll_col(int lane) { return 2 * (lane % (kMK / 2)); }
+__host__ __device__ inline int mpoll_lane_off(int lane) { return ((lane / (kMK / 2)) * 512 + mpoll_col(lane)) * 8; }
+// staging position of (row j4, column kk): 4-float groups XOR-swizzled so that the B reads of the
+// 16 (row, k-slice) combinations of a wave instruction fall on distinct bank groups
+__host__ __device__ inline int mstg_at(int j4, int kk) {
+    const int g = kk >> 2, sw = kMK == 128 ? (((g >> 4) & 1) << 2) | j4 : j4;
+    return j4 * kMK + 4 * (g ^ sw) + (kk & 3);
+}
+
+__host__ __device__ inline XcdmLds xcdm_lds_layout(int nq) {
+    const int nr = 4 * nq;
+    XcdmLds l;
+    int o = 0;
+    l.stg_h1 = o; o += kMWaves * nq * kMStg;       // the h1 slice (GRU2, then W_hh1)
+    l.stg = o;    o += kMWaves * nq * kMStg;       // y / h2 / f1 slices
+    l.pbig = o;   o += 3 * 16 * nr * kMWaves;          // cross-wave partials: W_ih2·h1, then W_hh2·h2
+    l.phh1 = o;   o += 3 * 16 * nr * kMWaves;          // W_hh1·h1
+    l.pfc1 = o;   o += 16 * nr * kMWaves;
+    l.pfc2 = o;   o += 16 * nr * kMWaves;
+    l.gh1 = o;    o += 3 * 16 * nr;                    // Σ W_hh1·h1 (next step's GRU1)
+    l.gh2 = o;    o += 3 * 16 * nr;                    // Σ W_hh2·h2 (next step's GRU2)
+    l.f2 = o;     o += 16 * nr;
+    l.ring = o;   o += 2 * nr * kMRing;                // terms of steps t, t + 1 (by parity)
+    l.nz = o;     o += 2 * nr * kMNoise;
+    l.cst = o;    o += kMCst;
+    l.w3 = o;     o += 32 * 16;
+    l.xs = o;     o += 16;
+    l.misc = o;   o += 8;                              // [0] abort flag, [1] member index
+    l.total = o;
+    return l;
+}
+
+}  // namespace wrnn

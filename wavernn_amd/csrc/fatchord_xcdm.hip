@@ -1,0 +1,620 @@
+// fatchord_xcdm.hip — XCD-resident persistent kernel for MANY MoL rows (rnn 512, fc 512): the sample
+// loop of models/fatchord_version.py:201-241 for up to 16 rows per XCD (128 per launch), e.g. the
+// folds of fold_with_overlap (:293-340; BASELINE config 2 batched: 10 folds, config 3: 115 folds)
+// or independent utterances.
+//
+// The weights of the loop are held once per XCD, spread over its 32 CUs as MFMA A operands in
+// VGPRs (176 per lane and wave): workgroup c owns GRU units 16c..16c+15 (both GRUs) and fc rows
+// 16c..16c+15; wave w multiplies the K window [64w, 64w + 64) of every one of the eleven 16-row
+// weight sets (fatchord_xcdm.h, MSet) with v_mfma_f32_4x4x1_16b_f32 — 16 blocks of (4 weight rows
+// × 1 k) · (1 k × 4 batch rows) per instruction, so a batch quad of 4 rows costs what one row
+// would: block b = 4s' + g takes row group g and k-slice s' of the window, 16 MFMAs walk the
+// slice's 16 columns.  The activations (B operands) of the window come from the hop vectors: each
+// wave polls only its own 64-wide slice of every vector (granules of 4 producer workgroups),
+// stages it in LDS and reads it back as B.  K-split partial sums are reduced in the wave (the four
+// k-slices: permlane16/32 swaps) and across the 8 waves (LDS, fixed order) by the threads that
+// finish each layer, one (unit or fc row, batch row) each.
+//
+// Per step t (x = x_{t-1} of every row):
+//   A  GRU1 of the own units (gate math; W_hh1·h1_{t-1} from the previous step)  → publish h1  [hop H1]
+//   B  h1 slice → W_ih2·h1 (3 sets)                                              → barrier
+//   C  GRU2 gate math → h2, y = x_I + h1 + h2                                     → publish y, h2 [hop Y]
+//   D  W_hh1·h1 from the staged h1 slice (the next step's GRU1; fills hop Y's window)
+//   E  y slice → fc1 (1 set)                                                      → barrier
+//   F  fc1 epilogue (relu, V1 = fc1's a3 part + bias)                             → publish f1  [hop F1]
+//   G  h2 slice → W_hh2·h2 (the next step's GRU2; fills hop F1's window)
+//   H  f1 slice → fc2 (1 set)                                                     → barrier
+//   I  fc2 epilogue → f2 → barrier → fc3 partial logits of the 16 own f2 rows      → publish     [hop F2]
+//   J  sample (utils/distribution.py:87-123): ≤ 4 rows per XCD — every workgroup sums all 32
+//      producers' partials of every row and samples it itself (waves 0..3, one row each);
+//      more rows — workgroup c samples row c alone and publishes x [hop X], every workgroup
+//      gathers the x of all rows (a fifth hop instead of 32× the partial-logit traffic)
+// The conditioning terms of step t + 1 (terms GEMM, capi.cpp) and its sampler noise are loaded
+// by waves 4..7 after their f1 poll and stored into an LDS ring before the step's last barrier.
+//
+// Membership as in fatchord_xcd.hip (XCC id + per-XCD arrival counter; bounded waits).  fp32,
+// sums re-associated (MoL tolerance-checked against the oracle like the other kernels).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fatchord_loop.h"
+#include "fatchord_xcd.h"
+#include "fatchord_xcdm.h"
+#include "wrnn_device.h"
+#include "xcd_device.h"
+
+namespace wrnn {
+
+// v_mfma_f32_4x4x1_16b_f32 as inline asm, so that the weights (A) stay where they are: sets
+// MS_IH2..MS_HH2 (256 values per lane) in AGPRs, read by the MFMA directly ("a"), the W_hh1 sets
+// in VGPRs — with the builtin, hipcc keeps the weights in AGPRs and copies each one to a VGPR
+// (v_accvgpr_read) in front of its MFMA.  Hazards the compiler cannot see inside asm: the
+// accumulator chain is dst == srcC (back-to-back, no wait states); the first MFMA of a chain
+// takes srcC = 0 (no VALU-written input); the weights are written once, before the loop; the B
+// operands come straight from ds_read (waitcnt, no wait states); the VALU reads of a finished
+// accumulator wait behind mfma_drain's s_nop (which ties the accumulators).
+template <bool kAgpr>
+__device__ __forceinline__ void mfma_first(f4v &d, float a, float b) {
+    if (kAgpr) asm volatile("v_mfma_f32_4x4x1_16b_f32 %0, %1, %2, 0" : "=&v"(d) : "a"(a), "v"(b));
+    else asm volatile("v_mfma_f32_4x4x1_16b_f32 %0, %1, %2, 0" : "=&v"(d) : "v"(a), "v"(b));
+}
+template <bool kAgpr>
+__device__ __forceinline__ void mfma_acc(f4v &d, float a, float b) {
+    if (kAgpr) asm volatile("v_mfma_f32_4x4x1_16b_f32 %0, %1, %2, %0" : "+v"(d) : "a"(a), "v"(b));
+    else asm volatile("v_mfma_f32_4x4x1_16b_f32 %0, %1, %2, %0" : "+v"(d) : "v"(a), "v"(b));
+}
+// ≥ 8 wait states between the last MFMA writing these accumulators and any VALU read of them
+__device__ __forceinline__ void mfma_drain(f4v &a0) { asm volatile("s_nop 7\n\ts_nop 1" : "+v"(a0)); }
+__device__ __forceinline__ void mfma_drain(f4v &a0, f4v &a1, f4v &a2, f4v &a3) {
+    asm volatile("s_nop 7\n\ts_nop 1" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3));
+}
+__device__ __forceinline__ void mfma_drain(f4v &a0, f4v &a1, f4v &a2, f4v &a3, f4v &a4, f4v &a5) {
+    asm volatile("s_nop 7\n\ts_nop 1" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5));
+}
+
+// Σ of the wave's four k-slices (lanes l, l ^ 16, l ^ 32, l ^ 48): identical bits in all four
+__device__ __forceinline__ f4v kslice_sum(f4v d) {
+    return f4v{cross_rows(d.x), cross_rows(d.y), cross_rows(d.z), cross_rows(d.w)};
+}
+
+// Σ of the waves' partials of one output, fixed order
+__device__ __forceinline__ float sum8(const float *p) {
+    const f4v u = lds4(p);
+    if (kMWaves == 4) return (u.x + u.y) + (u.z + u.w);
+    const f4v v = lds4(p + 4);
+    return ((u.x + u.y) + (u.z + u.w)) + ((v.x + v.y) + (v.z + v.w));
+}
+
+// Poll wave w's slice [64w, 64w + 64) of a hop vector for every quad: lane l reads the granule
+// pairs (row 4q + 2h + (l >> 5), columns 64w + 2(l & 31) + {0, 1}), h = 0, 1.  Bounded.
+template <int NQ>
+__device__ __forceinline__ void mpoll(const unsigned long long *vec, int w, uint32_t tag, int *ctl, long long timeout,
+                                      int step, int hop, int *lds_abort, int lane, u4v (&v)[kMPL * NQ]) {
+    const __amdgpu_buffer_rsrc_t r = hop_rsrc(vec);
+    const int off = kMK * w * 8 + mpoll_lane_off(lane);
+    const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
+    unsigned spins = 0;
+    for (;;) {
+#pragma unroll
+        for (int i = 0; i < kMPL * NQ; ++i) v[i] = ld16_sc1(r, off + mpoll_row(i) * 512 * 8);
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < kMPL * NQ; ++i) ok &= (v[i].y == tag) & (v[i].w == tag);
+        if (ok) return;
+        if ((++spins & 63u) == 0) {
+            const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - c0) > timeout;
+            const bool other = __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+            if (late || other) {
+                if (late) record_abort(ctl, -4, step, hop, blockIdx.x);
+                *lds_abort = 1;
+                return;
+            }
+        }
+    }
+}
+
+// polled pairs → the wave's staging area ([quad][row j4][64], XOR-swizzled by 4·j4)
+template <int NQ>
+__device__ __forceinline__ void mstage(float *stg, int lane, const u4v (&v)[kMPL * NQ]) {
+#pragma unroll
+    for (int i = 0; i < kMPL * NQ; ++i) {
+        const int q = i / kMPL, j4 = mpoll_row(i) - 4 * q + lane / (kMK / 2), kk = mpoll_col(lane);
+        *reinterpret_cast<f2v *>(stg + q * kMStg + mstg_at(j4, kk)) = f2v{__uint_as_float(v[i].x), __uint_as_float(v[i].z)};
+    }
+}
+
+// Poll + stage a wave's slice of all NQ quads, at most two quads per poll round (register budget)
+template <int NQ, int Q0 = 0>
+__device__ __forceinline__ void mgather(const unsigned long long *vec, float *stg, int w, uint32_t tag, int *ctl,
+                                        long long timeout, int step, int hop, int *lds_abort, int lane) {
+    if constexpr (Q0 < NQ) {
+        constexpr int G = NQ - Q0 < 2 ? NQ - Q0 : 2;
+        u4v v[kMPL * G];
+        mpoll<G>(vec + (size_t)Q0 * 4 * 512, w, tag, ctl, timeout, step, hop, lds_abort, lane, v);
+        mstage<G>(stg + Q0 * kMStg, lane, v);
+        mgather<NQ, Q0 + G>(vec, stg, w, tag, ctl, timeout, step, hop, lds_abort, lane);
+    }
+}
+
+// B operands of quad q: lane (b, j4) needs row 4q + j4 at columns kMJ·s' + j of the window
+__device__ __forceinline__ void mbop(const float *stg, int q, int lane, f4v (&b)[kMJ / 4]) {
+    const int j4 = lane & 3, sp = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < kMJ / 4; ++i) b[i] = lds4(stg + q * kMStg + mstg_at(j4, kMJ * sp + 4 * i));
+}
+
+// NS sets from S0 against one quad's B operands, NC accumulator chains per set (MFMA j → chain j % NC)
+template <int S0, int NS, int NC>
+__device__ __forceinline__ void mmul(const float (&A)[kMSets][kMJ], const f4v (&b)[kMJ / 4], f4v (&acc)[NS][NC]) {
+    constexpr bool kAgpr = S0 < MS_HH1;
+#pragma unroll
+    for (int j = 0; j < kMJ; ++j)
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            if (j < NC) mfma_first<kAgpr>(acc[s][j % NC], A[S0 + s][j], b[j >> 2][j & 3]);
+            else mfma_acc<kAgpr>(acc[s][j % NC], A[S0 + s][j], b[j >> 2][j & 3]);
+        }
+    static_assert(NS * NC == 6 || NS * NC == 4, "mfma_drain arity");
+    if constexpr (NS * NC == 6) mfma_drain(acc[0][0], acc[0][1], acc[1][0], acc[1][1], acc[2][0], acc[2][1]);
+    else if constexpr (NS == 1) mfma_drain(acc[0][0], acc[0][1], acc[0][2], acc[0][3]);
+}
+
+// the wave's partial of every (row of the set, batch row of quad q) → P[set][row][nr][wave]
+template <int NS, int NC>
+__device__ __forceinline__ void mput(f4v (&acc)[NS][NC], float *P, int nr, int q, int lane, int wave) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        f4v d = acc[s][0];
+#pragma unroll
+        for (int cc = 1; cc < NC; ++cc) d += acc[s][cc];
+        d = kslice_sum(d);
+        if (lane < 16) {
+            const int g = lane >> 2, n = 4 * q + (lane & 3);
+            float *p = P + ((s * 16 + 4 * g) * nr + n) * kMWaves + wave;
+            p[0] = d.x;
+            p[nr * kMWaves] = d.y;
+            p[2 * nr * kMWaves] = d.z;
+            p[3 * nr * kMWaves] = d.w;
+        }
+    }
+}
+
+// One layer's MFMAs for all quads of a staged slice, partials to P
+template <int NQ, int S0, int NS, int NC>
+__device__ __forceinline__ void mlayer(const float (&A)[kMSets][kMJ], const float *stg, float *P, int lane, int wave) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        f4v b[kMJ / 4];
+        mbop(stg, q, lane, b);
+        f4v acc[NS][NC];
+        mmul<S0, NS, NC>(A, b, acc);
+        mput<NS, NC>(acc, P, 4 * NQ, q, lane, wave);
+        __builtin_amdgcn_sched_barrier(0);   // one quad's B operands and accumulators live at a time
+    }
+}
+
+// MoL sample of XCD row n by one wave: Σ of the 32 producers' partial logits + b3, then
+// mol_sample_pairs (xcd_device.h) with the row's noise terms (ring).  Wave-uniform result.
+__device__ __forceinline__ float msample(const unsigned long long *f2, int n, uint32_t tag, const float *nz,
+                                         const float *cst, int *ctl, long long timeout, int step, int *lds_abort,
+                                         int lane) {
+    const int jp = lane & 15, pg = lane >> 4;
+    const float ua = nz[jp < 5 ? 2 * jp : 0], ub = nz[jp < 5 ? 2 * jp + 1 : 0], u10 = nz[10];
+    const float b3a = cst[MC_B3 + 2 * jp], b3b = cst[MC_B3 + 2 * jp + 1];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const __amdgpu_buffer_rsrc_t rf = hop_rsrc(f2);
+    const int goff = ((n * kXcdWgs + 8 * pg) * 32 + 2 * jp) * 8;
+    const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
+    unsigned spins = 0;
+    float pa[8], pb[8];
+    for (;;) {
+        u4v v[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) v[m] = ld16_sc1(rf, goff + m * 32 * 8);
+        bool ok = true;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) ok &= (v[m].y == tag) & (v[m].w == tag);
+        if (ok) {
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                pa[m] = __uint_as_float(v[m].x);
+                pb[m] = __uint_as_float(v[m].z);
+            }
+            break;
+        }
+        if ((++spins & 63u) == 0) {
+            const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - c0) > timeout;
+            const bool other = __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+            if (late || other) {
+                if (late) record_abort(ctl, -4, step, MH_F2, blockIdx.x);
+                *lds_abort = 1;
+#pragma unroll
+                for (int m = 0; m < 8; ++m) pa[m] = pb[m] = 0.0f;
+                break;
+            }
+        }
+    }
+#pragma unroll
+    for (int w = 4; w >= 1; w /= 2)
+#pragma unroll
+        for (int m = 0; m < w; ++m) {
+            pa[m] += pa[m + w];
+            pb[m] += pb[m + w];
+        }
+    const float la = cross_rows(pa[0]) + b3a, lb = cross_rows(pb[0]) + b3b;
+    return mol_sample_pairs(la, lb, ua, ub, u10, jp);
+}
+
+// diagnostics (template kDbg, WRNN_DEBUG_STAMPS=<steps>): lane 0 of every wave stamps the shader
+// clock at the phase boundaries below; tools/stamps_xcdm.py reads them
+#define MST(kk)                                                                                              \
+    do {                                                                                                     \
+        if (kDbg && lane == 0 && t - a.t0 < a.dbg_steps)                                                     \
+            a.dbg[(((size_t)blockIdx.x * kMWaves + wave) * a.dbg_steps + (t - a.t0)) * kMStamps + (kk)] =    \
+                (unsigned)__builtin_amdgcn_s_memtime();                                                      \
+    } while (0)
+
+template <int NQ, bool kDbg>
+__global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm_kernel(XcdmArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int NR = 4 * NQ;
+    constexpr bool kTwoLevel = NQ >= 2;
+    constexpr int N = kXcdWgs * kXTerms;
+    const XcdmLds ll = xcdm_lds_layout(NQ);
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    float *stg_h1 = smem + ll.stg_h1 + wave * NQ * kMStg, *stg = smem + ll.stg + wave * NQ * kMStg;
+    float *pbig = smem + ll.pbig, *phh1 = smem + ll.phh1, *pfc1 = smem + ll.pfc1, *pfc2 = smem + ll.pfc2;
+    float *gh1 = smem + ll.gh1, *gh2 = smem + ll.gh2, *f2s = smem + ll.f2, *ring = smem + ll.ring, *nzr = smem + ll.nz;
+    float *cst = smem + ll.cst, *w3s = smem + ll.w3, *xs = smem + ll.xs;
+    int *misc = reinterpret_cast<int *>(smem + ll.misc);
+    int *abort_flag = misc;
+
+    // ---- membership: XCD k (launch rows k, k + 8, ...) and index c within it
+    if (tid == 0) {
+        const int kx = (int)xcc_id();
+        int cc = kXcdWgs;
+        if (kx < a.nb) cc = atomicAdd(&a.members[kx], 1);
+        misc[1] = (kx < a.nb && cc < kXcdWgs) ? kx * kXcdWgs + cc : -1;
+        misc[0] = 0;
+    }
+    __syncthreads();
+    const int mem = misc[1];
+    if (mem < 0) return;
+    const int k = mem / kXcdWgs, c = mem - k * kXcdWgs;
+    const int RX = (a.nb - k + kXcds - 1) / kXcds;     // rows n < RX of this XCD: launch row k + 8n
+    const int t_end = a.t0 + a.Lc;
+    unsigned long long *xg = a.xg + (size_t)k * kMXcdStride;
+    const float *S = a.slab + (size_t)c * a.s.total;
+    auto TERMS = [&](int t, int n) {
+        return a.terms + ((size_t)(t - a.t0) * a.nb + (k + kXcds * n)) * N + (size_t)c * kXTerms;
+    };
+
+    // ---- register-resident MFMA A operands: the wave's K window of all eleven sets
+    float A[kMSets][kMJ];
+#pragma unroll
+    for (int s = 0; s < kMSets; ++s)
+#pragma unroll
+        for (int j = 0; j < kMJ; ++j) A[s][j] = S[a.s.a + ((wave * kMSets + s) * kMJ + j) * 64 + lane];
+
+    // roles: (unit / fc row u, batch row n) for the layer epilogues; (logit j, row n) for fc3
+    const bool gru = tid < 16 * NR;
+    const int gu = tid & 15, gn = tid >> 4;
+    constexpr int kRingF4 = kMRing / 4;   // float4s of one row's terms
+    // ring loader threads: all (≤ 4 rows per XCD: the sampler waves store their loads after
+    // sampling) or waves 1..3 (two-level sampler: they store before it, wave 0 samples)
+    constexpr int kLdThreads = kTwoLevel ? kMThreads - 64 : kMThreads;
+    constexpr int kRingLd = (NR * kRingF4 + kLdThreads - 1) / kLdThreads;   // ring loads per thread
+
+    // terms of step t → ring slot t & 1 (rows n < RX; the rest stay zero)
+    auto ring_at = [&](int t) { return ring + (t & 1) * NR * kMRing; };
+    auto nz_at = [&](int t) { return nzr + (t & 1) * NR * kMNoise; };
+    auto noise_uu = [&](int t, int n, int kk) -> float {
+        const int lr = k + kXcds * n;
+        if (a.noise) return a.noise[((size_t)t * a.Bt + a.b0 + lr) * 11 + kk];
+        // opaque seed: hipcc would otherwise hoist all ten Philox round keys out of the step loop
+        // into (spilled) VGPRs
+        unsigned long long seed = a.seed;
+        asm volatile("" : "+s"(seed));
+        return philox_noise(seed, (unsigned long long)(a.row0 + lr), (uint32_t)t, (uint32_t)kk, 1);
+    };
+
+    // ---- prologue: constants, zeroed accumulators / ring, state, the terms of step t0
+    for (int i = tid; i < kMCst; i += kMThreads) cst[i] = S[a.s.cst + i];
+    for (int i = tid; i < 32 * 16; i += kMThreads) w3s[i] = S[a.s.w3 + i];
+    for (int i = tid; i < 2 * NR * kMRing; i += kMThreads) ring[i] = 0.0f;
+    for (int i = tid; i < 2 * NR * kMNoise; i += kMThreads) nzr[i] = 0.0f;
+    for (int i = tid; i < 3 * 16 * NR; i += kMThreads) gh1[i] = gh2[i] = 0.0f;
+    if (tid < 16) xs[tid] = 0.0f;
+    __syncthreads();
+    const bool resume = a.t0 > 0;
+    float *st = a.state + ((size_t)k * kXcdWgs + c) * kMStateW;
+    float h1v = 0.0f, h2v = 0.0f;   // h1 / h2 of (unit gu, row gn): this thread's recurrent state
+    if (resume) {
+        if (gru) {
+            h1v = st[gu * 16 + gn];
+            h2v = st[256 + gu * 16 + gn];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                gh1[(q * 16 + gu) * NR + gn] = st[512 + (q * 16 + gu) * 16 + gn];
+                gh2[(q * 16 + gu) * NR + gn] = st[1280 + (q * 16 + gu) * 16 + gn];
+            }
+        }
+        if (tid < RX) xs[tid] = st[2048 + tid];
+    }
+    for (int i = tid; i < RX * kRingF4; i += kMThreads) {
+        const int n = i / kRingF4, f = i - n * kRingF4;
+        *reinterpret_cast<f4v *>(ring_at(a.t0) + n * kMRing + 4 * f) = *reinterpret_cast<const f4v *>(TERMS(a.t0, n) + 4 * f);
+    }
+    for (int i = tid; i < 11 * RX; i += kMThreads) {
+        const int n = i / 11, kk = i - 11 * n;
+        nz_at(a.t0)[n * kMNoise + kk] = mol_noise_term(noise_uu(a.t0, n, kk), kk);
+    }
+    __syncthreads();
+
+    for (int t = a.t0; t < t_end; ++t) {
+        // per-thread indices re-derived every step from an opaque copy of threadIdx.x: otherwise
+        // hipcc hoists every per-thread address out of the loop and keeps them all live in VGPRs,
+        // which the weights leave no room for (spills)
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const int lane = tid & 63, gu = tid & 15, gn = tid >> 4;
+        const uint32_t tag = (uint32_t)t + 1u;
+        const float *rg = ring_at(t);
+        const bool more = t + 1 < t_end;
+        float x = 0.0f;
+        MST(0);
+        // ---- A: GRU1 (:208-210) of unit gu, row gn: W_ih1·x_I is rank-1 in x given the terms
+        if (gru) {
+            x = xs[gn];
+            const float *tr = rg + gn * kMRing;
+            float sr, sz, gin, ghn;
+            {
+                const int i0 = gu, i1 = 16 + gu, i2 = 32 + gu;
+                sr = (gh1[i0 * NR + gn] + cst[MC_BHH1 + i0]) + (tr[XT_P1 + gu * 3 + 0] + cst[MC_BIH1 + i0]);
+                sz = (gh1[i1 * NR + gn] + cst[MC_BHH1 + i1]) + (tr[XT_P1 + gu * 3 + 1] + cst[MC_BIH1 + i1]);
+                gin = tr[XT_P1 + gu * 3 + 2] + cst[MC_BIH1 + i2];
+                ghn = gh1[i2 * NR + gn] + cst[MC_BHH1 + i2];
+            }
+            const float r = sigmoid_(fmaf(x, cst[MC_Q1 + gu], sr));
+            const float z = sigmoid_(fmaf(x, cst[MC_Q1 + 16 + gu], sz));
+            const float nn = tanh_(fmaf(x, cst[MC_Q1 + 32 + gu], gin) + ghn * r);
+            h1v = (h1v - nn) * z + nn;
+            xpub(xg + kMHopOff[MH_H1] + gn * 512 + 16 * c + gu, tag, h1v);
+        }
+        MST(1);
+        // ---- B: the h1 slice → W_ih2[:, :R]·h1 (the GRU2 input gates, :213-214)
+        {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            mgather<NQ>(xg + kMHopOff[MH_H1], stg_h1, wave, tag, a.ctl, a.timeout_ticks, t, MH_H1, abort_flag, lane);
+            MST(2);
+            mlayer<NQ, MS_IH2, 3, 2>(A, stg_h1, pbig, lane, wave);
+            MST(3);
+        }
+        bar();
+        MST(4);
+        // ---- C: GRU2 (:212-214) gate math → h2; y = (x_I + h1) + h2 (:212, :216)
+        if (gru) {
+            const float *tr = rg + gn * kMRing;
+            float gi[3], gh[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const int i = q * 16 + gu;
+                gi[q] = sum8(pbig + (i * NR + gn) * kMWaves) + (fmaf(x, cst[MC_Q2 + i], tr[XT_P2 + gu * 3 + q]) + cst[MC_BIH2 + i]);
+                gh[q] = gh2[i * NR + gn] + cst[MC_BHH2 + i];
+            }
+            h2v = gru_gate_math(gi[0], gi[1], gi[2], gh[0], gh[1], gh[2], h2v);
+            const float xi = fmaf(cst[MC_WI0 + gu], x, tr[XT_CI + gu]);
+            const float y = (xi + h1v) + h2v;
+            xpub(xg + kMHopOff[MH_Y] + gn * 512 + 16 * c + gu, tag, y);
+            xpub(xg + kMHopOff[MH_H2] + gn * 512 + 16 * c + gu, tag, h2v);
+        }
+        MST(5);
+        // ---- D: W_hh1·h1 (the GRU1 terms of step t + 1; carried to the next chunk after the
+        // last one) from the staged h1 slice
+        mlayer<NQ, MS_HH1, 3, 2>(A, stg_h1, phh1, lane, wave);
+        MST(6);
+        // ---- E: the y slice → fc1 (:217-218)
+        {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            mgather<NQ>(xg + kMHopOff[MH_Y], stg, wave, tag, a.ctl, a.timeout_ticks, t, MH_Y, abort_flag, lane);
+            MST(7);
+            mlayer<NQ, MS_FC1, 1, 4>(A, stg, pfc1, lane, wave);
+            MST(8);
+        }
+        bar();
+        MST(9);
+        // ---- F: fc1 epilogue → f1; Σ W_hh1·h1 for the next GRU1
+        if (gru) {
+            const float f = sum8(pfc1 + (gu * NR + gn) * kMWaves) + rg[gn * kMRing + XT_V1 + gu];
+            xpub(xg + kMHopOff[MH_F1] + gn * 512 + 16 * c + gu, tag, f > 0.0f ? f : 0.0f);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const int i = q * 16 + gu;
+                gh1[i * NR + gn] = sum8(phh1 + (i * NR + gn) * kMWaves);
+            }
+        }
+        MST(10);
+        // ---- G: the h2 slice → W_hh2·h2 (the next step's GRU2; fills hop F1's window)
+        {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            mgather<NQ>(xg + kMHopOff[MH_H2], stg, wave, tag, a.ctl, a.timeout_ticks, t, MH_H2, abort_flag, lane);
+            MST(11);
+            mlayer<NQ, MS_HH2, 3, 2>(A, stg, pbig, lane, wave);
+            MST(12);
+        }
+        // ---- H: the f1 slice → fc2 (:220-221)
+        {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            mgather<NQ>(xg + kMHopOff[MH_F1], stg, wave, tag, a.ctl, a.timeout_ticks, t, MH_F1, abort_flag, lane);
+            MST(13);
+            mlayer<NQ, MS_FC2, 1, 4>(A, stg, pfc2, lane, wave);
+            MST(14);
+        }
+        bar();
+        MST(15);
+        // the terms and noise of step t + 1 → registers now, into the ring before the last barrier
+        // (issued here, they have landed by the sampler's poll of hop F2)
+        f4v rl[kRingLd];
+        float uu = 0.0f;
+        const int lt = kTwoLevel ? tid - 64 : tid;
+        if (more && lt >= 0) {
+#pragma unroll
+            for (int i = 0; i < kRingLd; ++i) {
+                const int idx = lt + kLdThreads * i;
+                if (idx < RX * kRingF4) {
+                    const int n = idx / kRingF4, f = idx - n * kRingF4;
+                    rl[i] = *reinterpret_cast<const f4v *>(TERMS(t + 1, n) + 4 * f);
+                }
+            }
+            if (lt < 11 * RX) {
+                const int n = lt / 11, kk = lt - 11 * n;
+                uu = noise_uu(t + 1, n, kk);
+            }
+        }
+        auto ring_store = [&]() {
+            if (more && lt >= 0) {
+                float *rn = ring_at(t + 1);
+#pragma unroll
+                for (int i = 0; i < kRingLd; ++i) {
+                    const int idx = lt + kLdThreads * i;
+                    if (idx < RX * kRingF4) {
+                        const int n = idx / kRingF4, f = idx - n * kRingF4;
+                        *reinterpret_cast<f4v *>(rn + n * kMRing + 4 * f) = rl[i];
+                    }
+                }
+                if (lt < 11 * RX) {
+                    const int n = lt / 11, kk = lt - 11 * n;
+                    nz_at(t + 1)[n * kMNoise + kk] = mol_noise_term(uu, kk);
+                }
+            }
+        };
+        // ---- I: fc2 epilogue → f2 (LDS); Σ W_hh2·h2 for the next GRU2
+        if (gru) {
+            const float f = sum8(pfc2 + (gu * NR + gn) * kMWaves) + rg[gn * kMRing + XT_V2 + gu];
+            f2s[gu * NR + gn] = f > 0.0f ? f : 0.0f;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const int i = q * 16 + gu;
+                gh2[i * NR + gn] = sum8(pbig + (i * NR + gn) * kMWaves);
+            }
+        }
+        MST(16);
+        bar();
+        MST(17);
+        // fc3 (:223) partial logits of the own 16 f2 rows: logit fj of row fn
+#pragma unroll
+        for (int i = tid; i < 32 * NR; i += kMThreads) {
+            const int fj = i & 31, fn = i >> 5;
+            float p = 0.0f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) p = fmaf(w3s[fj * 16 + r], f2s[r * NR + fn], p);
+            xpub(xg + kMHopOff[MH_F2] + (fn * kXcdWgs + c) * 32 + fj, tag, p);
+        }
+        MST(18);
+        if (kTwoLevel) ring_store();
+        MST(19);
+        // ---- J: sample (:225-229)
+        const float *nz = nz_at(t);
+        if (!kTwoLevel) {
+            if (wave < RX) {
+                const float xn = msample(xg + kMHopOff[MH_F2], wave, tag, nz + wave * kMNoise, cst, a.ctl, a.timeout_ticks,
+                                         t, abort_flag, lane);
+                if (lane == 0) {
+                    xs[wave] = xn;
+                    if (c == 0) a.out[(size_t)(a.b0 + k + kXcds * wave) * a.L + t] = xn;
+                }
+            }
+        } else if (wave == 0) {
+            if (c < RX) {   // this workgroup samples row c and publishes its x
+                const float xn = msample(xg + kMHopOff[MH_F2], c, tag, nz + c * kMNoise, cst, a.ctl, a.timeout_ticks, t,
+                                         abort_flag, lane);
+                if (lane == 0) {
+                    xpub(xg + kMHopOff[MH_X] + c, tag, xn);
+                    a.out[(size_t)(a.b0 + k + kXcds * c) * a.L + t] = xn;
+                }
+            }
+            // every workgroup: the x of all rows (lane n < RX polls row n)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const unsigned long long *gx = xg + kMHopOff[MH_X] + (lane < RX ? lane : 0);
+            const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
+            unsigned spins = 0;
+            unsigned long long g;
+            for (;;) {
+                g = __hip_atomic_load(gx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const bool ok = lane >= RX || (uint32_t)(g >> 32) == tag;
+                if (__ballot(!ok) == 0) break;
+                if ((++spins & 63u) == 0) {
+                    const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - c0) > a.timeout_ticks;
+                    const bool other = __hip_atomic_load(&a.ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+                    if (late || other) {
+                        if (late) record_abort(a.ctl, -4, t, MH_X, blockIdx.x);
+                        *abort_flag = 1;
+                        break;
+                    }
+                }
+            }
+            if (lane < RX) xs[lane] = __uint_as_float((uint32_t)g);
+        }
+        MST(20);
+        // ring: the terms and noise of step t + 1 (loaded in H)
+        if (!kTwoLevel) ring_store();
+        MST(21);
+        bar();
+        if (*abort_flag) return;
+    }
+    // ---- carry the recurrent state to the next time chunk
+    if (gru) {
+        st[gu * 16 + gn] = h1v;
+        st[256 + gu * 16 + gn] = h2v;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            st[512 + (q * 16 + gu) * 16 + gn] = gh1[(q * 16 + gu) * NR + gn];
+            st[1280 + (q * 16 + gu) * 16 + gn] = gh2[(q * 16 + gu) * NR + gn];
+        }
+    }
+    if (tid < RX) st[2048 + tid] = xs[tid];
+}
+
+static const void *xcdm_kernel(int nq, bool dbg) {
+    static const void *k[2][kMQuadMax] = {
+        {(const void *)fatchord_xcdm_kernel<1, false>, (const void *)fatchord_xcdm_kernel<2, false>,
+         (const void *)fatchord_xcdm_kernel<3, false>, (const void *)fatchord_xcdm_kernel<4, false>},
+        {(const void *)fatchord_xcdm_kernel<1, true>, (const void *)fatchord_xcdm_kernel<2, true>,
+         (const void *)fatchord_xcdm_kernel<3, true>, (const void *)fatchord_xcdm_kernel<4, true>}};
+    return k[dbg ? 1 : 0][nq < 1 ? 0 : nq > kMQuadMax ? kMQuadMax - 1 : nq - 1];
+}
+
+hipError_t launch_xcdm(const XcdmArgs &a, int nq, hipStream_t st) {
+    XcdmArgs args = a;
+    void *params[] = {&args};
+    const void *kf = xcdm_kernel(nq, a.dbg != nullptr);
+    return hipLaunchKernel(kf, dim3(kXcds * kXcdWgs), dim3(kMThreads), params, xcdm_lds_layout(nq).total * sizeof(float), st);
+}
+
+hipError_t prepare_xcdm_kernel(int max_lds_bytes) {
+    for (int dbg = 0; dbg < 2; ++dbg)
+        for (int nq = 1; nq <= kMQuadMax; ++nq) {
+            hipError_t e = hipFuncSetAttribute(xcdm_kernel(nq, dbg), hipFuncAttributeMaxDynamicSharedMemorySize, max_lds_bytes);
+            if (e != hipSuccess) return e;
+        }
+    return hipSuccess;
+}
+
+// largest quad count whose launch is co-resident (one workgroup per CU); 0 if none
+hipError_t xcdm_max_quads(int max_lds_bytes, int *nq_max) {
+    *nq_max = 0;
+    for (int nq = 1; nq <= kMQuadMax; ++nq) {
+        const size_t lds = xcdm_lds_layout(nq).total * sizeof(float);
+        if (lds > (size_t)max_lds_bytes) break;
+        int n = 0;
+        for (int dbg = 0; dbg < 2; ++dbg) {
+            hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xcdm_kernel(nq, dbg), kMThreads, lds);
+            if (e != hipSuccess) return e;
+            if (n < 1) return hipSuccess;
+        }
+        *nq_max = nq;
+    }
+    return hipSuccess;
+}
+
+}  // namespace wrnn
