@@ -8,8 +8,10 @@ loop → float64 post-processing).  N GPUs = N ranks, one utterance each (weak s
 utterances are independent, there is no collective in the data path).
 
 Prints ONE JSON line on rank 0.  `roofline` is computed for the persistent loop kernel from
-HIP events around its launch; `cpu_baseline` times the C oracle (oracle/, the CPU restatement)
-on a bounded slice of the same workload on this host.
+HIP events around its launch; `cpu_baseline` times the reference's own op sequence as a
+PyTorch-CPU eager restatement (oracle/torch_cpu.py: upsample, the per-step loop, float64 post) on
+this host's cores over a bounded slice of the same workload; `cpu_baseline_c_oracle` the
+single-threaded C oracle (oracle/wavernn_oracle.c) on the same slice.
 """
 from __future__ import annotations
 
@@ -53,6 +55,8 @@ def pmc_config_traffic(key: str):
     c = json.load(open(PMC_PROFILE)).get("other_configs", {}).get(key)
     return c["bytes_per_step"] if c else None
 COND_BYTES_PER_ROW_STEP = 836  # 208 fp32 conditioning + 1 fp32 output
+KERNELS = {7: "fatchord_xcdm_kernel (many rows per XCD, MFMA)", 5: "fatchord_xcd_kernel (one XCD, 32 CUs)",
+           4: "fatchord_split_kernel", 2: "fatchord_rows_kernel", 1: "fatchord_loop_kernel"}
 
 
 def loop_weight_bytes(d: syn.FatchordDims) -> int:
@@ -172,7 +176,7 @@ def main():
     ap.add_argument("--seconds", type=float, default=5.0, help="utterance length")
     ap.add_argument("--mode", default="MOL", choices=["MOL", "RAW"])
     ap.add_argument("--batched", action="store_true", help="fold-batched generate (target 11000, overlap 550)")
-    ap.add_argument("--cpu-steps", type=int, default=50000, help="oracle steps timed for cpu_baseline (0: skip)")
+    ap.add_argument("--cpu-steps", type=int, default=25000, help="loop steps timed for cpu_baseline (0: skip)")
     ap.add_argument("--other-configs", type=int, default=1, help="also time BASELINE configs 3/4/5 on this GPU (N=1)")
     ap.add_argument("--fold-batched", type=int, default=1, help="also time the same utterance through generate(batched=True)")
     args = ap.parse_args()
@@ -257,8 +261,7 @@ def main():
                 "mode": args.mode, "rnn_dims": d.rnn_dims, "fc_dims": d.fc_dims, "utterance_s": args.seconds,
                 "loop_steps": L, "rows": B, "samples_per_utterance": int(n_samples / args.steps),
                 "parallelism": f"utterance-sharded x{world}",
-                "kernel": {5: "fatchord_xcd_kernel (one XCD, 32 CUs)", 4: "fatchord_split_kernel", 2: "fatchord_rows_kernel",
-                           1: "fatchord_loop_kernel"}.get(info["last_path"], str(info["last_path"])),
+                "kernel": KERNELS.get(info["last_path"], str(info["last_path"])),
             },
             "rtf_per_gpu": value / world / d.sample_rate,
             "loop_kernel_ms": loop_ms_max,
@@ -267,11 +270,15 @@ def main():
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": pmc_traffic_bytes(args.mode, args.batched, args.seconds),
+                "traffic_from": os.path.relpath(PMC_PROFILE, REPO) if pmc_traffic_bytes(args.mode, args.batched,
+                                                                                       args.seconds) else None,
                 "note": "achieved = algorithmic bytes (all loop weights fp32 per step + 836 B/row-step) per launch "
                         "/ launch time (HIP events); the weights are LDS/VGPR-resident on one XCD's 32 CUs "
                         "(fatchord_xcd_kernel), the kernel is hand-off-latency bound. "
-                        f"traffic = 2 x FETCH_SIZE + WRITE_SIZE bytes per launch (gfx950 read correction) from "
-                        f"{os.path.basename(PMC_PROFILE)}: conditioning-terms reads; the hand-offs stay in the XCD's L2",
+                        f"traffic = 2 x FETCH_SIZE + WRITE_SIZE bytes per launch (gfx950 read correction), NOT measured "
+                        f"in this run: read from the committed rocprofv3 --pmc passes of the same command in "
+                        f"{os.path.relpath(PMC_PROFILE, REPO)} (traffic_from): conditioning-terms reads; the hand-offs "
+                        f"stay in the XCD's L2",
             },
         }
         if args.fold_batched and not args.batched and args.mode == "MOL":
@@ -290,8 +297,10 @@ def main():
                 "rows": int(condb.shape[1]), "loop_steps": int(condb.shape[0]), "device_ms": kb,
                 "us_per_loop_step": kb * 1e3 / condb.shape[0],
                 "kernel_path": model.loop_handle().info["last_path"],
+                "kernel": KERNELS.get(model.loop_handle().info["last_path"]),
                 "note": "same 5 s utterance, generate(batched=True) as gen_wavernn.py runs it with the 800k "
-                        "hparams (10 folds: XCD-resident kernel, 8 + 2 rows in two launches) + conditioning-terms GEMM",
+                        "hparams (10 folds in one launch) + conditioning-terms GEMM; rate over the whole "
+                        "generate() wall time (upsample, loop, float64 post)",
             }
         if args.other_configs and world == 1 and args.mode == "MOL":
             rec["other_configs"] = other_configs(dev)
@@ -300,20 +309,35 @@ def main():
                 if tr is not None and "roofline" in v:
                     v["roofline"]["traffic_per_step"] = tr   # HBM bytes per loop step (PMC, corrected)
         if args.cpu_steps > 0 and world == 1:
-            from oracle import oracle
-            cpu = cond.transpose(0, 1).cpu().numpy()
+            # the reference's op sequence on this host's cores: PyTorch-CPU eager (oracle/torch_cpu.py),
+            # whole pre/post + a bounded slice of the loop; and the C oracle on the same slice
+            from oracle import oracle, torch_cpu
+            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
             n = min(args.cpu_steps, L)
+            noise = syn.make_noise(d.mode, B, L, d.n_classes, 7)
+            r = torch_cpu.timed_generate(state, d, mel[0].numpy(), args.batched, target, overlap, True, noise,
+                                         loop_steps=n, threads=threads)
+            frac = n / L
+            t_cpu = r["loop_s"] + frac * (r["pre_s"] + r["post_s"])
+            rec["cpu_baseline"] = {
+                "value": n * B / t_cpu, "unit": "samples/s", "cores": r["threads"], "kind": "port",
+                "sample": f"PyTorch-CPU eager generate() (oracle/torch_cpu.py, torch.set_num_threads({r['threads']})): "
+                          f"upsample + fold of the whole {args.seconds:g} s mel, {n} of {L} loop steps x {B} row(s), "
+                          f"float64 post-processing of the whole utterance; value = loop-step samples / (loop time + "
+                          f"{frac:.3f} x pre/post time)",
+                "loop_s": r["loop_s"], "pre_s": r["pre_s"], "post_s": r["post_s"],
+                "rtf": n * B / t_cpu / d.sample_rate}
+            cpu = cond.transpose(0, 1).cpu().numpy()
             mels_c = np.ascontiguousarray(cpu[:, :n, :d.feat_dims])
             aux_c = np.ascontiguousarray(cpu[:, :n, d.feat_dims:])
-            noise = syn.make_noise(d.mode, B, n, d.n_classes, 7)
             oracle.build()
             t = time.perf_counter()
-            oracle.fatchord_loop(state, d.mode, mels_c, aux_c, noise)
+            oracle.fatchord_loop(state, d.mode, mels_c, aux_c, noise[:n])
             dt = time.perf_counter() - t
-            rec["cpu_baseline"] = {"value": n * B / dt, "unit": "samples/s", "cores": 1, "kind": "port",
-                                   "sample": f"{n} of {L} loop steps x {B} row(s), same weights/conditioning, "
-                                             f"C oracle (oracle/wavernn_oracle.c, gcc -O3, 1 thread)",
-                                   "seconds": dt}
+            rec["cpu_baseline_c_oracle"] = {"value": n * B / dt, "unit": "samples/s", "cores": 1, "kind": "port",
+                                            "sample": f"{n} of {L} loop steps x {B} row(s), same weights/conditioning, "
+                                                      f"C oracle (oracle/wavernn_oracle.c, gcc -O3, 1 thread), loop only",
+                                            "seconds": dt}
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()

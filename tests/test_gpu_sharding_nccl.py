@@ -1,0 +1,40 @@
+"""generate_sharded under the "nccl" backend (RCCL) on the GPU box: world_size 1, one process,
+127.0.0.1 rendezvous.  The gathered float64 audio equals each utterance's own generate()
+bit-for-bit (the same Philox keying by global utterance index)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+
+from wavernn_amd import sharding
+from wavernn_amd import synthetic as syn
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_generate_sharded_nccl_world1():
+    from wavernn_amd.fatchord_version import WaveRNN
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        d = syn.DEFAULT_MOL
+        m = WaveRNN(**d.ctor_kwargs()).to(dev)
+        m.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in syn.make_fatchord_state(d, 3).items()})
+        mels = [torch.from_numpy(syn.make_mel(d.feat_dims, T, 10 + T))[None] for T in (30, 41, 25)]
+        got = sharding.generate_sharded(m, mels, False, 11000, 550, True, base_seed=77, device=dev)
+        assert dist.get_backend() == "nccl" and len(got) == 3
+        for i, mel in enumerate(mels):
+            ref = m.generate(mel, None, False, 11000, 550, True, seed=77 + i, verbose=False)
+            assert got[i].dtype == np.float64 and np.array_equal(got[i], ref)
+    finally:
+        dist.destroy_process_group()

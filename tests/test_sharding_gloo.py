@@ -22,8 +22,11 @@ def _free_port():
 
 
 def fake_audio(i: int) -> np.ndarray:
+    """float64 audio with bits float32 cannot hold: the gather must not round it"""
     rng = np.random.default_rng(100 + i)
-    return rng.uniform(-1, 1, size=1000 + 37 * i).astype(np.float32).astype(np.float64)
+    a = rng.uniform(-1, 1, size=1000 + 37 * i)
+    assert not np.array_equal(a, a.astype(np.float32).astype(np.float64))
+    return a
 
 
 def _worker(rank, world, port, n_items, q):
@@ -53,7 +56,9 @@ def test_sharded_gather_reassembles_in_order(n_items):
         assert p.exitcode == 0
     assert len(got) == n_items
     for i, a in enumerate(got):
-        np.testing.assert_array_equal(np.asarray(a), fake_audio(i))
+        a = np.asarray(a)
+        assert a.dtype == np.float64
+        np.testing.assert_array_equal(a, fake_audio(i))     # bit-exact float64
 
 
 def test_shard_indices_partition():

@@ -1,10 +1,10 @@
 """Phase timings of the many-row XCD kernel from its debug stamps (WRNN_DEBUG_STAMPS).
 
-    python tools/stamps_xcdm.py B [steps] [L]
+    python tools/stamps_xcdm.py B [L]
 
-Runs one MoL generate through the kernel with stamps on, then prints, per wave, the median over
-steps (skipping the first 20) and over workgroups of each phase boundary relative to the step
-start, in shader cycles and µs (clock from s_memtime vs the device time of the launch)."""
+Runs one MoL generate through the kernel with stamps on (48 steps, kept in LDS, from step 16),
+then prints, per wave, the median over those steps and over workgroups of each phase boundary
+relative to the step start, in shader cycles and µs (clock: stamped step vs the launch's mean)."""
 import os
 import subprocess
 import sys
@@ -22,10 +22,9 @@ NAMES = {0: "step start", 1: "A  GRU1 + publish h1", 2: "B  h1 poll done", 3: "B
 
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 10
-    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 300
-    L = int(sys.argv[3]) if len(sys.argv) > 3 else 2000
+    L = int(sys.argv[2]) if len(sys.argv) > 2 else 2000
     path = "/tmp/xcdm_stamps.bin" if not os.environ.get("GRAFT_REPO_ROOT") else "gpurun_out/xcdm_stamps.bin"
-    env = dict(os.environ, WRNN_DEBUG_STAMPS=str(steps), WRNN_DEBUG_FILE=path, WRNN_PATH="xcdm")
+    env = dict(os.environ, WRNN_DEBUG_STAMPS="1", WRNN_DEBUG_FILE=path, WRNN_PATH="xcdm")
     code = (
         "import numpy as np, torch, sys; sys.path.insert(0, '.')\n"
         "from wavernn_amd import synthetic as syn\nfrom wavernn_amd.loop import FatchordLoop\n"
@@ -42,18 +41,19 @@ def main():
     st = raw[3:].view(np.uint32).reshape(G, S, K).astype(np.int64)
     waves = 4
     st = st.reshape(G // waves, waves, S, K)
-    live = st[:, 0, 25, 0] != 0                      # workgroups of XCDs that had rows
+    live = st[:, 0, 5, 0] != 0                       # workgroups of XCDs that had rows
     st = st[live]
-    base = st[:, :, 20:, 0:1]
-    step = np.median(np.diff(st[:, 0, 20:, 0], axis=1))
-    cyc_per_us = step / (ms * 1e3 / L)               # stamped step vs the launch's mean step
-    print(f"B={B}: {live.sum()} workgroups, median step {step:.0f} cycles; launch {ms * 1e3 / L:.3f} us/step "
-          f"(stamped steps slower by the stamps themselves); ~{cyc_per_us:.0f} cycles/us")
+    base = st[:, :, :, 0:1]
+    step = np.median(np.diff(st[:, 0, :, 0], axis=1))
+    real = np.median(np.diff(st[:, 0, :, K - 1], axis=1))   # s_memrealtime (100 MHz) at step start
+    cyc_per_us = step / (real / 100.0)
+    print(f"B={B}: {live.sum()} workgroups, median stamped step {step:.0f} cycles = {real / 100:.3f} us "
+          f"(shader clock {cyc_per_us / 1e3:.2f} GHz); launch incl. the stamp dump {ms * 1e3 / L:.3f} us/step")
     for w in range(waves):
-        rel = st[:, w, 20:, :] - base[:, w]
+        rel = st[:, w, :, :] - base[:, w]
         print(f"-- wave {w}")
         prev = 0.0
-        for k in range(1, K):
+        for k in range(1, K - 1):
             v = rel[..., k]
             v = v[(v > 0) & (v < 10 * step)]
             if v.size == 0:

@@ -53,6 +53,7 @@ hipError_t xcds_occupancy(int *blocks_per_cu);
 hipError_t launch_xcdm(const XcdmArgs &a, int nq, hipStream_t st);
 hipError_t prepare_xcdm_kernel(int max_lds_bytes);
 hipError_t xcdm_max_quads(int max_lds_bytes, int *nq_max);
+hipError_t launch_philox_fill(float *out, unsigned long long seed, long long row0, int nb, int t0, int Lc, hipStream_t st);
 }  // namespace wrnn
 
 using namespace wrnn;
@@ -145,7 +146,8 @@ struct wrnn_ctx {
     bool xcdm_ok = false;
     int xcdm_nq = 0;                                // largest co-resident quad count (rows per XCD / 4)
     XcdmSlab xms{};
-    float *d_xmslab = nullptr, *d_xmstate = nullptr;
+    float *d_xmslab = nullptr, *d_xmstate = nullptr, *d_xmnoise = nullptr;
+    size_t xmnoise_cap = 0;
     unsigned long long *d_xmxg = nullptr;
 };
 
@@ -1579,10 +1581,10 @@ int generate_xcdm(wrnn_t *h, const float *cond, int B, int L, const float *noise
     if (!h->d_xmstate) HIP_TRY(h, hipMalloc(&h->d_xmstate, (size_t)kXcds * kXcdWgs * kMStateW * sizeof(float)));
     const int rows_max = kXcds * 4 * h->xcdm_nq;
     const float one = 1.0f, zero = 0.0f;
-    // diagnostics: WRNN_DEBUG_STAMPS=<steps> WRNN_DEBUG_FILE=<path>: per-wave phase stamps of
-    // the first launch ([256 · kMWaves][steps][kMStamps] shader clocks, int32 header)
+    // diagnostics: WRNN_DEBUG_STAMPS=1 WRNN_DEBUG_FILE=<path>: per-wave phase stamps of the first
+    // launch ([256 · kMWaves][kMDbgSteps][kMStamps] shader clocks, int32 header)
     const char *dbg_env = std::getenv("WRNN_DEBUG_STAMPS");
-    const int dbg_steps = dbg_env ? std::min(L, std::atoi(dbg_env)) : 0;
+    const int dbg_steps = (dbg_env && std::atoi(dbg_env) > 0 && L >= kMDbgSkip + kMDbgSteps) ? kMDbgSteps : 0;
     const size_t dbg_n = (size_t)kXcds * kXcdWgs * kMWaves * dbg_steps * kMStamps;
     unsigned *d_dbg = nullptr;
     if (dbg_steps > 0) {
@@ -1593,7 +1595,8 @@ int generate_xcdm(wrnn_t *h, const float *cond, int B, int L, const float *noise
         const int nb = std::min(rows_max, B - b0);
         const int nq = (((nb + kXcds - 1) / kXcds) + 3) / 4;   // quads on the fullest XCD
         const int Lc_max = (int)std::max(1.0, std::min((double)L, budget / ((double)nb * (N + h->KXc))));
-        if (grow(h, h->d_X, h->X_cap, (size_t)Lc_max * nb * h->KXc) || grow(h, h->d_T, h->T_cap, (size_t)Lc_max * nb * N))
+        if (grow(h, h->d_X, h->X_cap, (size_t)Lc_max * nb * h->KXc) || grow(h, h->d_T, h->T_cap, (size_t)Lc_max * nb * N) ||
+            (!noise && grow(h, h->d_xmnoise, h->xmnoise_cap, (size_t)Lc_max * nb * 11)))
             return WRNN_EHIP;
         HIP_TRY(h, hipMemsetAsync(h->d_xmxg, 0, xg_words * 8, st));   // tags restart at 1
         for (int t0 = 0; t0 < L; t0 += Lc_max) {
@@ -1608,7 +1611,18 @@ int generate_xcdm(wrnn_t *h, const float *cond, int B, int L, const float *noise
             XcdmArgs a{};
             a.slab = h->d_xmslab;
             a.terms = h->d_T;
-            a.noise = noise;
+            if (noise) {   // injected [L][B][11]
+                a.noise = noise;
+                a.nz_t0 = 0;
+                a.nz_ts = B;
+                a.nz_b0 = b0;
+            } else {       // Philox, drawn for this chunk by a small kernel first ([Lc][nb][11])
+                HIP_TRY(h, launch_philox_fill(h->d_xmnoise, seed, row_offset + b0, nb, t0, Lc, st));
+                a.noise = h->d_xmnoise;
+                a.nz_t0 = t0;
+                a.nz_ts = nb;
+                a.nz_b0 = 0;
+            }
             a.out = out;
             a.state = h->d_xmstate;
             a.xg = h->d_xmxg;
@@ -1624,8 +1638,7 @@ int generate_xcdm(wrnn_t *h, const float *cond, int B, int L, const float *noise
             a.b0 = b0;
             a.nb = nb;
             a.s = h->xms;
-            a.dbg = (b0 == 0 && t0 == 0) ? d_dbg : nullptr;
-            a.dbg_steps = std::min(dbg_steps, Lc);
+            a.dbg = (b0 == 0 && t0 == 0 && Lc >= kMDbgSkip + kMDbgSteps) ? d_dbg : nullptr;
             HIP_TRY(h, launch_xcdm(a, nq, st));
         }
     }
@@ -2170,7 +2183,7 @@ void wrnn_destroy(wrnn_t *h) {
                     (void *)h->d_dmflags, (void *)h->d_dmxg, (void *)h->d_sgslab, (void *)h->d_sfslab,
                     (void *)h->d_sWt, (void *)h->g2.d_slab, (void *)h->g2.d_Wt, (void *)h->dm2.d_slab,
                     (void *)h->d_gact, (void *)h->d_xslab, (void *)h->d_xWt, (void *)h->d_xstate, (void *)h->d_xgx,
-                    (void *)h->d_members, (void *)h->d_xmslab, (void *)h->d_xmstate, (void *)h->d_xmxg})
+                    (void *)h->d_members, (void *)h->d_xmslab, (void *)h->d_xmstate, (void *)h->d_xmxg, (void *)h->d_xmnoise})
         if (p) (void)hipFree(p);
     if (h->blas) (void)rocblas_destroy_handle(h->blas);
     delete h;

@@ -66,7 +66,10 @@ constexpr int kMStateW = 256 + 256 + 768 + 768 + 16;
 struct XcdmArgs {
     const float *slab;            // [kXcdWgs][slab.total]
     const float *terms;           // [Lc][nb][kXcdWgs·kXTerms], row (t - t0)·nb + launch row
-    const float *noise;           // [L][Bt][11] or nullptr (Philox)
+    const float *noise;           // uniforms of step t, launch row lr: noise[((t - nz_t0)·nz_ts + nz_b0 + lr)·11 + k],
+                                  // or nullptr (in-kernel Philox)
+    long long nz_ts;
+    int nz_t0, nz_b0;
     float *out;                   // [Bt][L]
     float *state;                 // [kXcds][kXcdWgs][kMStateW]
     unsigned long long *xg;       // [kXcds][kMXcdStride] granules
@@ -77,13 +80,12 @@ struct XcdmArgs {
     long long timeout_ticks;
     int L, t0, Lc, Bt, b0, nb;    // launch rows b0 .. b0 + nb - 1 of the call's Bt; nb <= kMRowsMax
     XcdmSlab s;
-    unsigned *dbg;                // WRNN_DEBUG_STAMPS: [256 wg][kMWaves][dbg_steps][kMStamps] s_memtime, or nullptr
-    int dbg_steps;
+    unsigned *dbg;                // WRNN_DEBUG_STAMPS: [256 wg][kMWaves][kMDbgSteps][kMStamps] s_memtime, or nullptr
 };
-constexpr int kMStamps = 24;
+constexpr int kMStamps = 24, kMDbgSteps = 48, kMDbgSkip = 16;
 
 struct XcdmLds {
-    int stg_h1, stg, pbig, phh1, pfc1, pfc2, gh1, gh2, f2, ring, nz, cst, w3, xs, misc, total;
+    int stg_h1, stg, pbig, phh1, pfc1, pfc2, gh1, gh2, f2, ring, nz, cst, w3, xs, misc, dbg, total;
 };
 
 // staging of a polled vector slice, per wave: [quad][4 rows][64], value k of row j4 at
@@ -100,13 +102,18 @@ __host__ __device__ inline int mstg_at(int j4, int kk) {
     const int g = kk >> 2, sw = kMK == 128 ? (((g >> 4) & 1) << 2) | j4 : j4;
     return j4 * kMK + 4 * (g ^ sw) + (kk & 3);
 }
+// the 16x16x4 form (≥ 3 quads): all 16 rows of a wave's slice in one [16][kMK] image, row n's
+// 4-float group g at g ^ n (the 16 rows of a B read fall on distinct bank groups)
+__host__ __device__ inline int mstg16_at(int n, int kk) { return n * kMK + 4 * ((kk >> 2) ^ n) + (kk & 3); }
+// quads whose MFMAs use v_mfma_f32_16x16x4_f32 (rows on N, no k-slices) instead of the 4x4x1 form
+__host__ __device__ constexpr bool xcdm_big(int nq) { return nq >= 3; }
 
-__host__ __device__ inline XcdmLds xcdm_lds_layout(int nq) {
-    const int nr = 4 * nq;
+__host__ __device__ inline XcdmLds xcdm_lds_layout(int nq, bool dbg = false) {
+    const int nr = 4 * nq, nq_stg = xcdm_big(nq) ? kMQuadMax : nq;
     XcdmLds l;
     int o = 0;
-    l.stg_h1 = o; o += kMWaves * nq * kMStg;       // the h1 slice (GRU2, then W_hh1)
-    l.stg = o;    o += kMWaves * nq * kMStg;       // y / h2 / f1 slices
+    l.stg_h1 = o; o += kMWaves * nq_stg * kMStg;   // the h1 slice (GRU2, then W_hh1)
+    l.stg = o;    o += kMWaves * nq_stg * kMStg;   // y / h2 / f1 slices
     l.pbig = o;   o += 3 * 16 * nr * kMWaves;          // cross-wave partials: W_ih2·h1, then W_hh2·h2
     l.phh1 = o;   o += 3 * 16 * nr * kMWaves;          // W_hh1·h1
     l.pfc1 = o;   o += 16 * nr * kMWaves;
@@ -120,6 +127,7 @@ __host__ __device__ inline XcdmLds xcdm_lds_layout(int nq) {
     l.w3 = o;     o += 32 * 16;
     l.xs = o;     o += 16;
     l.misc = o;   o += 8;                              // [0] abort flag, [1] member index
+    l.dbg = o;    o += dbg ? kMDbgSteps * kMWaves * kMStamps : 0;
     l.total = o;
     return l;
 }

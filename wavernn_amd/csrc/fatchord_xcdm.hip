@@ -63,14 +63,24 @@ __device__ __forceinline__ void mfma_acc(f4v &d, float a, float b) {
     if (kAgpr) asm volatile("v_mfma_f32_4x4x1_16b_f32 %0, %1, %2, %0" : "+v"(d) : "a"(a), "v"(b));
     else asm volatile("v_mfma_f32_4x4x1_16b_f32 %0, %1, %2, %0" : "+v"(d) : "v"(a), "v"(b));
 }
-// ≥ 8 wait states between the last MFMA writing these accumulators and any VALU read of them
-__device__ __forceinline__ void mfma_drain(f4v &a0) { asm volatile("s_nop 7\n\ts_nop 1" : "+v"(a0)); }
-__device__ __forceinline__ void mfma_drain(f4v &a0, f4v &a1, f4v &a2, f4v &a3) {
-    asm volatile("s_nop 7\n\ts_nop 1" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3));
+// the same for v_mfma_f32_16x16x4_f32 (16 weight rows × 16 batch rows × 4 columns)
+template <bool kAgpr>
+__device__ __forceinline__ void mfma16_first(f4v &d, float a, float b) {
+    if (kAgpr) asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, 0" : "=&v"(d) : "a"(a), "v"(b));
+    else asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, 0" : "=&v"(d) : "v"(a), "v"(b));
 }
-__device__ __forceinline__ void mfma_drain(f4v &a0, f4v &a1, f4v &a2, f4v &a3, f4v &a4, f4v &a5) {
-    asm volatile("s_nop 7\n\ts_nop 1" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5));
+template <bool kAgpr>
+__device__ __forceinline__ void mfma16_acc(f4v &d, float a, float b) {
+    if (kAgpr) asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(d) : "a"(a), "v"(b));
+    else asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(d) : "v"(a), "v"(b));
 }
+__device__ __forceinline__ void mfma16_drain_begin() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory"); }
+
+// ≥ 8 wait states between the last MFMA writing an accumulator and any VALU read of it: one
+// s_nop pair, then an empty asm per accumulator that "redefines" it (volatile asm keep their
+// order, so every read of the accumulator comes after the nops)
+__device__ __forceinline__ void mfma_drain_begin() { asm volatile("s_nop 7\n\ts_nop 1" ::: "memory"); }
+__device__ __forceinline__ void mfma_tie(f4v &a) { asm volatile("" : "+v"(a)); }
 
 // Σ of the wave's four k-slices (lanes l, l ^ 16, l ^ 32, l ^ 48): identical bits in all four
 __device__ __forceinline__ f4v kslice_sum(f4v d) {
@@ -114,12 +124,15 @@ __device__ __forceinline__ void mpoll(const unsigned long long *vec, int w, uint
 }
 
 // polled pairs → the wave's staging area ([quad][row j4][64], XOR-swizzled by 4·j4)
-template <int NQ>
-__device__ __forceinline__ void mstage(float *stg, int lane, const u4v (&v)[kMPL * NQ]) {
+// (quads q0 .. q0 + NQ - 1 of the wave's staging image; the 16x16x4 form's swizzle depends on
+// the absolute row)
+template <int NQ, bool kBig>
+__device__ __forceinline__ void mstage(float *stg, int q0, int lane, const u4v (&v)[kMPL * NQ]) {
 #pragma unroll
     for (int i = 0; i < kMPL * NQ; ++i) {
-        const int q = i / kMPL, j4 = mpoll_row(i) - 4 * q + lane / (kMK / 2), kk = mpoll_col(lane);
-        *reinterpret_cast<f2v *>(stg + q * kMStg + mstg_at(j4, kk)) = f2v{__uint_as_float(v[i].x), __uint_as_float(v[i].z)};
+        const int q = q0 + i / kMPL, j4 = mpoll_row(i) - 4 * (i / kMPL) + lane / (kMK / 2), kk = mpoll_col(lane);
+        const int at = kBig ? mstg16_at(4 * q + j4, kk) : q * kMStg + mstg_at(j4, kk);
+        *reinterpret_cast<f2v *>(stg + at) = f2v{__uint_as_float(v[i].x), __uint_as_float(v[i].z)};
     }
 }
 
@@ -131,32 +144,9 @@ __device__ __forceinline__ void mgather(const unsigned long long *vec, float *st
         constexpr int G = NQ - Q0 < 2 ? NQ - Q0 : 2;
         u4v v[kMPL * G];
         mpoll<G>(vec + (size_t)Q0 * 4 * 512, w, tag, ctl, timeout, step, hop, lds_abort, lane, v);
-        mstage<G>(stg + Q0 * kMStg, lane, v);
+        mstage<G, xcdm_big(NQ)>(stg, Q0, lane, v);
         mgather<NQ, Q0 + G>(vec, stg, w, tag, ctl, timeout, step, hop, lds_abort, lane);
     }
-}
-
-// B operands of quad q: lane (b, j4) needs row 4q + j4 at columns kMJ·s' + j of the window
-__device__ __forceinline__ void mbop(const float *stg, int q, int lane, f4v (&b)[kMJ / 4]) {
-    const int j4 = lane & 3, sp = lane >> 4;
-#pragma unroll
-    for (int i = 0; i < kMJ / 4; ++i) b[i] = lds4(stg + q * kMStg + mstg_at(j4, kMJ * sp + 4 * i));
-}
-
-// NS sets from S0 against one quad's B operands, NC accumulator chains per set (MFMA j → chain j % NC)
-template <int S0, int NS, int NC>
-__device__ __forceinline__ void mmul(const float (&A)[kMSets][kMJ], const f4v (&b)[kMJ / 4], f4v (&acc)[NS][NC]) {
-    constexpr bool kAgpr = S0 < MS_HH1;
-#pragma unroll
-    for (int j = 0; j < kMJ; ++j)
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            if (j < NC) mfma_first<kAgpr>(acc[s][j % NC], A[S0 + s][j], b[j >> 2][j & 3]);
-            else mfma_acc<kAgpr>(acc[s][j % NC], A[S0 + s][j], b[j >> 2][j & 3]);
-        }
-    static_assert(NS * NC == 6 || NS * NC == 4, "mfma_drain arity");
-    if constexpr (NS * NC == 6) mfma_drain(acc[0][0], acc[0][1], acc[1][0], acc[1][1], acc[2][0], acc[2][1]);
-    else if constexpr (NS == 1) mfma_drain(acc[0][0], acc[0][1], acc[0][2], acc[0][3]);
 }
 
 // the wave's partial of every (row of the set, batch row of quad q) → P[set][row][nr][wave]
@@ -179,18 +169,109 @@ __device__ __forceinline__ void mput(f4v (&acc)[NS][NC], float *P, int nr, int q
     }
 }
 
-// One layer's MFMAs for all quads of a staged slice, partials to P
+// One layer: NS sets from S0 against every quad of the staged slice, the wave's partials to P.
+// MFMA order: k-chunk (4 columns) outer, then column, quad, set; NC accumulator chains per
+// (quad, set) (column j → chain j % NC) so that ≥ 8 independent chains interleave — the
+// dependent-accumulator latency of v_mfma_f32_4x4x1_16b_f32 is ≈ 52 cycles for an 8-cycle issue
+// (tools/mfma4_bench.hip), and one wave per SIMD has no partner to hide it.
 template <int NQ, int S0, int NS, int NC>
 __device__ __forceinline__ void mlayer(const float (&A)[kMSets][kMJ], const float *stg, float *P, int lane, int wave) {
+    constexpr bool kAgpr = S0 < MS_HH1;
+    const int j4 = lane & 3, sp = lane >> 4;
+    f4v acc[NQ][NS][NC];
+    // B operands double-buffered: chunk jc + 1's LDS reads are in flight during chunk jc's MFMAs
+    // (the asm MFMAs are volatile, so hipcc would not hoist a read above them by itself)
+    f4v b[2][NQ];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        f4v b[kMJ / 4];
-        mbop(stg, q, lane, b);
-        f4v acc[NS][NC];
-        mmul<S0, NS, NC>(A, b, acc);
-        mput<NS, NC>(acc, P, 4 * NQ, q, lane, wave);
-        __builtin_amdgcn_sched_barrier(0);   // one quad's B operands and accumulators live at a time
+    for (int q = 0; q < NQ; ++q) b[0][q] = lds4(stg + q * kMStg + mstg_at(j4, kMJ * sp));
+#pragma unroll
+    for (int jc = 0; jc < kMJ / 4; ++jc) {
+        if (jc + 1 < kMJ / 4) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) b[(jc + 1) & 1][q] = lds4(stg + q * kMStg + mstg_at(j4, kMJ * sp + 4 * (jc + 1)));
+        }
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int j = 4 * jc + jj;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q)
+#pragma unroll
+                for (int s = 0; s < NS; ++s) {
+                    if (j < NC) mfma_first<kAgpr>(acc[q][s][j % NC], A[S0 + s][j], b[jc & 1][q][jj]);
+                    else mfma_acc<kAgpr>(acc[q][s][j % NC], A[S0 + s][j], b[jc & 1][q][jj]);
+                }
+        }
     }
+    mfma_drain_begin();
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int cc = 0; cc < NC; ++cc) mfma_tie(acc[q][s][cc]);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) mput<NS, NC>(acc[q], P, 4 * NQ, q, lane, wave);
+}
+
+// The same layer with v_mfma_f32_16x16x4_f32 (≥ 3 quads): lane l = 16g + n takes batch row n and
+// columns kMK·w + kMJ·g + i of MFMA i (the A operands are the 4x4x1 form's, lane for lane: row
+// l & 15, column kMK·w + kMJ·(l >> 4) + i); the K reduction happens inside the MFMA, so lane l
+// ends with rows 4(l >> 4) + r, r = 0..3, of batch row n, summed over the wave's whole window.
+template <int NQ, int S0, int NS, int NC>
+__device__ __forceinline__ void mlayer16(const float (&A)[kMSets][kMJ], const float *stg, float *P, int lane, int wave) {
+    constexpr bool kAgpr = S0 < MS_HH1;
+    constexpr int NR = 4 * NQ;
+    const int n = lane & 15, g = lane >> 4;
+    f4v acc[NS][NC];
+    f4v b[2];
+    b[0] = lds4(stg + mstg16_at(n, kMJ * g));
+#pragma unroll
+    for (int ic = 0; ic < kMJ / 4; ++ic) {
+        if (ic + 1 < kMJ / 4) b[(ic + 1) & 1] = lds4(stg + mstg16_at(n, kMJ * g + 4 * (ic + 1)));
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) {
+            const int i = 4 * ic + ii;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                if (i < NC) mfma16_first<kAgpr>(acc[s][i % NC], A[S0 + s][i], b[ic & 1][ii]);
+                else mfma16_acc<kAgpr>(acc[s][i % NC], A[S0 + s][i], b[ic & 1][ii]);
+            }
+        }
+    }
+    mfma16_drain_begin();
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int cc = 0; cc < NC; ++cc) mfma_tie(acc[s][cc]);
+    if (n < NR) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            f4v d = acc[s][0];
+#pragma unroll
+            for (int cc = 1; cc < NC; ++cc) d += acc[s][cc];
+            float *p = P + ((s * 16 + 4 * g) * NR + n) * kMWaves + wave;
+            p[0] = d.x;
+            p[NR * kMWaves] = d.y;
+            p[2 * NR * kMWaves] = d.z;
+            p[3 * NR * kMWaves] = d.w;
+        }
+    }
+}
+
+// the layer in the kernel's MFMA form
+template <int NQ, int S0, int NS>
+__device__ __forceinline__ void mlayer_any(const float (&A)[kMSets][kMJ], const float *stg, float *P, int lane, int wave);
+
+// accumulator chains per (quad, set) for ≥ 8 in flight
+template <int NQ, int NS>
+struct MChains {
+    static constexpr int v = (8 + NQ * NS - 1) / (NQ * NS);
+};
+
+template <int NQ, int S0, int NS>
+__device__ __forceinline__ void mlayer_any(const float (&A)[kMSets][kMJ], const float *stg, float *P, int lane, int wave) {
+    if constexpr (xcdm_big(NQ)) mlayer16<NQ, S0, NS, 2>(A, stg, P, lane, wave);
+    else mlayer<NQ, S0, NS, MChains<NQ, NS>::v>(A, stg, P, lane, wave);
 }
 
 // MoL sample of XCD row n by one wave: Σ of the 32 producers' partial logits + b3, then
@@ -245,12 +326,13 @@ __device__ __forceinline__ float msample(const unsigned long long *f2, int n, ui
     return mol_sample_pairs(la, lb, ua, ub, u10, jp);
 }
 
-// diagnostics (template kDbg, WRNN_DEBUG_STAMPS=<steps>): lane 0 of every wave stamps the shader
-// clock at the phase boundaries below; tools/stamps_xcdm.py reads them
+// diagnostics (template kDbg, WRNN_DEBUG_STAMPS=1): lane 0 of every wave stamps the shader clock
+// at the phase boundaries below into LDS for kMDbgSteps steps from t0 + kMDbgSkip (global stores
+// would sit in vmcnt ahead of the polls); copied out after the loop; tools/stamps_xcdm.py reads them
 #define MST(kk)                                                                                              \
     do {                                                                                                     \
-        if (kDbg && lane == 0 && t - a.t0 < a.dbg_steps)                                                     \
-            a.dbg[(((size_t)blockIdx.x * kMWaves + wave) * a.dbg_steps + (t - a.t0)) * kMStamps + (kk)] =    \
+        if (kDbg && lane == 0 && (unsigned)(t - a.t0 - kMDbgSkip) < (unsigned)kMDbgSteps)                   \
+            dbgs[((t - a.t0 - kMDbgSkip) * kMWaves + wave) * kMStamps + (kk)] =                              \
                 (unsigned)__builtin_amdgcn_s_memtime();                                                      \
     } while (0)
 
@@ -260,14 +342,16 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
     constexpr int NR = 4 * NQ;
     constexpr bool kTwoLevel = NQ >= 2;
     constexpr int N = kXcdWgs * kXTerms;
-    const XcdmLds ll = xcdm_lds_layout(NQ);
+    const XcdmLds ll = xcdm_lds_layout(NQ, kDbg);
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    float *stg_h1 = smem + ll.stg_h1 + wave * NQ * kMStg, *stg = smem + ll.stg + wave * NQ * kMStg;
+    constexpr int kStgQ = xcdm_big(NQ) ? kMQuadMax : NQ;   // staged quads per wave
+    float *stg_h1 = smem + ll.stg_h1 + wave * kStgQ * kMStg, *stg = smem + ll.stg + wave * kStgQ * kMStg;
     float *pbig = smem + ll.pbig, *phh1 = smem + ll.phh1, *pfc1 = smem + ll.pfc1, *pfc2 = smem + ll.pfc2;
     float *gh1 = smem + ll.gh1, *gh2 = smem + ll.gh2, *f2s = smem + ll.f2, *ring = smem + ll.ring, *nzr = smem + ll.nz;
     float *cst = smem + ll.cst, *w3s = smem + ll.w3, *xs = smem + ll.xs;
     int *misc = reinterpret_cast<int *>(smem + ll.misc);
     int *abort_flag = misc;
+    unsigned *dbgs = reinterpret_cast<unsigned *>(smem + ll.dbg);
 
     // ---- membership: XCD k (launch rows k, k + 8, ...) and index c within it
     if (tid == 0) {
@@ -310,7 +394,7 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
     auto nz_at = [&](int t) { return nzr + (t & 1) * NR * kMNoise; };
     auto noise_uu = [&](int t, int n, int kk) -> float {
         const int lr = k + kXcds * n;
-        if (a.noise) return a.noise[((size_t)t * a.Bt + a.b0 + lr) * 11 + kk];
+        if (a.noise) return a.noise[((size_t)(t - a.nz_t0) * a.nz_ts + a.nz_b0 + lr) * 11 + kk];
         // opaque seed: hipcc would otherwise hoist all ten Philox round keys out of the step loop
         // into (spilled) VGPRs
         unsigned long long seed = a.seed;
@@ -363,6 +447,8 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         const bool more = t + 1 < t_end;
         float x = 0.0f;
         MST(0);
+        if (kDbg && lane == 0 && (unsigned)(t - a.t0 - kMDbgSkip) < (unsigned)kMDbgSteps)
+            dbgs[((t - a.t0 - kMDbgSkip) * kMWaves + wave) * kMStamps + kMStamps - 1] = (unsigned)__builtin_amdgcn_s_memrealtime();
         // ---- A: GRU1 (:208-210) of unit gu, row gn: W_ih1·x_I is rank-1 in x given the terms
         if (gru) {
             x = xs[gn];
@@ -387,7 +473,7 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             mgather<NQ>(xg + kMHopOff[MH_H1], stg_h1, wave, tag, a.ctl, a.timeout_ticks, t, MH_H1, abort_flag, lane);
             MST(2);
-            mlayer<NQ, MS_IH2, 3, 2>(A, stg_h1, pbig, lane, wave);
+            mlayer_any<NQ, MS_IH2, 3>(A, stg_h1, pbig, lane, wave);
             MST(3);
         }
         bar();
@@ -411,14 +497,14 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         MST(5);
         // ---- D: W_hh1·h1 (the GRU1 terms of step t + 1; carried to the next chunk after the
         // last one) from the staged h1 slice
-        mlayer<NQ, MS_HH1, 3, 2>(A, stg_h1, phh1, lane, wave);
+        mlayer_any<NQ, MS_HH1, 3>(A, stg_h1, phh1, lane, wave);
         MST(6);
         // ---- E: the y slice → fc1 (:217-218)
         {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             mgather<NQ>(xg + kMHopOff[MH_Y], stg, wave, tag, a.ctl, a.timeout_ticks, t, MH_Y, abort_flag, lane);
             MST(7);
-            mlayer<NQ, MS_FC1, 1, 4>(A, stg, pfc1, lane, wave);
+            mlayer_any<NQ, MS_FC1, 1>(A, stg, pfc1, lane, wave);
             MST(8);
         }
         bar();
@@ -439,7 +525,7 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             mgather<NQ>(xg + kMHopOff[MH_H2], stg, wave, tag, a.ctl, a.timeout_ticks, t, MH_H2, abort_flag, lane);
             MST(11);
-            mlayer<NQ, MS_HH2, 3, 2>(A, stg, pbig, lane, wave);
+            mlayer_any<NQ, MS_HH2, 3>(A, stg, pbig, lane, wave);
             MST(12);
         }
         // ---- H: the f1 slice → fc2 (:220-221)
@@ -447,7 +533,7 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             mgather<NQ>(xg + kMHopOff[MH_F1], stg, wave, tag, a.ctl, a.timeout_ticks, t, MH_F1, abort_flag, lane);
             MST(13);
-            mlayer<NQ, MS_FC2, 1, 4>(A, stg, pfc2, lane, wave);
+            mlayer_any<NQ, MS_FC2, 1>(A, stg, pfc2, lane, wave);
             MST(14);
         }
         bar();
@@ -562,6 +648,13 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         bar();
         if (*abort_flag) return;
     }
+    if (kDbg && a.dbg) {
+        __syncthreads();
+        for (int i = tid; i < kMDbgSteps * kMWaves * kMStamps; i += kMThreads) {
+            const int stp = i / (kMWaves * kMStamps), w = (i / kMStamps) % kMWaves, kk = i % kMStamps;
+            a.dbg[(((size_t)blockIdx.x * kMWaves + w) * kMDbgSteps + stp) * kMStamps + kk] = dbgs[i];
+        }
+    }
     // ---- carry the recurrent state to the next time chunk
     if (gru) {
         st[gu * 16 + gn] = h1v;
@@ -573,6 +666,22 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         }
     }
     if (tid < RX) st[2048 + tid] = xs[tid];
+}
+
+// The in-kernel Philox draws of launch rows [0, nb) for steps [t0, t0 + Lc) into the injected-noise
+// layout [Lc][nb][11] (philox_noise keyed by (seed, row0 + row, step, k) exactly as the loop
+// kernels key them: bit-identical audio), so the loop only loads them
+__global__ void philox_fill_kernel(float *out, unsigned long long seed, long long row0, int nb, int t0, int Lc) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long long)Lc * nb * 11) return;
+    const int kk = (int)(i % 11), lr = (int)((i / 11) % nb), dt = (int)(i / (11LL * nb));
+    out[i] = philox_noise(seed, (unsigned long long)(row0 + lr), (uint32_t)(t0 + dt), (uint32_t)kk, 1);
+}
+
+hipError_t launch_philox_fill(float *out, unsigned long long seed, long long row0, int nb, int t0, int Lc, hipStream_t st) {
+    const long long n = (long long)Lc * nb * 11;
+    hipLaunchKernelGGL(philox_fill_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out, seed, row0, nb, t0, Lc);
+    return hipGetLastError();
 }
 
 static const void *xcdm_kernel(int nq, bool dbg) {
@@ -588,7 +697,8 @@ hipError_t launch_xcdm(const XcdmArgs &a, int nq, hipStream_t st) {
     XcdmArgs args = a;
     void *params[] = {&args};
     const void *kf = xcdm_kernel(nq, a.dbg != nullptr);
-    return hipLaunchKernel(kf, dim3(kXcds * kXcdWgs), dim3(kMThreads), params, xcdm_lds_layout(nq).total * sizeof(float), st);
+    return hipLaunchKernel(kf, dim3(kXcds * kXcdWgs), dim3(kMThreads), params,
+                           xcdm_lds_layout(nq, a.dbg != nullptr).total * sizeof(float), st);
 }
 
 hipError_t prepare_xcdm_kernel(int max_lds_bytes) {
@@ -604,10 +714,10 @@ hipError_t prepare_xcdm_kernel(int max_lds_bytes) {
 hipError_t xcdm_max_quads(int max_lds_bytes, int *nq_max) {
     *nq_max = 0;
     for (int nq = 1; nq <= kMQuadMax; ++nq) {
-        const size_t lds = xcdm_lds_layout(nq).total * sizeof(float);
-        if (lds > (size_t)max_lds_bytes) break;
+        if (xcdm_lds_layout(nq, true).total * sizeof(float) > (size_t)max_lds_bytes) break;
         int n = 0;
         for (int dbg = 0; dbg < 2; ++dbg) {
+            const size_t lds = xcdm_lds_layout(nq, dbg).total * sizeof(float);
             hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xcdm_kernel(nq, dbg), kMThreads, lds);
             if (e != hipSuccess) return e;
             if (n < 1) return hipSuccess;

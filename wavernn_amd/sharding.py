@@ -25,21 +25,20 @@ def gather_audio(local: Dict[int, np.ndarray], n_items: int, device: torch.devic
                  group=None) -> Optional[List[np.ndarray]]:
     """Collect {global index: float64 audio} from every rank on rank 0, in global order.
 
-    Shapes differ per utterance, so each rank packs its outputs into a [n_slots, L_max] fp32
-    tensor plus an int64 [n_slots, 2] (index, length) table; two all-gathers move them.  fp32
-    on the wire is exact for the float32 samples the loop produced; the float64 host
-    post-processing is re-applied by the caller if it needs it (here the values are the
-    already post-processed float64 audio cast to fp32, as save_wav writes)."""
+    Shapes differ per utterance, so each rank packs its outputs into a [n_slots, L_max] float64
+    tensor plus an int64 [n_slots, 2] (index, length) table; two all-gathers move them.  The
+    audio travels as the float64 generate() returns (RCCL and gloo move float64 natively), so
+    rank 0's list is bit-identical to what each rank's generate() produced."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     n_slots = (n_items + world - 1) // world
     lens = torch.tensor([max((len(v) for v in local.values()), default=0)], dtype=torch.int64, device=device)
     dist.all_reduce(lens, op=dist.ReduceOp.MAX, group=group)
     L = int(lens.item())
-    data = torch.zeros(n_slots, max(L, 1), dtype=torch.float32, device=device)
+    data = torch.zeros(n_slots, max(L, 1), dtype=torch.float64, device=device)
     meta = torch.full((n_slots, 2), -1, dtype=torch.int64, device=device)
     for s, (idx, audio) in enumerate(sorted(local.items())):
-        data[s, :len(audio)] = torch.as_tensor(np.asarray(audio, dtype=np.float32), device=device)
+        data[s, :len(audio)] = torch.as_tensor(np.asarray(audio, dtype=np.float64), device=device)
         meta[s, 0], meta[s, 1] = idx, len(audio)
     if dist.get_backend(group) == "nccl":
         all_data = torch.empty(world * n_slots, data.shape[1], dtype=data.dtype, device=device)
@@ -58,7 +57,7 @@ def gather_audio(local: Dict[int, np.ndarray], n_items: int, device: torch.devic
     all_data = all_data.cpu().numpy()
     for row, (idx, n) in enumerate(all_meta.cpu().numpy()):
         if idx >= 0:
-            out[int(idx)] = all_data[row, :int(n)].astype(np.float64)
+            out[int(idx)] = all_data[row, :int(n)].copy()
     return out  # type: ignore[return-value]
 
 
