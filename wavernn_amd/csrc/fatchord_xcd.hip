@@ -77,7 +77,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
         for (int i = 2; i < 8; ++i) misc[i] = 0;
     }
     __syncthreads();
-    const int mem = misc[1];
+    const int mem = __builtin_amdgcn_readfirstlane(misc[1]);   // wave-uniform: hop addresses in SGPRs
     if (mem < 0) return;
     const int k = mem / kXcdWgs, c = mem - k * kXcdWgs;
     const int b = a.b0 + k;

@@ -149,6 +149,46 @@ __device__ __forceinline__ void mgather(const unsigned long long *vec, float *st
     }
 }
 
+// A poll of the first G quads of a wave's slice that rides along an off-critical MFMA layer: the
+// layer calls step(jc) at the start of each of its 8 k-chunks, and the poll's loads are issued
+// once, at chunk kAt, so that the rest of the layer's MFMAs cover their round trip; finish()
+// checks them after the layer (a wait only if they have not landed) and falls back to the
+// bounded blocking poll (mpoll) if some granule still carried an old tag.  (Checking inside the
+// layer would stall it: reading the loaded registers waits for the loads, landed or not.)
+struct MPollNone {
+    __device__ __forceinline__ void step(int) {}
+};
+template <int G, int kAt>
+struct MPoll {
+    u4v v[G > 0 ? kMPL * G : 1];
+    __amdgpu_buffer_rsrc_t r;
+    int off;
+    uint32_t tag;
+    __device__ __forceinline__ MPoll(const unsigned long long *vec, int w, uint32_t tag_, int lane) : off(0), tag(tag_) {
+        if constexpr (G > 0) {
+            r = hop_rsrc(vec);
+            off = kMK * w * 8 + mpoll_lane_off(lane);
+        }
+    }
+    __device__ __forceinline__ void step(int jc) {
+        if constexpr (G > 0) {
+            if (jc == kAt) {
+#pragma unroll
+                for (int i = 0; i < kMPL * G; ++i) v[i] = ld16_sc1(r, off + mpoll_row(i) * 512 * 8);
+            }
+        }
+    }
+    __device__ __forceinline__ void finish(const unsigned long long *vec, int w, int *ctl, long long timeout, int step_,
+                                           int hop, int *lds_abort, int lane) {
+        if constexpr (G > 0) {
+            bool ok = true;
+#pragma unroll
+            for (int i = 0; i < kMPL * G; ++i) ok &= (v[i].y == tag) & (v[i].w == tag);
+            if (__ballot(!ok) != 0) mpoll<G>(vec, w, tag, ctl, timeout, step_, hop, lds_abort, lane, v);
+        }
+    }
+};
+
 // the wave's partial of every (row of the set, batch row of quad q) → P[set][row][nr][wave]
 template <int NS, int NC>
 __device__ __forceinline__ void mput(f4v (&acc)[NS][NC], float *P, int nr, int q, int lane, int wave) {
@@ -174,8 +214,9 @@ __device__ __forceinline__ void mput(f4v (&acc)[NS][NC], float *P, int nr, int q
 // (quad, set) (column j → chain j % NC) so that ≥ 8 independent chains interleave — the
 // dependent-accumulator latency of v_mfma_f32_4x4x1_16b_f32 is ≈ 52 cycles for an 8-cycle issue
 // (tools/mfma4_bench.hip), and one wave per SIMD has no partner to hide it.
-template <int NQ, int S0, int NS, int NC>
-__device__ __forceinline__ void mlayer(const float (&A)[kMSets][kMJ], const float *stg, float *P, int lane, int wave) {
+template <int NQ, int S0, int NS, int NC, typename Hook = MPollNone>
+__device__ __forceinline__ void mlayer(const float (&A)[kMSets][kMJ], const float *stg, float *P, int lane, int wave,
+                                       Hook &&hook = Hook{}) {
     constexpr bool kAgpr = S0 < MS_HH1;
     const int j4 = lane & 3, sp = lane >> 4;
     f4v acc[NQ][NS][NC];
@@ -186,6 +227,7 @@ __device__ __forceinline__ void mlayer(const float (&A)[kMSets][kMJ], const floa
     for (int q = 0; q < NQ; ++q) b[0][q] = lds4(stg + q * kMStg + mstg_at(j4, kMJ * sp));
 #pragma unroll
     for (int jc = 0; jc < kMJ / 4; ++jc) {
+        hook.step(jc);
         if (jc + 1 < kMJ / 4) {
 #pragma unroll
             for (int q = 0; q < NQ; ++q) b[(jc + 1) & 1][q] = lds4(stg + q * kMStg + mstg_at(j4, kMJ * sp + 4 * (jc + 1)));
@@ -217,8 +259,9 @@ __device__ __forceinline__ void mlayer(const float (&A)[kMSets][kMJ], const floa
 // columns kMK·w + kMJ·g + i of MFMA i (the A operands are the 4x4x1 form's, lane for lane: row
 // l & 15, column kMK·w + kMJ·(l >> 4) + i); the K reduction happens inside the MFMA, so lane l
 // ends with rows 4(l >> 4) + r, r = 0..3, of batch row n, summed over the wave's whole window.
-template <int NQ, int S0, int NS, int NC>
-__device__ __forceinline__ void mlayer16(const float (&A)[kMSets][kMJ], const float *stg, float *P, int lane, int wave) {
+template <int NQ, int S0, int NS, int NC, typename Hook = MPollNone>
+__device__ __forceinline__ void mlayer16(const float (&A)[kMSets][kMJ], const float *stg, float *P, int lane, int wave,
+                                         Hook &&hook = Hook{}) {
     constexpr bool kAgpr = S0 < MS_HH1;
     constexpr int NR = 4 * NQ;
     const int n = lane & 15, g = lane >> 4;
@@ -227,6 +270,7 @@ __device__ __forceinline__ void mlayer16(const float (&A)[kMSets][kMJ], const fl
     b[0] = lds4(stg + mstg16_at(n, kMJ * g));
 #pragma unroll
     for (int ic = 0; ic < kMJ / 4; ++ic) {
+        hook.step(ic);
         if (ic + 1 < kMJ / 4) b[(ic + 1) & 1] = lds4(stg + mstg16_at(n, kMJ * g + 4 * (ic + 1)));
 #pragma unroll
         for (int ii = 0; ii < 4; ++ii) {
@@ -258,9 +302,6 @@ __device__ __forceinline__ void mlayer16(const float (&A)[kMSets][kMJ], const fl
     }
 }
 
-// the layer in the kernel's MFMA form
-template <int NQ, int S0, int NS>
-__device__ __forceinline__ void mlayer_any(const float (&A)[kMSets][kMJ], const float *stg, float *P, int lane, int wave);
 
 // accumulator chains per (quad, set) for ≥ 8 in flight
 template <int NQ, int NS>
@@ -268,10 +309,36 @@ struct MChains {
     static constexpr int v = (8 + NQ * NS - 1) / (NQ * NS);
 };
 
-template <int NQ, int S0, int NS>
-__device__ __forceinline__ void mlayer_any(const float (&A)[kMSets][kMJ], const float *stg, float *P, int lane, int wave) {
-    if constexpr (xcdm_big(NQ)) mlayer16<NQ, S0, NS, 2>(A, stg, P, lane, wave);
-    else mlayer<NQ, S0, NS, MChains<NQ, NS>::v>(A, stg, P, lane, wave);
+// the layer in the kernel's MFMA form (optionally with a poll riding along)
+template <int NQ, int S0, int NS, typename Hook = MPollNone>
+__device__ __forceinline__ void mlayer_any(const float (&A)[kMSets][kMJ], const float *stg, float *P, int lane, int wave,
+                                           Hook &&hook = Hook{}) {
+    // (16x16x4: ≥ 3 sets interleaved already cover its ≈ 40-cycle dependent latency)
+    if constexpr (xcdm_big(NQ)) mlayer16<NQ, S0, NS, 2>(A, stg, P, lane, wave, hook);
+    else mlayer<NQ, S0, NS, MChains<NQ, NS>::v>(A, stg, P, lane, wave, hook);
+}
+
+// quads polled beside an off-critical layer (none above one quad: the registers are not there),
+// and the k-chunk at which its loads are issued
+template <int NQ>
+struct MRide {
+    static constexpr int G = NQ == 1 ? 1 : 2;
+    static constexpr int at = 3;
+};
+
+// Poll + stage the hop vector `vec` (all quads) with its first MRide group already polled by `pr`
+template <int NQ>
+__device__ __forceinline__ void mgather_rest(MPoll<MRide<NQ>::G, MRide<NQ>::at> &pr, const unsigned long long *vec,
+                                             float *stg, int w, int *ctl, long long timeout, int step, int hop,
+                                             int *lds_abort, int lane) {
+    constexpr int G = MRide<NQ>::G;
+    if constexpr (G > 0) {
+        pr.finish(vec, w, ctl, timeout, step, hop, lds_abort, lane);
+        mstage<G, xcdm_big(NQ)>(stg, 0, lane, pr.v);
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    mgather<NQ, G>(vec, stg, w, pr.tag, ctl, timeout, step, hop, lds_abort, lane);
 }
 
 // MoL sample of XCD row n by one wave: Σ of the 32 producers' partial logits + b3, then
@@ -362,7 +429,7 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         misc[0] = 0;
     }
     __syncthreads();
-    const int mem = misc[1];
+    const int mem = __builtin_amdgcn_readfirstlane(misc[1]);   // wave-uniform: hop addresses in SGPRs
     if (mem < 0) return;
     const int k = mem / kXcdWgs, c = mem - k * kXcdWgs;
     const int RX = (a.nb - k + kXcds - 1) / kXcds;     // rows n < RX of this XCD: launch row k + 8n
@@ -496,13 +563,13 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         }
         MST(5);
         // ---- D: W_hh1·h1 (the GRU1 terms of step t + 1; carried to the next chunk after the
-        // last one) from the staged h1 slice
-        mlayer_any<NQ, MS_HH1, 3>(A, stg_h1, phh1, lane, wave);
+        // last one) from the staged h1 slice, with the y poll of E riding along (hop Y's window)
+        MPoll<MRide<NQ>::G, MRide<NQ>::at> py(xg + kMHopOff[MH_Y], wave, tag, lane);
+        mlayer_any<NQ, MS_HH1, 3>(A, stg_h1, phh1, lane, wave, py);
         MST(6);
         // ---- E: the y slice → fc1 (:217-218)
         {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            mgather<NQ>(xg + kMHopOff[MH_Y], stg, wave, tag, a.ctl, a.timeout_ticks, t, MH_Y, abort_flag, lane);
+            mgather_rest<NQ>(py, xg + kMHopOff[MH_Y], stg, wave, a.ctl, a.timeout_ticks, t, MH_Y, abort_flag, lane);
             MST(7);
             mlayer_any<NQ, MS_FC1, 1>(A, stg, pfc1, lane, wave);
             MST(8);
@@ -520,18 +587,17 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
             }
         }
         MST(10);
-        // ---- G: the h2 slice → W_hh2·h2 (the next step's GRU2; fills hop F1's window)
+        // ---- G: the h2 slice → W_hh2·h2 (the next step's GRU2), with the f1 poll of H riding
+        // along (hop F1's window); f1 is staged once the layer's B reads of the h2 slice are done
         {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             mgather<NQ>(xg + kMHopOff[MH_H2], stg, wave, tag, a.ctl, a.timeout_ticks, t, MH_H2, abort_flag, lane);
             MST(11);
-            mlayer_any<NQ, MS_HH2, 3>(A, stg, pbig, lane, wave);
+            MPoll<MRide<NQ>::G, MRide<NQ>::at> pf(xg + kMHopOff[MH_F1], wave, tag, lane);
+            mlayer_any<NQ, MS_HH2, 3>(A, stg, pbig, lane, wave, pf);
             MST(12);
-        }
-        // ---- H: the f1 slice → fc2 (:220-221)
-        {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            mgather<NQ>(xg + kMHopOff[MH_F1], stg, wave, tag, a.ctl, a.timeout_ticks, t, MH_F1, abort_flag, lane);
+            // ---- H: the f1 slice → fc2 (:220-221)
+            mgather_rest<NQ>(pf, xg + kMHopOff[MH_F1], stg, wave, a.ctl, a.timeout_ticks, t, MH_F1, abort_flag, lane);
             MST(13);
             mlayer_any<NQ, MS_FC2, 1>(A, stg, pfc2, lane, wave);
             MST(14);
