@@ -451,8 +451,8 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
     const bool gru = tid < 16 * NR;
     const int gu = tid & 15, gn = tid >> 4;
     constexpr int kRingF4 = kMRing / 4;   // float4s of one row's terms
-    // ring loader threads: all (≤ 4 rows per XCD: the sampler waves store their loads after
-    // sampling) or waves 1..3 (two-level sampler: they store before it, wave 0 samples)
+    // ring loader threads: all (≤ 4 rows per XCD: sampler waves store their loads after sampling,
+    // the others before it) or waves 1..3 (two-level sampler: they store before it, wave 0 samples)
     constexpr int kLdThreads = kTwoLevel ? kMThreads - 64 : kMThreads;
     constexpr int kRingLd = (NR * kRingF4 + kLdThreads - 1) / kLdThreads;   // ring loads per thread
 
@@ -571,9 +571,11 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         {
             mgather_rest<NQ>(py, xg + kMHopOff[MH_Y], stg, wave, a.ctl, a.timeout_ticks, t, MH_Y, abort_flag, lane);
             MST(7);
-            mlayer_any<NQ, MS_FC1, 1>(A, stg, pfc1, lane, wave);
-            MST(8);
         }
+        // h2 was published with y: its poll rides along fc1 and is checked in G, after F
+        MPoll<MRide<NQ>::G, MRide<NQ>::at> ph(xg + kMHopOff[MH_H2], wave, tag, lane);
+        mlayer_any<NQ, MS_FC1, 1>(A, stg, pfc1, lane, wave, ph);
+        MST(8);
         bar();
         MST(9);
         // ---- F: fc1 epilogue → f1; Σ W_hh1·h1 for the next GRU1
@@ -590,8 +592,7 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         // ---- G: the h2 slice → W_hh2·h2 (the next step's GRU2), with the f1 poll of H riding
         // along (hop F1's window); f1 is staged once the layer's B reads of the h2 slice are done
         {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            mgather<NQ>(xg + kMHopOff[MH_H2], stg, wave, tag, a.ctl, a.timeout_ticks, t, MH_H2, abort_flag, lane);
+            mgather_rest<NQ>(ph, xg + kMHopOff[MH_H2], stg, wave, a.ctl, a.timeout_ticks, t, MH_H2, abort_flag, lane);
             MST(11);
             MPoll<MRide<NQ>::G, MRide<NQ>::at> pf(xg + kMHopOff[MH_F1], wave, tag, lane);
             mlayer_any<NQ, MS_HH2, 3>(A, stg, pbig, lane, wave, pf);
@@ -608,7 +609,9 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         // (issued here, they have landed by the sampler's poll of hop F2)
         f4v rl[kRingLd];
         float uu = 0.0f;
-        const int lt = kTwoLevel ? tid - 64 : tid;
+        // (direct sampler: loader index counted from the last thread, so that with few rows the
+        // loads sit in waves that do not sample and store them before J)
+        const int lt = kTwoLevel ? tid - 64 : kMThreads - 1 - tid;
         if (more && lt >= 0) {
 #pragma unroll
             for (int i = 0; i < kRingLd; ++i) {
@@ -663,7 +666,7 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
             xpub(xg + kMHopOff[MH_F2] + (fn * kXcdWgs + c) * 32 + fj, tag, p);
         }
         MST(18);
-        if (kTwoLevel) ring_store();
+        if (kTwoLevel || wave >= RX) ring_store();
         MST(19);
         // ---- J: sample (:225-229)
         const float *nz = nz_at(t);
@@ -709,7 +712,7 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         }
         MST(20);
         // ring: the terms and noise of step t + 1 (loaded in H)
-        if (!kTwoLevel) ring_store();
+        if (!kTwoLevel && wave < RX) ring_store();
         MST(21);
         bar();
         if (*abort_flag) return;
