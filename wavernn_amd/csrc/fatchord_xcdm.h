@@ -108,16 +108,24 @@ __host__ __device__ inline int mstg16_at(int n, int kk) { return n * kMK + 4 * (
 // quads whose MFMAs use v_mfma_f32_16x16x4_f32 (rows on N, no k-slices) instead of the 4x4x1 form
 __host__ __device__ constexpr bool xcdm_big(int nq) { return nq >= 3; }
 
+// floats of one set's cross-wave partials: [row][nr][wave] (16x16x4 form, k-slices reduced in
+// the MFMA) or [wave][row][nr + 1 pad][4 k-slices] (4x4x1 form, k-slices left unreduced: the
+// consumer sums 16 values instead of the producer running a permlane reduction)
+__host__ __device__ constexpr int xcdm_pstride_row(int nq) { return 4 * (4 * nq) + 4; }
+__host__ __device__ constexpr int xcdm_pset(int nq) {
+    return xcdm_big(nq) ? 16 * 4 * nq * kMWaves : kMWaves * 16 * xcdm_pstride_row(nq);
+}
+
 __host__ __device__ inline XcdmLds xcdm_lds_layout(int nq, bool dbg = false) {
     const int nr = 4 * nq, nq_stg = xcdm_big(nq) ? kMQuadMax : nq;
     XcdmLds l;
     int o = 0;
     l.stg_h1 = o; o += kMWaves * nq_stg * kMStg;   // the h1 slice (GRU2, then W_hh1)
     l.stg = o;    o += kMWaves * nq_stg * kMStg;   // y / h2 / f1 slices
-    l.pbig = o;   o += 3 * 16 * nr * kMWaves;          // cross-wave partials: W_ih2·h1, then W_hh2·h2
-    l.phh1 = o;   o += 3 * 16 * nr * kMWaves;          // W_hh1·h1
-    l.pfc1 = o;   o += 16 * nr * kMWaves;
-    l.pfc2 = o;   o += 16 * nr * kMWaves;
+    l.pbig = o;   o += 3 * xcdm_pset(nq);              // cross-wave partials: W_ih2·h1, then W_hh2·h2
+    l.phh1 = o;   o += 3 * xcdm_pset(nq);              // W_hh1·h1
+    l.pfc1 = o;   o += xcdm_pset(nq);
+    l.pfc2 = o;   o += xcdm_pset(nq);
     l.gh1 = o;    o += 3 * 16 * nr;                    // Σ W_hh1·h1 (next step's GRU1)
     l.gh2 = o;    o += 3 * 16 * nr;                    // Σ W_hh2·h2 (next step's GRU2)
     l.f2 = o;     o += 16 * nr;

@@ -189,23 +189,41 @@ struct MPoll {
     }
 };
 
-// the wave's partial of every (row of the set, batch row of quad q) → P[set][row][nr][wave]
-template <int NS, int NC>
-__device__ __forceinline__ void mput(f4v (&acc)[NS][NC], float *P, int nr, int q, int lane, int wave) {
+// the wave's partials of every (row of the set, batch row of quad q), k-slices unreduced: lane
+// l = 16·sp + 4g + j holds rows 4g + i (i = 0..3) of batch row 4q + j over k-slice sp →
+// P[set][wave][row][n][sp] (row stride xcdm_pstride_row: the 64 lanes of one store hit 64 banks)
+template <int NQ, int NS, int NC>
+__device__ __forceinline__ void mput(f4v (&acc)[NS][NC], float *P, int q, int lane, int wave) {
+    constexpr int S = xcdm_pstride_row(NQ);
+    const int g = (lane >> 2) & 3, n = 4 * q + (lane & 3), sp = lane >> 4;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         f4v d = acc[s][0];
 #pragma unroll
         for (int cc = 1; cc < NC; ++cc) d += acc[s][cc];
-        d = kslice_sum(d);
-        if (lane < 16) {
-            const int g = lane >> 2, n = 4 * q + (lane & 3);
-            float *p = P + ((s * 16 + 4 * g) * nr + n) * kMWaves + wave;
-            p[0] = d.x;
-            p[nr * kMWaves] = d.y;
-            p[2 * nr * kMWaves] = d.z;
-            p[3 * nr * kMWaves] = d.w;
-        }
+        float *p = P + ((s * kMWaves + wave) * 16 + 4 * g) * S + 4 * n + sp;
+        p[0] = d.x;
+        p[S] = d.y;
+        p[2 * S] = d.z;
+        p[3 * S] = d.w;
+    }
+}
+
+// Σ over waves (and k-slices) of the partials of output (set·16 + row) i, batch row n; fixed order
+template <int NQ>
+__device__ __forceinline__ float mpart(const float *P, int i, int n) {
+    if constexpr (xcdm_big(NQ)) {
+        return sum8(P + (i * (4 * NQ) + n) * kMWaves);
+    } else {
+        constexpr int S = xcdm_pstride_row(NQ);
+        const int s = i >> 4, r = i & 15;
+        f4v u[kMWaves];
+#pragma unroll
+        for (int w = 0; w < kMWaves; ++w) u[w] = lds4(P + ((s * kMWaves + w) * 16 + r) * S + 4 * n);
+        float t[kMWaves];
+#pragma unroll
+        for (int w = 0; w < kMWaves; ++w) t[w] = (u[w].x + u[w].y) + (u[w].z + u[w].w);
+        return (t[0] + t[1]) + (t[2] + t[3]);
     }
 }
 
@@ -252,7 +270,7 @@ __device__ __forceinline__ void mlayer(const float (&A)[kMSets][kMJ], const floa
 #pragma unroll
             for (int cc = 0; cc < NC; ++cc) mfma_tie(acc[q][s][cc]);
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) mput<NS, NC>(acc[q], P, 4 * NQ, q, lane, wave);
+    for (int q = 0; q < NQ; ++q) mput<NQ, NS, NC>(acc[q], P, q, lane, wave);
 }
 
 // The same layer with v_mfma_f32_16x16x4_f32 (≥ 3 quads): lane l = 16g + n takes batch row n and
@@ -303,10 +321,11 @@ __device__ __forceinline__ void mlayer16(const float (&A)[kMSets][kMJ], const fl
 }
 
 
-// accumulator chains per (quad, set) for ≥ 8 in flight
+// accumulator chains per (quad, set): back-to-back accumulation into one chain costs nothing
+// extra from three independent chains up (tools/xcdm_layer_bench.hip)
 template <int NQ, int NS>
 struct MChains {
-    static constexpr int v = (8 + NQ * NS - 1) / (NQ * NS);
+    static constexpr int v = NQ * NS >= 3 ? 1 : 2;
 };
 
 // the layer in the kernel's MFMA form (optionally with a poll riding along)
@@ -449,6 +468,10 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
 
     // roles: (unit / fc row u, batch row n) for the layer epilogues; (logit j, row n) for fc3
     const bool gru = tid < 16 * NR;
+    // the off-critical recurrent sums (Σ W_hh·h of the next step; 16 partials each in the 4x4x1
+    // form) are taken by the waves that do not sample, while the samplers run J: waves ≥ aux_w0
+    // (none when every wave samples: then the epilogue threads take them in F and I)
+    const int aux_w0 = xcdm_big(NQ) ? kMWaves : kTwoLevel ? 1 : RX;
     const int gu = tid & 15, gn = tid >> 4;
     constexpr int kRingF4 = kMRing / 4;   // float4s of one row's terms
     // ring loader threads: all (≤ 4 rows per XCD: sampler waves store their loads after sampling,
@@ -552,7 +575,7 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
 #pragma unroll
             for (int q = 0; q < 3; ++q) {
                 const int i = q * 16 + gu;
-                gi[q] = sum8(pbig + (i * NR + gn) * kMWaves) + (fmaf(x, cst[MC_Q2 + i], tr[XT_P2 + gu * 3 + q]) + cst[MC_BIH2 + i]);
+                gi[q] = mpart<NQ>(pbig, i, gn) + (fmaf(x, cst[MC_Q2 + i], tr[XT_P2 + gu * 3 + q]) + cst[MC_BIH2 + i]);
                 gh[q] = gh2[i * NR + gn] + cst[MC_BHH2 + i];
             }
             h2v = gru_gate_math(gi[0], gi[1], gi[2], gh[0], gh[1], gh[2], h2v);
@@ -580,12 +603,14 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         MST(9);
         // ---- F: fc1 epilogue → f1; Σ W_hh1·h1 for the next GRU1
         if (gru) {
-            const float f = sum8(pfc1 + (gu * NR + gn) * kMWaves) + rg[gn * kMRing + XT_V1 + gu];
+            const float f = mpart<NQ>(pfc1, gu, gn) + rg[gn * kMRing + XT_V1 + gu];
             xpub(xg + kMHopOff[MH_F1] + gn * 512 + 16 * c + gu, tag, f > 0.0f ? f : 0.0f);
+            if (aux_w0 >= kMWaves) {
 #pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                const int i = q * 16 + gu;
-                gh1[i * NR + gn] = sum8(phh1 + (i * NR + gn) * kMWaves);
+                for (int q = 0; q < 3; ++q) {
+                    const int i = q * 16 + gu;
+                    gh1[i * NR + gn] = mpart<NQ>(phh1, i, gn);
+                }
             }
         }
         MST(10);
@@ -645,12 +670,14 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         };
         // ---- I: fc2 epilogue → f2 (LDS); Σ W_hh2·h2 for the next GRU2
         if (gru) {
-            const float f = sum8(pfc2 + (gu * NR + gn) * kMWaves) + rg[gn * kMRing + XT_V2 + gu];
+            const float f = mpart<NQ>(pfc2, gu, gn) + rg[gn * kMRing + XT_V2 + gu];
             f2s[gu * NR + gn] = f > 0.0f ? f : 0.0f;
+            if (aux_w0 >= kMWaves) {
 #pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                const int i = q * 16 + gu;
-                gh2[i * NR + gn] = sum8(pbig + (i * NR + gn) * kMWaves);
+                for (int q = 0; q < 3; ++q) {
+                    const int i = q * 16 + gu;
+                    gh2[i * NR + gn] = mpart<NQ>(pbig, i, gn);
+                }
             }
         }
         MST(16);
@@ -667,6 +694,14 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         }
         MST(18);
         if (kTwoLevel || wave >= RX) ring_store();
+        if (wave >= aux_w0) {
+            const int na = (kMWaves - aux_w0) * 64;
+            for (int e = tid - aux_w0 * 64; e < 3 * 16 * NR; e += na) {
+                const int i = e / NR, n = e - i * NR;
+                gh1[e] = mpart<NQ>(phh1, i, n);
+                gh2[e] = mpart<NQ>(pbig, i, n);
+            }
+        }
         MST(19);
         // ---- J: sample (:225-229)
         const float *nz = nz_at(t);
