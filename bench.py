@@ -33,7 +33,7 @@ from wavernn_amd import synthetic as syn  # noqa: E402
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak (dense)
 MOL_MACS_PER_ROW_STEP = 3825152   # loop MACs per row-step, MoL rnn 512
-PMC_PROFILE = os.environ.get("WRNN_PMC_PROFILE", os.path.join(REPO, "profiles", "r02_v6_pmc_traffic.json"))
+PMC_PROFILE = os.environ.get("WRNN_PMC_PROFILE", os.path.join(REPO, "profiles", "r03_v1_pmc_traffic.json"))
 SPARSE896_BYTES_PER_STEP = 5536598   # config 4 sparse values + int16 block indices, fp32
 DM_BYTES_PER_STEP = 12200196         # config 5 deepmind weights, fp32
 
@@ -120,6 +120,7 @@ def other_configs(dev) -> dict:
     res["config3_mol_fold_60s"] = {"samples_per_s": out.shape[0] / dt, "rtf": out.shape[0] / dt / d.sample_rate,
                                    "rows": 115, "loop_steps": 12100, "device_ms": ms, "wall_s": dt,
                                    "us_per_loop_step": ms * 1e3 / 12100,
+                                   "kernel_path": model.loop_handle().info["last_path"],
                                    "roofline": {"bound": "fp32 (vector/mfma)", "achieved": flops / (ms / 1e3) / 1e12,
                                                 "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                                                 "frac": flops / (ms / 1e3) / 1e12 / FP32_PEAK_TFLOPS,

@@ -54,8 +54,12 @@ def test_xcd_vs_reference_fixture(name, monkeypatch):
 @pytest.mark.parametrize("B", [1, 2, 8, 11, 17])
 def test_xcd_rows_vs_oracle(B, monkeypatch):
     """One row per XCD, up to 8 per launch: 11 and 17 rows take 2 and 3 launches (rows 8.., 16..
-    reuse the XCDs); every row against the oracle."""
-    monkeypatch.delenv("WRNN_PATH", raising=False)        # the default for B <= 48
+    reuse the XCDs; forced — above 8 rows the many-row kernel is the default); every row
+    against the oracle."""
+    if B <= 8:
+        monkeypatch.delenv("WRNN_PATH", raising=False)    # the default for B <= 8
+    else:
+        monkeypatch.setenv("WRNN_PATH", "xcd")
     d, state, mels, aux, noise, ref = _oracle_case(B, 300, 110 + B)
     loop = _loop(d)
     loop.set_weights(state)
@@ -117,16 +121,18 @@ def test_xcd_row_offset_sharding_invariance(monkeypatch):
     assert (full[2:] - part).abs().max().item() <= 2 * gf.MOL_TOL
 
 
-def test_large_batches_keep_the_rows_kernel(monkeypatch):
-    """Above 48 rows the multi-row kernel (rows through HBM) is the default."""
+@pytest.mark.parametrize("B,path", [(1, 5), (8, 5), (9, 7), (49, 7), (200, 7)])
+def test_default_path_by_rows(B, path, monkeypatch):
+    """Default MoL rnn-512 kernel by row count: one row per XCD (path 5) up to 8 rows, the
+    many-row XCD kernel (path 7) above, in launches of up to 128 rows."""
     monkeypatch.delenv("WRNN_PATH", raising=False)
     d = syn.DEFAULT_MOL
     state = syn.make_fatchord_state(d, 161)
-    mels, aux = syn.make_conditioning(49, 40, d.feat_dims, d.res_out_dims, 162)
+    mels, aux = syn.make_conditioning(B, 40, d.feat_dims, d.res_out_dims, 162)
     loop = _loop(d)
     loop.set_weights(state)
     loop.generate(_cond(mels, aux), seed=1)
-    assert loop.info["last_path"] == 2
+    assert loop.info["last_path"] == path
 
 
 def test_xcd_full_headline_length(monkeypatch):

@@ -13,7 +13,7 @@ if [ -z "$SKIP_TESTS" ]; then
 fi
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 600 rocprofv3 --pmc $c -d "$R/gpurun_out/pmc_$c" -o pmc --output-format csv -- \
-      python "$R/bench.py" --steps 1 --warmup 0 --cpu-steps 0 --other-configs 1 > gpurun_out/pmc_$c.log 2>&1
+      python "$R/bench.py" --steps 1 --warmup 0 --cpu-steps 0 --other-configs 1 --fold-batched 0 > gpurun_out/pmc_$c.log 2>&1
   rc=$?; echo "pmc $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
 python tools/pmc_summary.py gpurun_out gpurun_out/pmc_traffic.json > /dev/null

@@ -21,7 +21,7 @@ import sys
 HEADLINE = ("fatchord_xcd_kernel", "fatchord_split_kernel", "fatchord_loop_kernel")
 # loop kernel -> (config key in bench.py's other_configs, loop steps of its dispatches in one
 # bench.py --steps 1 --other-configs 1 run: warm-up + timed generate of that config)
-OTHER = {"fatchord_rows_kernel": ("config3_mol_fold_60s", 2 * 12100),
+OTHER = {"fatchord_xcdm_kernel": ("config3_mol_fold_60s", 2 * 12100),
          "fatchord_xcds_kernel": ("config4_sparse896_8utt", 100 + 110275),
          "deepmind_rows_kernel": ("config5_deepmind_32utt", 100 + 16000)}
 
