@@ -72,8 +72,10 @@ def test_dm_philox_row_keyed():
 
 def test_dm_row_groups_agree(monkeypatch):
     """One group of G workgroups vs two groups of G/2 (twice the units each): the coarse/fine
-    labels are bit-exact across partitions (Philox keyed by global row)."""
+    labels are bit-exact across partitions (Philox keyed by global row).  Multi-row kernel forced
+    (hidden 896 defaults to the XCD-resident kernel)."""
     from wavernn_amd.loop import DeepmindLoop
+    monkeypatch.setenv("WRNN_PATH", "rows")
     d = syn.DEFAULT_DM
     res = {}
     for g in ("1", "2"):
@@ -89,8 +91,10 @@ def test_dm_row_groups_agree(monkeypatch):
 @pytest.mark.parametrize("B", [3, 20, 40])
 def test_dm_granule_and_bulk_handoffs(B, monkeypatch):
     """Granule hand-offs (small row groups) and bulk flag + DMA hand-offs, both forced: the
-    combined labels are bit-exact between the two (Philox keyed by global row)."""
+    combined labels are bit-exact between the two (Philox keyed by global row).  Multi-row
+    kernel forced."""
     from wavernn_amd.loop import DeepmindLoop
+    monkeypatch.setenv("WRNN_PATH", "rows")
     d = syn.DEFAULT_DM
     res = {}
     for g in ("0", "1"):

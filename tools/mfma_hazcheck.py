@@ -1,10 +1,17 @@
-"""Static check of the inline-asm MFMAs in fatchord_xcdm.hip (hipcc does not pad hazards around
-inline asm): no VALU write to an MFMA source within 2 wait states before it, no non-MFMA read of
-an MFMA result within 8 (4x4x1) / 19 (16x16x4) wait states after it.  Input: the device asm,
-    hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -fno-slp-vectorize --cuda-device-only -S \
-        -o /tmp/xcdm.s wavernn_amd/csrc/fatchord_xcdm.hip"""
-import re,sys
-s=open('/tmp/xcdm.s').read()
+"""Static check of the inline-asm MFMAs in fatchord_xcdm.hip and deepmind_xcd.hip (hipcc does not
+pad hazards around inline asm): no VALU write to an MFMA source within 2 wait states before it,
+no non-MFMA read of an MFMA result within 8 (4x4x1) / 19 (16x16x4) wait states after it.
+Compiles the device asm of both files itself (hipcc, gfx950) into /tmp.
+
+    python tools/mfma_hazcheck.py"""
+import os
+import re
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNELS = [("fatchord_xcdm.hip", ["_ZN4wrnn20fatchord_xcdm_kernelILi%sELb0EEEvNS_8XcdmArgsE" % q for q in "1234"]),
+           ("deepmind_xcd.hip", ["_ZN4wrnn19deepmind_xcd_kernelILb0EEEvNS_6DxArgsE"])]
 def regs(tok):
     # expand v5 / v[4:7] / a3 / a[0:3]
     out=set()
@@ -12,8 +19,18 @@ def regs(tok):
         if m.group(1): out|={m.group(1)+str(i) for i in range(int(m.group(2)),int(m.group(3))+1)}
         else: out.add(m.group(4)+m.group(5))
     return out
-for nq in '1234':
-    a=s.index('_ZN4wrnn20fatchord_xcdm_kernelILi%sELb0EEEvNS_8XcdmArgsE: ;'%nq)
+def asm(src):
+    out = "/tmp/hazcheck_" + src.replace(".hip", ".s")
+    subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-I" + os.path.join(REPO, "include"),
+                    "-fno-slp-vectorize", "--cuda-device-only", "-S", "-o", out,
+                    os.path.join(REPO, "wavernn_amd", "csrc", src)], check=True, capture_output=True)
+    return open(out).read()
+total = 0
+for src, syms in KERNELS:
+  s = asm(src)
+  for sym in syms:
+    nq = sym
+    a=s.index(sym + ':')
     b=s.index('.Lfunc_end',a)
     ins=[l.strip() for l in s[a:b].split('\n')]
     ins=[l for l in ins if l and not l.startswith(';') and not l.startswith('.') and not l.endswith(':')]
@@ -31,7 +48,7 @@ for nq in '1234':
                 if p.startswith('v_') and not p.startswith('v_mfma'):
                     d=regs(p.split(None,1)[1].split(',')[0]) if ' ' in p else set()
                     if d & (srcab|srcc):
-                        print("NQ",nq,"VALU->MFMA hazard:",p,"|",l); bad+=1
+                        print(sym,"VALU->MFMA hazard:",p,"|",l); bad+=1
                 ws+=1; j-=1
             # look ahead: non-MFMA reading dst within 8 wait states
             ws=0; j=i+1
@@ -46,6 +63,8 @@ for nq in '1234':
                         ops2=parts[1].split(',')
                         srcs=set().union(*[regs(o) for o in ops2])
                     if srcs & dst:
-                        print("NQ",nq,"MFMA->read hazard:",l,"|",p,"ws",ws); bad+=1
+                        print(sym,"MFMA->read hazard:",l,"|",p,"ws",ws); bad+=1
                 ws+=1; j+=1
-    print("NQ",nq,"mfma",sum(1 for l in ins if l.startswith('v_mfma')),"hazards",bad)
+    print(src, sym, "mfma", sum(1 for l in ins if l.startswith('v_mfma')), "hazards", bad)
+    total += bad
+sys.exit(1 if total else 0)

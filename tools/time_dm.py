@@ -21,8 +21,8 @@ def main(rows):
         loop.generate(B, 100, seed=1)
         loop.generate(B, 4000, seed=2)
         ms = loop.elapsed_ms()
-        print(f"groups {os.environ.get('WRNN_ROW_GROUPS', 'auto')} B={B}: {ms * 1e3 / 4000:.2f} us/step, "
-              f"{B * 4000 / ms * 1e3 / 1e6:.3f} M samples/s", flush=True)
+        print(f"path {loop.info['last_path']} groups {os.environ.get('WRNN_ROW_GROUPS', 'auto')} B={B}: "
+              f"{ms * 1e3 / 4000:.2f} us/step, {B * 4000 / ms * 1e3 / 1e6:.3f} M samples/s", flush=True)
     loop.close()
 
 

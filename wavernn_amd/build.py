@@ -10,8 +10,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "_lib", "libwavernn_amd.so")
-SOURCES = [os.path.join(CSRC, f) for f in ("fatchord_loop.hip", "fatchord_split.hip", "fatchord_xcd.hip", "fatchord_xcds.hip", "fatchord_xcdm.hip", "fatchord_rows.hip", "deepmind_rows.hip", "condition.hip", "capi.cpp")]
-HEADERS = [os.path.join(CSRC, f) for f in ("fatchord_loop.h", "fatchord_split.h", "fatchord_xcd.h", "fatchord_xcds.h", "fatchord_xcdm.h", "xcd_device.h", "fatchord_rows.h", "deepmind_rows.h", "wrnn_device.h",
+SOURCES = [os.path.join(CSRC, f) for f in ("fatchord_loop.hip", "fatchord_split.hip", "fatchord_xcd.hip", "fatchord_xcds.hip", "fatchord_xcdm.hip", "fatchord_rows.hip", "deepmind_rows.hip", "deepmind_xcd.hip", "condition.hip", "capi.cpp")]
+HEADERS = [os.path.join(CSRC, f) for f in ("fatchord_loop.h", "fatchord_split.h", "fatchord_xcd.h", "fatchord_xcds.h", "fatchord_xcdm.h", "deepmind_xcd.h", "mfma_device.h", "xcd_device.h", "fatchord_rows.h", "deepmind_rows.h", "wrnn_device.h",
                                            "rows_device.h")] + \
     [os.path.join(REPO, "include", "wavernn_amd.h")]
 ARCH = os.environ.get("WRNN_OFFLOAD_ARCH", "gfx950")
@@ -35,7 +35,7 @@ def up_to_date() -> bool:
 # SLP vectorizer packs them into v_pk_fma_f32 with operand-shuffling moves and mid-loop LDS
 # waits (measured 4x slower jobs on gfx950)
 EXTRA_FLAGS = {"fatchord_rows.hip": ["-fno-slp-vectorize"], "fatchord_split.hip": ["-fno-slp-vectorize"],
-               "fatchord_xcd.hip": ["-fno-slp-vectorize"], "fatchord_xcds.hip": ["-fno-slp-vectorize"], "fatchord_xcdm.hip": ["-fno-slp-vectorize"], "deepmind_rows.hip": ["-fno-slp-vectorize"]}
+               "fatchord_xcd.hip": ["-fno-slp-vectorize"], "fatchord_xcds.hip": ["-fno-slp-vectorize"], "fatchord_xcdm.hip": ["-fno-slp-vectorize"], "deepmind_rows.hip": ["-fno-slp-vectorize"], "deepmind_xcd.hip": ["-fno-slp-vectorize"]}
 
 
 def build(force: bool = False, verbose: bool = True) -> str:

@@ -22,6 +22,7 @@
 #include "fatchord_xcd.h"
 #include "fatchord_xcds.h"
 #include "fatchord_xcdm.h"
+#include "deepmind_xcd.h"
 
 namespace wrnn {
 hipError_t launch_ci_gemm(const float *cond, int CD, int Bt, int b0, int Bc, int t0, int L, const float *W, int ldw,
@@ -53,7 +54,10 @@ hipError_t xcds_occupancy(int *blocks_per_cu);
 hipError_t launch_xcdm(const XcdmArgs &a, int nq, hipStream_t st);
 hipError_t prepare_xcdm_kernel(int max_lds_bytes);
 hipError_t xcdm_max_quads(int max_lds_bytes, int *nq_max);
-hipError_t launch_philox_fill(float *out, unsigned long long seed, long long row0, int nb, int t0, int Lc, hipStream_t st);
+hipError_t launch_philox_fill(float *out, unsigned long long seed, long long row0, int nb, int t0, int Lc, int K, int mol,
+                              hipStream_t st);
+hipError_t launch_dx(const DxArgs &a, hipStream_t st);
+hipError_t prepare_dx_kernel(int max_lds_bytes, bool *ok);
 }  // namespace wrnn
 
 using namespace wrnn;
@@ -148,6 +152,11 @@ struct wrnn_ctx {
     XcdmSlab xms{};
     float *d_xmslab = nullptr, *d_xmstate = nullptr, *d_xmnoise = nullptr;
     size_t xmnoise_cap = 0;
+    // XCD-resident deepmind kernel (hidden 896, quantisation 256, MFMA): deepmind_xcd.hip
+    bool dx_ok = false;
+    float *d_dxslab = nullptr, *d_dxstate = nullptr, *d_dxnoise = nullptr;
+    size_t dxnoise_cap = 0;
+    unsigned long long *d_dxxg = nullptr;
     unsigned long long *d_xmxg = nullptr;
 };
 
@@ -634,6 +643,77 @@ void pack_dm_slab(const wrnn_ctx &h, int w, float *out) {
         std::memcpy(out + s.o4 + (size_t)r * S, W("O4.weight") + (size_t)j * S, S * 4);
         out[s.o2b + r] = W("O2.bias")[j];
         out[s.o4b + r] = W("O4.bias")[j];
+    }
+}
+
+// ---- XCD-resident deepmind kernel (deepmind_xcd.h): the slab of workgroup c (the same on every
+// XCD, replicated 8×): A operands [wave][DxA][lane] and constants
+void pack_dx_slab(const wrnn_ctx &h, std::vector<float> &slab) {
+    const int H = kDxH, S = kDxS, U = kDxU;
+    const DxSlab L = dx_slab_layout();
+    slab.assign((size_t)kXcds * kXcdWgs * L.total, 0.0f);
+    auto W = [&](const char *n) { return h.w.at(n).data(); };
+    const float *R = W("R.weight"), *O1 = W("O1.weight"), *O3 = W("O3.weight"), *O2 = W("O2.weight"), *O4 = W("O4.weight");
+    std::vector<float> one((size_t)L.total);
+    for (int c = 0; c < kXcdWgs; ++c) {
+        std::fill(one.begin(), one.end(), 0.0f);
+        // WG-local R row rr = (half·3 + g)·14 + u → R row g·H + half·S + 14c + u
+        auto rrow = [&](int rr) {
+            const int half = rr / (3 * U), g = (rr / U) % 3, u = rr % U;
+            return R + (size_t)(g * H + half * S + U * c + u) * H;
+        };
+        for (int w = 0; w < kDxWaves; ++w)
+            for (int l = 0; l < 64; ++l) {
+                const int j = l & 3, b = l >> 2, g4 = b & 3, sp = b >> 2, g2 = b & 1, ks = b >> 1;
+                float *A = one.data() + L.a + (size_t)w * kDxA * 64 + l;
+                for (int s = 0; s < 5; ++s) {
+                    const float *row = rrow(16 * s + 4 * g4 + j);
+                    for (int m = 0; m < 56; ++m) {
+                        const int col = (m < 28 ? 0 : S) + kDxKW * w + 28 * sp + (m % 28);
+                        A[(DA_R + 56 * s + m) * 64] = row[col];
+                    }
+                }
+                {
+                    const float *row = rrow(80 + j);
+                    for (int m = 0; m < 14; ++m) A[(DA_RQ + m) * 64] = row[(m < 7 ? 0 : S) + kDxKW * w + 7 * b + (m % 7)];
+                }
+                const int r13 = 4 * g4 + j;
+                if (r13 < U)
+                    for (int m = 0; m < 28; ++m) {
+                        const int col = kDxKW * w + 28 * sp + m;
+                        A[(DA_O1 + m) * 64] = O1[(size_t)(U * c + r13) * S + col];
+                        A[(DA_O3 + m) * 64] = O3[(size_t)(U * c + r13) * S + col];
+                    }
+                const int r24 = 4 * g2 + j;
+                for (int m = 0; m < 14; ++m) {
+                    const int col = kDxKW * w + 14 * ks + m;
+                    A[(DA_O2 + m) * 64] = O2[(size_t)(kDxUO2 * c + r24) * S + col];
+                    A[(DA_O4 + m) * 64] = O4[(size_t)(kDxUO2 * c + r24) * S + col];
+                }
+            }
+        float *C = one.data() + L.cst;
+        for (int r = 0; r < U; ++r) {
+            C[DC_B1 + r] = W("O1.bias")[U * c + r];
+            C[DC_B3 + r] = W("O3.bias")[U * c + r];
+        }
+        for (int r = 0; r < kDxUO2; ++r) {
+            C[DC_B2 + r] = W("O2.bias")[kDxUO2 * c + r];
+            C[DC_B4 + r] = W("O4.bias")[kDxUO2 * c + r];
+        }
+        for (int g = 0; g < 3; ++g)
+            for (int u = 0; u < U; ++u) {
+                const int j = U * c + u;
+                for (int q = 0; q < 2; ++q) C[DC_IC + (g * U + u) * 2 + q] = W("I_coarse.weight")[(g * S + j) * 2 + q];
+                for (int q = 0; q < 3; ++q) C[DC_IF + (g * U + u) * 3 + q] = W("I_fine.weight")[(g * S + j) * 3 + q];
+            }
+        for (int half = 0; half < 2; ++half)
+            for (int u = 0; u < U; ++u) {
+                C[DC_BU + half * U + u] = W("bias_u")[half * S + U * c + u];
+                C[DC_BR + half * U + u] = W("bias_r")[half * S + U * c + u];
+                C[DC_BE + half * U + u] = W("bias_e")[half * S + U * c + u];
+            }
+        for (int k = 0; k < kXcds; ++k)
+            std::copy(one.begin(), one.end(), slab.begin() + (size_t)(k * kXcdWgs + c) * L.total);
     }
 }
 
@@ -1264,6 +1344,81 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
 }
 
 // deepmind_version: B rows (utterances) in row groups of <= kRowsMax, one launch each
+// deepmind rows through the XCD-resident kernel: up to kDxRowsMax rows per launch (launch row r
+// on XCD r % 8); Philox draws precomputed per time chunk (≤ WRNN_DM_NOISE_MB, default 64 MiB, so a
+// chunk's draws stay in the Infinity Cache); the recurrent state carried per workgroup in d_dxstate.
+int generate_dx(wrnn_t *h, int B, int L, const float *noise, uint64_t seed, int64_t row_offset, float *out,
+                int32_t *labels, hipStream_t st) {
+    const size_t xg_words = (size_t)kXcds * kDxXcdStride;
+    if (!h->d_members) HIP_TRY(h, hipMalloc(&h->d_members, kXcds * sizeof(int)));
+    if (!h->d_dxxg) HIP_TRY(h, hipMalloc(&h->d_dxxg, xg_words * 8));
+    if (!h->d_dxstate) HIP_TRY(h, hipMalloc(&h->d_dxstate, (size_t)kXcds * kXcdWgs * kDxStateW * sizeof(float)));
+    const char *mb_env = std::getenv("WRNN_DM_NOISE_MB");
+    const double budget = (mb_env ? std::atof(mb_env) : 64.0) * (1 << 20) / 4.0;   // floats
+    const char *dbg_env = std::getenv("WRNN_DEBUG_STAMPS");
+    const int dbg_steps = (dbg_env && std::atoi(dbg_env) > 0 && L >= kDxDbgSkip + kDxDbgSteps) ? kDxDbgSteps : 0;
+    const size_t dbg_n = (size_t)kXcds * kXcdWgs * kDxWaves * dbg_steps * kDxStamps;
+    unsigned *d_dbg = nullptr;
+    if (dbg_steps > 0) {
+        HIP_TRY(h, hipMalloc(&d_dbg, dbg_n * 4));
+        HIP_TRY(h, hipMemsetAsync(d_dbg, 0, dbg_n * 4, st));
+    }
+    for (int b0 = 0; b0 < B; b0 += kDxRowsMax) {
+        const int nb = std::min(kDxRowsMax, B - b0);
+        const int Lc_max = noise ? L : (int)std::max(1.0, std::min((double)L, budget / ((double)nb * 2 * kDxQ)));
+        if (!noise && grow(h, h->d_dxnoise, h->dxnoise_cap, (size_t)Lc_max * nb * 2 * kDxQ)) return WRNN_EHIP;
+        HIP_TRY(h, hipMemsetAsync(h->d_dxxg, 0, xg_words * 8, st));   // tags restart at 1
+        for (int t0 = 0; t0 < L; t0 += Lc_max) {
+            const int Lc = std::min(Lc_max, L - t0);
+            HIP_TRY(h, hipMemsetAsync(h->d_members, 0, kXcds * sizeof(int), st));
+            DxArgs a{};
+            a.slab = h->d_dxslab;
+            if (noise) {   // injected [L][B][2Q]
+                a.noise = noise;
+                a.nz_t0 = 0;
+                a.nz_ts = B;
+                a.nz_b0 = b0;
+            } else {       // Philox Exp(1) draws of this chunk ([Lc][nb][2Q]), keyed as every kernel keys them
+                HIP_TRY(h, launch_philox_fill(h->d_dxnoise, seed, row_offset + b0, nb, t0, Lc, 2 * kDxQ, 0, st));
+                a.noise = h->d_dxnoise;
+                a.nz_t0 = t0;
+                a.nz_ts = nb;
+                a.nz_b0 = 0;
+            }
+            a.out = out;
+            a.labels = labels;
+            a.state = h->d_dxstate;
+            a.xg = h->d_dxxg;
+            a.members = h->d_members;
+            a.ctl = h->d_ctl;
+            a.timeout_ticks = h->timeout_ticks;
+            a.L = L;
+            a.t0 = t0;
+            a.Lc = Lc;
+            a.Bt = B;
+            a.b0 = b0;
+            a.nb = nb;
+            a.s = dx_slab_layout();
+            a.dbg = (b0 == 0 && t0 == 0 && Lc >= kDxDbgSkip + kDxDbgSteps) ? d_dbg : nullptr;
+            HIP_TRY(h, launch_dx(a, st));
+        }
+    }
+    if (d_dbg) {
+        std::vector<unsigned> host(dbg_n);
+        HIP_TRY(h, hipStreamSynchronize(st));
+        HIP_TRY(h, hipMemcpy(host.data(), d_dbg, dbg_n * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(h, hipFree(d_dbg));
+        const char *path = std::getenv("WRNN_DEBUG_FILE");
+        if (FILE *f = std::fopen(path ? path : "wrnn_stamps.bin", "wb")) {
+            int hdr[3] = {kXcds * kXcdWgs * kDxWaves, dbg_steps, kDxStamps};
+            std::fwrite(hdr, sizeof(hdr), 1, f);
+            std::fwrite(host.data(), 4, host.size(), f);
+            std::fclose(f);
+        }
+    }
+    return WRNN_OK;
+}
+
 int generate_dm(wrnn_t *h, int B, int L, const float *noise, uint64_t seed, int64_t row_offset, float *out,
                 int32_t *labels, hipStream_t st) {
     // two row groups per launch (G/2 workgroups each) unless WRNN_ROW_GROUPS=1 or one row
@@ -1617,7 +1772,7 @@ int generate_xcdm(wrnn_t *h, const float *cond, int B, int L, const float *noise
                 a.nz_ts = B;
                 a.nz_b0 = b0;
             } else {       // Philox, drawn for this chunk by a small kernel first ([Lc][nb][11])
-                HIP_TRY(h, launch_philox_fill(h->d_xmnoise, seed, row_offset + b0, nb, t0, Lc, st));
+                HIP_TRY(h, launch_philox_fill(h->d_xmnoise, seed, row_offset + b0, nb, t0, Lc, 11, 1, st));
                 a.noise = h->d_xmnoise;
                 a.nz_t0 = t0;
                 a.nz_ts = nb;
@@ -1805,6 +1960,12 @@ int wrnn_create(const wrnn_config *cfg, int device, wrnn_t **out) {
             }
             h->dm2.ok = ok;
         }
+        // hidden 896 / quantisation 256 on a full 8 × 32-CU MI355X: the XCD-resident MFMA kernel
+        if (H == kDxH && Q == kDxQ && c.grid <= 0 && h->num_cus == kXcds * kXcdWgs) {
+            bool ok = false;
+            HIP_TRY(h, prepare_dx_kernel(h->max_lds, &ok));
+            h->dx_ok = ok;
+        }
         h->timeout_ticks = (long long)(c.timeout_ms > 0 ? c.timeout_ms : 2000) * 100000LL;
         HIP_TRY(h, hipMalloc(&h->d_ctl, kCtlWords * sizeof(int)));
         HIP_TRY(h, hipMemset(h->d_ctl, 0, kCtlWords * sizeof(int)));
@@ -1936,6 +2097,14 @@ int wrnn_set_weights(wrnn_t *h, const wrnn_tensor *tensors, int n) {
             h->d_dmslab = nullptr;
             HIP_TRY(h, hipMalloc(&h->d_dmslab, slab.size() * 4));
             HIP_TRY(h, hipMemcpy(h->d_dmslab, slab.data(), slab.size() * 4, hipMemcpyHostToDevice));
+        }
+        if (h->dx_ok) {
+            std::vector<float> slab;
+            pack_dx_slab(*h, slab);
+            if (h->d_dxslab) HIP_TRY(h, hipFree(h->d_dxslab));
+            h->d_dxslab = nullptr;
+            HIP_TRY(h, hipMalloc(&h->d_dxslab, slab.size() * 4));
+            HIP_TRY(h, hipMemcpy(h->d_dxslab, slab.data(), slab.size() * 4, hipMemcpyHostToDevice));
         }
         h->ready = true;
         return WRNN_OK;
@@ -2084,8 +2253,11 @@ int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise
     const bool split = !xcd && !xcds && h->split_ok && (pe == "split" || (pe.empty() && B == 1));
     HIP_TRY(h, hipMemsetAsync(h->d_ctl, 0, kCtlWords * sizeof(int), st));
     HIP_TRY(h, hipEventRecord(h->ev0, st));
-    h->last_path = h->dm ? 3 : xcdm ? 7 : xcd ? 5 : xcds ? 6 : split ? 4 : rows ? 2 : 1;
-    const int rc = h->dm    ? generate_dm(h, B, L, noise, seed, row_offset, out, labels, st)
+    // deepmind hidden 896 / quantisation 256: the XCD-resident kernel (WRNN_PATH=rows: the multi-row one)
+    const bool dx = h->dm && h->dx_ok && pe != "rows";
+    h->last_path = dx ? 8 : h->dm ? 3 : xcdm ? 7 : xcd ? 5 : xcds ? 6 : split ? 4 : rows ? 2 : 1;
+    const int rc = dx       ? generate_dx(h, B, L, noise, seed, row_offset, out, labels, st)
+                   : h->dm  ? generate_dm(h, B, L, noise, seed, row_offset, out, labels, st)
                    : xcdm  ? generate_xcdm(h, cond, B, L, noise, seed, row_offset, out, st)
                    : xcd   ? generate_xcd(h, cond, B, L, noise, seed, row_offset, out, st)
                    : xcds  ? generate_xcds(h, cond, B, L, noise, seed, row_offset, out, st)
@@ -2113,7 +2285,8 @@ int wrnn_check(wrnn_t *h, void *stream) {
         static const char *split_hops[] = {"y", "f1", "f2", "h2", "h2", "gru1-terms", "gru1-terms"};
         static const char *xcd_hops[] = {"y", "f1", "f2", "h2", "gru1-terms", "gru1-terms"};
         static const char *xcdm_hops[] = {"h1", "y", "h2", "f1", "f2 (partial logits)", "x"};
-        const char *name = h->last_path == 7   ? (hop >= 0 && hop < 6 ? xcdm_hops[hop] : "?")
+        const char *name = h->last_path == 8   ? (hop >= 0 && hop < 6 ? dm_hops[hop] : "?")
+                           : h->last_path == 7 ? (hop >= 0 && hop < 6 ? xcdm_hops[hop] : "?")
                            : h->last_path >= 5 ? (hop >= 0 && hop < 6 ? xcd_hops[hop] : "?")
                            : h->last_path == 4 ? (hop >= 0 && hop < 7 ? split_hops[hop] : "?")
                            : h->last_path == 3 ? (hop >= 0 && hop < 8 ? dm_hops[hop] : "?")
@@ -2149,6 +2322,7 @@ int wrnn_query(const wrnn_t *h, wrnn_info *info) {
         info->rows_grid = h->G;
         info->rows_units_rnn = h->dmU;
         info->last_path = h->last_path;
+        info->xcd_rows = h->dx_ok ? kDxRowsMax : 0;
         return WRNN_OK;
     }
     const bool rows_only = h->max_rows < 1;      // e.g. rnn 896 with block-sparse GRU weights
@@ -2183,7 +2357,8 @@ void wrnn_destroy(wrnn_t *h) {
                     (void *)h->d_dmflags, (void *)h->d_dmxg, (void *)h->d_sgslab, (void *)h->d_sfslab,
                     (void *)h->d_sWt, (void *)h->g2.d_slab, (void *)h->g2.d_Wt, (void *)h->dm2.d_slab,
                     (void *)h->d_gact, (void *)h->d_xslab, (void *)h->d_xWt, (void *)h->d_xstate, (void *)h->d_xgx,
-                    (void *)h->d_members, (void *)h->d_xmslab, (void *)h->d_xmstate, (void *)h->d_xmxg, (void *)h->d_xmnoise})
+                    (void *)h->d_members, (void *)h->d_xmslab, (void *)h->d_xmstate, (void *)h->d_xmxg, (void *)h->d_xmnoise,
+                    (void *)h->d_dxslab, (void *)h->d_dxstate, (void *)h->d_dxnoise, (void *)h->d_dxxg})
         if (p) (void)hipFree(p);
     if (h->blas) (void)rocblas_destroy_handle(h->blas);
     delete h;

@@ -1,0 +1,595 @@
+// deepmind_xcd.hip — XCD-resident persistent kernel for the dual coarse/fine softmax WaveRNN
+// (models/deepmind_version.py:75-165, hidden 896, quantisation 256): up to 4 rows per XCD, 32 per
+// launch (BASELINE config 5: 32 utterances per GPU = one launch).
+//
+// The loop's 12.2 MB of fp32 weights are held once per XCD as MFMA A operands in the 32 CUs'
+// registers and LDS (deepmind_xcd.h, DxA: 378 per lane and wave: 252 in AGPRs, 84 in VGPRs, 42
+// in LDS); the 4 rows of an
+// XCD are the batch columns of v_mfma_f32_4x4x1_16b_f32.  Every hand-off is an XCD-local granule
+// vector ({tag = step + 1, value}, plain stores, 16-byte sc1 polls) as in fatchord_xcd.hip.
+//
+// Per step t (prev = the labels of step t − 1 of every row):
+//   coarse gates of the own 14 units × 4 rows (R·h_{t-1} from the LDS partials, I_coarse(prev))
+//                                                                       → publish h_c    [hop Hc]
+//   h_c slice → O1 (1 set)  → barrier → relu(+b)                        → publish o1     [hop O1]
+//   R[:, :S]·h_c — the coarse half of the next step's R·h (5 sets + a quarter set, accumulators
+//   kept in registers), the o1 poll riding along
+//   o1 slice → O2 (8 rows) → barrier → +b                               → publish logits [hop Lc]
+//   sample c_t: wave n polls row n's 256 logits and samples it (softmax → Categorical ≡
+//   argmax(p / q), q ~ Exp(1)) in every workgroup — no label hop
+//   fine gates (R·h_{t-1}, I_fine(prev, c_t))                            → publish h_f    [hop Hf]
+//   h_f slice → O3 → barrier → relu(+b)                                  → publish o3     [hop O3]
+//   R[:, S:]·h_f (finishes R·h_t; partials → LDS for step t + 1), the o3 poll riding along
+//   o3 slice → O4 → barrier → +b                                         → publish logits [hop Lf]
+//   sample f_t; workgroup 0 of the XCD writes combine_signal(c_t, f_t) (utils/dsp.py:33)
+// The draws of step t + 1 (Exp(1): injected, or Philox precomputed by philox_fill_kernel) are
+// loaded into registers after the h_c poll and stored into an LDS ring after f_t.
+//
+// Membership as in fatchord_xcd.hip (XCC id + per-XCD arrival counter; bounded waits).  fp32,
+// sums re-associated; the sampled labels are checked bit-exact against the oracle.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "deepmind_xcd.h"
+#include "mfma_device.h"
+#include "wrnn_device.h"
+#include "xcd_device.h"
+
+namespace wrnn {
+
+namespace {
+
+__device__ __forceinline__ f2v lds2(const float *p) { return *reinterpret_cast<const f2v *>(p); }
+
+// wave w's slice of a 448-wide hop vector, 4 rows: 224 granule pairs, pair p = min(lane + 64i,
+// 223) (i < 4; lanes 32..63 of i = 3 repeat pairs 192..223): row p / 56, columns
+// 112w + 2(p % 56) + {0, 1}
+__device__ __forceinline__ int dx_pair(int lane, int i) {
+    const int p = lane + 64 * i;
+    return p < 224 ? p : p - 32;
+}
+__device__ __forceinline__ int dx_poll_off(int w, int p) {   // bytes
+    const int n = p / 56, cp = p - 56 * n;
+    return (n * kDxS + kDxKW * w + 2 * cp) * 8;
+}
+
+// bounded poll of the wave's slice into v (all granules tagged `tag` on return, or *lds_abort)
+__device__ __forceinline__ void dx_poll(__amdgpu_buffer_rsrc_t r, int w, uint32_t tag, int *ctl, long long timeout,
+                                        int step, int hop, int *lds_abort, int lane, u4v (&v)[4]) {
+    const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
+    unsigned spins = 0;
+    for (;;) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = ld16_sc1(r, dx_poll_off(w, dx_pair(lane, i)));
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ok &= (v[i].y == tag) & (v[i].w == tag);
+        if (__ballot(!ok) == 0) return;
+        if ((++spins & 63u) == 0) {
+            const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - c0) > timeout;
+            const bool other = __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+            if (late || other) {
+                if (late) record_abort(ctl, -4, step, hop, blockIdx.x);
+                *lds_abort = 1;
+                return;
+            }
+        }
+    }
+}
+
+// polled pairs → the wave's staging rows [n][kDxST]
+__device__ __forceinline__ void dx_stage(float *stg, int lane, const u4v (&v)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int p = dx_pair(lane, i), n = p / 56, cp = p - 56 * n;
+        *reinterpret_cast<f2v *>(stg + n * kDxST + 2 * cp) = f2v{__uint_as_float(v[i].x), __uint_as_float(v[i].z)};
+    }
+}
+
+// A poll that rides along an MFMA layer: loads issued at chunk kAt, checked after the layer
+// (fallback: the bounded blocking poll), as MPoll in fatchord_xcdm.hip
+template <int kAt>
+struct DxRide {
+    u4v v[4];
+    __amdgpu_buffer_rsrc_t r;
+    int w, lane;
+    uint32_t tag;
+    __device__ __forceinline__ DxRide(const unsigned long long *vec, int w_, uint32_t tag_, int lane_)
+        : r(hop_rsrc(vec)), w(w_), lane(lane_), tag(tag_) {}
+    __device__ __forceinline__ void step(int c) {
+        if (c == kAt) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = ld16_sc1(r, dx_poll_off(w, dx_pair(lane, i)));
+        }
+    }
+    __device__ __forceinline__ void finish(int *ctl, long long timeout, int step_, int hop, int *lds_abort) {
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ok &= (v[i].y == tag) & (v[i].w == tag);
+        if (__ballot(!ok) != 0) dx_poll(r, w, tag, ctl, timeout, step_, hop, lds_abort, lane, v);
+    }
+};
+
+// O1 / O3: one 16-row set (4 row groups × 4 k-slices) over the wave's 112 columns, 28 MFMAs in
+// 4 accumulator chains; partials → P[wave][row 16][n (+1 pad)][k-slice 4] (row stride 20)
+template <bool kAgpr>
+__device__ __forceinline__ void dx_o13(const float (&A)[28], const float *stg, float *P, int lane, int wave) {
+    const int j = lane & 3, g = (lane >> 2) & 3, sp = lane >> 4;
+    const float *bp = stg + j * kDxST + 28 * sp;
+    f4v acc[4], b[2];
+    b[0] = lds4(bp);
+#pragma unroll
+    for (int c = 0; c < 7; ++c) {
+        if (c + 1 < 7) b[(c + 1) & 1] = lds4(bp + 4 * (c + 1));
+#pragma unroll
+        for (int mm = 0; mm < 4; ++mm) {
+            const int m = 4 * c + mm;
+            if (m < 4) mfma_first<kAgpr>(acc[m & 3], A[m], b[c & 1][mm]);
+            else mfma_acc<kAgpr>(acc[m & 3], A[m], b[c & 1][mm]);
+        }
+    }
+    mfma_drain_begin();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) mfma_tie(acc[q]);
+    const f4v d = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    float *p = P + (wave * 16 + 4 * g) * 20 + 4 * j + sp;
+    p[0] = d.x;
+    p[20] = d.y;
+    p[40] = d.z;
+    p[60] = d.w;
+}
+
+// O2 / O4: 8 rows (2 row groups × 8 k-slices of 14 columns), 14 MFMAs in 4 chains; partials →
+// P[wave][row 8][n 4][k-slice 8]
+// (A operands from LDS: Al = the wave's [14][64] image)
+__device__ __forceinline__ void dx_o24(const float *Al, const float *stg, float *P, int lane, int wave) {
+    const int j = lane & 3, b = lane >> 2, g = b & 1, ks = b >> 1;
+    const float *bp = stg + j * kDxST + 14 * ks;
+    f4v acc[4];
+    f2v x[7];
+    float A[14];
+#pragma unroll
+    for (int m = 0; m < 14; ++m) A[m] = Al[m * 64 + lane];
+#pragma unroll
+    for (int c = 0; c < 7; ++c) x[c] = lds2(bp + 2 * c);
+#pragma unroll
+    for (int m = 0; m < 14; ++m) {
+        if (m < 4) mfma_first<false>(acc[m & 3], A[m], x[m >> 1][m & 1]);
+        else mfma_acc<false>(acc[m & 3], A[m], x[m >> 1][m & 1]);
+    }
+    mfma_drain_begin();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) mfma_tie(acc[q]);
+    const f4v d = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    float *p = P + ((wave * 8 + 4 * g) * 4 + j) * 8 + ks;
+    p[0] = d.x;
+    p[32] = d.y;
+    p[64] = d.z;
+    p[96] = d.w;
+}
+
+// One half (kHalf 0: coarse columns from h_c, 1: fine columns from h_f) of R·h over the wave's
+// 112 columns: 5 sets (sets 0..3 AGPR, set 4 VGPR) × 28 MFMAs + the quarter set's 7 (A from
+// LDS), one chain per set continued across the halves; hook.step(c) at each of the 7 chunks
+template <int kHalf, typename Hook>
+__device__ __forceinline__ void dx_rhalf(const float (&AR)[5][56], const float *ARQl, const float *stg,
+                                         f4v (&accR)[5], f4v &accQ, int lane, Hook &hook) {
+    const int j = lane & 3, sp = lane >> 4, b = lane >> 2;
+    const float *bp = stg + j * kDxST + 28 * sp;
+    const float *bq = stg + j * kDxST + 7 * b;
+    f4v bb[2];
+    bb[0] = lds4(bp);
+#pragma unroll
+    for (int c = 0; c < 7; ++c) {
+        hook.step(c);
+        if (c + 1 < 7) bb[(c + 1) & 1] = lds4(bp + 4 * (c + 1));
+        const float qv = bq[c], qa = ARQl[(7 * kHalf + c) * 64 + lane];
+#pragma unroll
+        for (int mm = 0; mm < 4; ++mm) {
+            const int m = 4 * c + mm;
+#pragma unroll
+            for (int s = 0; s < 5; ++s) {
+                const float a = AR[s][28 * kHalf + m], x = bb[c & 1][mm];
+                if (kHalf == 0 && m == 0) {
+                    if (s < 4) mfma_first<true>(accR[s], a, x);
+                    else mfma_first<false>(accR[s], a, x);
+                } else {
+                    if (s < 4) mfma_acc<true>(accR[s], a, x);
+                    else mfma_acc<false>(accR[s], a, x);
+                }
+            }
+        }
+        if (kHalf == 0 && c == 0) mfma_first<false>(accQ, qa, qv);
+        else mfma_acc<false>(accQ, qa, qv);
+    }
+}
+
+// R·h partials → LDS: sets [set][wave][row 16][n (+1)][k-slice 4], quarter [wave][row 4][n][16]
+__device__ __forceinline__ void dx_rput(f4v (&accR)[5], f4v &accQ, float *PR, float *PRQ, int lane, int wave) {
+    mfma_drain_begin();
+#pragma unroll
+    for (int s = 0; s < 5; ++s) mfma_tie(accR[s]);
+    mfma_tie(accQ);
+    const int j = lane & 3, g = (lane >> 2) & 3, sp = lane >> 4, b = lane >> 2;
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+        float *p = PR + ((s * kDxWaves + wave) * 16 + 4 * g) * 20 + 4 * j + sp;
+        p[0] = accR[s].x;
+        p[20] = accR[s].y;
+        p[40] = accR[s].z;
+        p[60] = accR[s].w;
+    }
+    float *q = PRQ + (wave * 16 + j) * 16 + b;   // [wave][row i][n j][slice b]: row stride 64
+    q[0] = accQ.x;
+    q[64] = accQ.y;
+    q[128] = accQ.z;
+    q[192] = accQ.w;
+}
+
+// Σ over waves and k-slices of WG-local R row rr (0..83), batch row n — fixed order
+__device__ __forceinline__ float dx_rsum(const float *PR, const float *PRQ, int rr, int n) {
+    float t[kDxWaves];
+    if (rr < 80) {
+        const int s = rr >> 4, r = rr & 15;
+#pragma unroll
+        for (int w = 0; w < kDxWaves; ++w) {
+            const f4v u = lds4(PR + ((s * kDxWaves + w) * 16 + r) * 20 + 4 * n);
+            t[w] = (u.x + u.y) + (u.z + u.w);
+        }
+    } else {
+        const int i = rr - 80;
+#pragma unroll
+        for (int w = 0; w < kDxWaves; ++w) {
+            const float *p = PRQ + ((w * 4 + i) * 4 + n) * 16;
+            const f4v u0 = lds4(p), u1 = lds4(p + 4), u2 = lds4(p + 8), u3 = lds4(p + 12);
+            t[w] = (((u0.x + u0.y) + (u0.z + u0.w)) + ((u1.x + u1.y) + (u1.z + u1.w))) +
+                   (((u2.x + u2.y) + (u2.z + u2.w)) + ((u3.x + u3.y) + (u3.z + u3.w)));
+        }
+    }
+    return (t[0] + t[1]) + (t[2] + t[3]);
+}
+
+// Σ of an O1 / O3 output (row r < 16, n) and of an O2 / O4 output (row r < 8, n)
+__device__ __forceinline__ float dx_o13sum(const float *P, int r, int n) {
+    float t[kDxWaves];
+#pragma unroll
+    for (int w = 0; w < kDxWaves; ++w) {
+        const f4v u = lds4(P + (w * 16 + r) * 20 + 4 * n);
+        t[w] = (u.x + u.y) + (u.z + u.w);
+    }
+    return (t[0] + t[1]) + (t[2] + t[3]);
+}
+__device__ __forceinline__ float dx_o24sum(const float *P, int r, int n) {
+    float t[kDxWaves];
+#pragma unroll
+    for (int w = 0; w < kDxWaves; ++w) {
+        const float *p = P + ((w * 8 + r) * 4 + n) * 8;
+        const f4v u0 = lds4(p), u1 = lds4(p + 4);
+        t[w] = ((u0.x + u0.y) + (u0.z + u0.w)) + ((u1.x + u1.y) + (u1.z + u1.w));
+    }
+    return (t[0] + t[1]) + (t[2] + t[3]);
+}
+
+}  // namespace
+
+#define DST(kk)                                                                                              \
+    do {                                                                                                     \
+        if (kDbg && lane == 0 && (unsigned)(t - a.t0 - kDxDbgSkip) < (unsigned)kDxDbgSteps)                 \
+            dbgs[((t - a.t0 - kDxDbgSkip) * kDxWaves + wave) * kDxStamps + (kk)] =                           \
+                (unsigned)__builtin_amdgcn_s_memtime();                                                      \
+    } while (0)
+
+template <bool kDbg>
+__global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const DxLds ll = dx_lds_layout(kDbg);
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    float *pr = smem + ll.pr, *prq = smem + ll.prq, *po1 = smem + ll.po1, *po3 = smem + ll.po3;
+    float *po2 = smem + ll.po2, *po4 = smem + ll.po4, *lg = smem + ll.lg, *nzr = smem + ll.nz;
+    float *cst = smem + ll.cst, *lab = smem + ll.lab;
+    int *misc = reinterpret_cast<int *>(smem + ll.misc);
+    int *abort_flag = misc;
+    unsigned *dbgs = reinterpret_cast<unsigned *>(smem + ll.dbg);
+    auto stg_of = [&](int vec) { return smem + ll.stg + (vec * kDxWaves + wave) * 4 * kDxST; };
+    float *aol = smem + ll.ao + wave * kDxAL * 64;   // this wave's LDS A operands
+    const float *arq = aol, *ao2 = aol + 14 * 64, *ao4 = aol + 28 * 64;
+
+    // ---- membership: XCD k (launch rows k, k + 8, k + 16, k + 24) and index c within it
+    if (tid == 0) {
+        const int kx = (int)xcc_id();
+        int cc = kXcdWgs;
+        if (kx < a.nb) cc = atomicAdd(&a.members[kx], 1);
+        misc[1] = (kx < a.nb && cc < kXcdWgs) ? kx * kXcdWgs + cc : -1;
+        misc[0] = 0;
+    }
+    __syncthreads();
+    const int mem = __builtin_amdgcn_readfirstlane(misc[1]);   // wave-uniform: hop addresses in SGPRs
+    if (mem < 0) return;
+    const int k = mem / kXcdWgs, c = mem - k * kXcdWgs;
+    const int RX = min(kDxRowsXcd, (a.nb - k + kXcds - 1) / kXcds);   // rows n < RX: launch row k + 8n
+    unsigned long long *xg = a.xg + (size_t)k * kDxXcdStride;
+    const float *S = a.slab + (size_t)(k * kXcdWgs + c) * a.s.total;
+
+    // ---- register-resident A operands
+    float AR[5][56], AO1[28], AO3[28];
+    {
+        const float *Aw = S + a.s.a + (size_t)wave * kDxA * 64 + lane;
+#pragma unroll
+        for (int s = 0; s < 5; ++s)
+#pragma unroll
+            for (int m = 0; m < 56; ++m) AR[s][m] = Aw[(DA_R + 56 * s + m) * 64];
+#pragma unroll
+        for (int m = 0; m < 28; ++m) {
+            AO1[m] = Aw[(DA_O1 + m) * 64];
+            AO3[m] = Aw[(DA_O3 + m) * 64];
+        }
+        // the quarter set and O2 / O4 → LDS
+        for (int m = 0; m < kDxAL; ++m) aol[m * 64 + lane] = Aw[(DA_RQ + m) * 64];
+    }
+
+    // roles: gate threads (unit u, row n), 56 of them; O1/O3 epilogue (row r < 14, n); O2/O4 (r < 8, n)
+    const bool gate = tid < 4 * kDxU;
+    const int gu = tid % kDxU, gn = tid / kDxU;
+    const int t_end = a.t0 + a.Lc;
+    float *st = a.state + (size_t)(k * kXcdWgs + c) * kDxStateW;
+    auto noise_src = [&](int t, int n) {
+        return a.noise + ((size_t)(t - a.nz_t0) * a.nz_ts + a.nz_b0 + k + kXcds * n) * (2 * kDxQ);
+    };
+
+    // ---- prologue: constants, carried state, draws of step t0
+    for (int i = tid; i < kDxCst; i += kDxThreads) cst[i] = S[a.s.cst + i];
+    const bool resume = a.t0 > 0;
+    for (int i = tid; i < kDxPR; i += kDxThreads) pr[i] = resume ? st[8 * kDxU + i] : 0.0f;
+    for (int i = tid; i < kDxPRQ; i += kDxThreads) prq[i] = resume ? st[8 * kDxU + kDxPR + i] : 0.0f;
+    if (tid < 16) lab[tid] = (resume && tid < 8) ? st[8 * kDxU + kDxPR + kDxPRQ + tid] : 0.0f;   // out_coarse = out_fine = 0 (:89-90)
+    float hc = 0.0f, hf = 0.0f;   // h of (unit gu, row gn): this thread's recurrent state
+    if (gate && resume) {
+        hc = st[gn * 2 * kDxU + gu];
+        hf = st[gn * 2 * kDxU + kDxU + gu];
+    }
+    for (int i = tid; i < RX * 2 * kDxQ / 4; i += kDxThreads) {
+        const int n = i / (2 * kDxQ / 4), f = i - n * (2 * kDxQ / 4);
+        *reinterpret_cast<f4v *>(nzr + ((a.t0 & 1) * 4 + n) * 2 * kDxQ + 4 * f) =
+            *reinterpret_cast<const f4v *>(noise_src(a.t0, n) + 4 * f);
+    }
+    __syncthreads();
+
+    constexpr int kNzF4 = 2 * kDxQ / 4;                         // float4s of one row's draws
+    constexpr int kNzLd = (kDxRowsXcd * kNzF4 + kDxThreads - 1) / kDxThreads;   // per thread
+
+    for (int t = a.t0; t < t_end; ++t) {
+        int tid = threadIdx.x;   // opaque per step (see fatchord_xcdm.hip)
+        asm volatile("" : "+v"(tid));
+        const int lane = tid & 63, gu = tid % kDxU, gn = tid / kDxU;
+        const uint32_t tag = (uint32_t)t + 1u;
+        const bool more = t + 1 < t_end;
+        DST(0);
+        // ---- coarse gates (:106-125): R·h_{t-1} (partials of the previous step), I_coarse(prev)
+        if (gate) {
+            const float x0 = lab[gn] / 127.5f - 1.0f, x1 = lab[4 + gn] / 127.5f - 1.0f;
+            float I[3], Rg[3];
+#pragma unroll
+            for (int g = 0; g < 3; ++g) {   // separately rounded products (:111)
+                const float *wi = cst + DC_IC + (g * kDxU + gu) * 2;
+                I[g] = __fadd_rn(__fmul_rn(wi[0], x0), __fmul_rn(wi[1], x1));
+                Rg[g] = dx_rsum(pr, prq, g * kDxU + gu, gn);
+            }
+            const float uu = sigmoid_((Rg[0] + I[0]) + cst[DC_BU + gu]);
+            const float rr = sigmoid_((Rg[1] + I[1]) + cst[DC_BR + gu]);
+            const float ee = tanh_((rr * Rg[2] + I[2]) + cst[DC_BE + gu]);
+            hc = uu * hc + (1.0f - uu) * ee;
+            xpub(xg + kDxHopOff[DX_HC] + gn * kDxS + kDxU * c + gu, tag, hc);
+        }
+        DST(1);
+        // ---- h_c slice → O1 → relu → o1
+        {
+            u4v v[4];
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            dx_poll(hop_rsrc(xg + kDxHopOff[DX_HC]), wave, tag, a.ctl, a.timeout_ticks, t, DX_HC, abort_flag, lane, v);
+            dx_stage(stg_of(0), lane, v);
+        }
+        // the draws of step t + 1 → registers (stored into the ring after f_t); issued here, the
+        // first wait that covers them is the o1 poll's, one R half later
+        f4v nzl[kNzLd];
+        if (more) {
+#pragma unroll
+            for (int i = 0; i < kNzLd; ++i) {
+                const int idx = tid + kDxThreads * i;
+                if (idx < RX * kNzF4) {
+                    const int n = idx / kNzF4, f = idx - n * kNzF4;
+                    nzl[i] = *reinterpret_cast<const f4v *>(noise_src(t + 1, n) + 4 * f);
+                }
+            }
+        }
+        DST(2);
+        dx_o13<true>(AO1, stg_of(0), po1, lane, wave);
+        bar();
+        DST(3);
+        if (tid < 4 * kDxU) {
+            const int r = tid % kDxU, n = tid / kDxU;
+            const float o = dx_o13sum(po1, r, n) + cst[DC_B1 + r];
+            xpub(xg + kDxHopOff[DX_O1] + n * kDxS + kDxU * c + r, tag, o > 0.0f ? o : 0.0f);
+        }
+        DST(4);
+        // ---- R[:, :S]·h_c (next step's R·h, coarse half) with the o1 poll riding along
+        f4v accR[5], accQ;
+        {
+            DxRide<4> po(xg + kDxHopOff[DX_O1], wave, tag, lane);
+            dx_rhalf<0>(AR, arq, stg_of(0), accR, accQ, lane, po);
+            DST(5);
+            po.finish(a.ctl, a.timeout_ticks, t, DX_O1, abort_flag);
+            dx_stage(stg_of(1), lane, po.v);
+        }
+        DST(6);
+        // ---- o1 slice → O2 → coarse logits
+        dx_o24(ao2, stg_of(1), po2, lane, wave);
+        bar();
+        DST(7);
+        if (tid < 4 * kDxUO2) {
+            const int r = tid % kDxUO2, n = tid / kDxUO2;
+            xpub(xg + kDxHopOff[DX_LC] + n * kDxQ + kDxUO2 * c + r, tag, dx_o24sum(po2, r, n) + cst[DC_B2 + r]);
+        }
+        DST(8);
+        // ---- sample c_t (:129-131): wave n samples row n
+        auto sample_row = [&](int hop, int half) -> int {
+            const __amdgpu_buffer_rsrc_t rl = hop_rsrc(xg + kDxHopOff[hop]);
+            float *l = lg + wave * kDxQ;
+            const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
+            unsigned spins = 0;
+            for (;;) {
+                const u4v v0 = ld16_sc1(rl, (wave * kDxQ + 2 * lane) * 8);
+                const u4v v1 = ld16_sc1(rl, (wave * kDxQ + 2 * lane + 128) * 8);
+                const bool ok = (v0.y == tag) & (v0.w == tag) & (v1.y == tag) & (v1.w == tag);
+                if (__ballot(!ok) == 0) {
+                    *reinterpret_cast<f2v *>(l + 2 * lane) = f2v{__uint_as_float(v0.x), __uint_as_float(v0.z)};
+                    *reinterpret_cast<f2v *>(l + 2 * lane + 128) = f2v{__uint_as_float(v1.x), __uint_as_float(v1.z)};
+                    break;
+                }
+                if ((++spins & 63u) == 0) {
+                    const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - c0) > a.timeout_ticks;
+                    const bool other = __hip_atomic_load(&a.ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+                    if (late || other) {
+                        if (late) record_abort(a.ctl, -4, t, hop, blockIdx.x);
+                        *abort_flag = 1;
+                        return 0;
+                    }
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const float *q = nzr + ((t & 1) * 4 + wave) * 2 * kDxQ + half * kDxQ;
+            return raw_sample<4>(l, q, kDxQ, lane);
+        };
+        if (wave < RX) {
+            const int cl = sample_row(DX_LC, 0);
+            if (lane == 0) lab[8 + wave] = (float)cl;
+        }
+        bar();
+        DST(9);
+        // ---- fine gates (:135-145): I_fine(prev, c_t)
+        if (gate) {
+            const float x0 = lab[gn] / 127.5f - 1.0f, x1 = lab[4 + gn] / 127.5f - 1.0f;
+            const float x2 = lab[8 + gn] / 127.5f - 1.0f;
+            float I[3], Rg[3];
+#pragma unroll
+            for (int g = 0; g < 3; ++g) {   // (:137)
+                const float *wi = cst + DC_IF + (g * kDxU + gu) * 3;
+                I[g] = __fadd_rn(__fadd_rn(__fmul_rn(wi[0], x0), __fmul_rn(wi[1], x1)), __fmul_rn(wi[2], x2));
+                Rg[g] = dx_rsum(pr, prq, (3 + g) * kDxU + gu, gn);
+            }
+            const float uu = sigmoid_((Rg[0] + I[0]) + cst[DC_BU + kDxU + gu]);
+            const float rr = sigmoid_((Rg[1] + I[1]) + cst[DC_BR + kDxU + gu]);
+            const float ee = tanh_((rr * Rg[2] + I[2]) + cst[DC_BE + kDxU + gu]);
+            hf = uu * hf + (1.0f - uu) * ee;
+            xpub(xg + kDxHopOff[DX_HF] + gn * kDxS + kDxU * c + gu, tag, hf);
+        }
+        DST(10);
+        // ---- h_f slice → O3 → relu → o3
+        {
+            u4v v[4];
+            dx_poll(hop_rsrc(xg + kDxHopOff[DX_HF]), wave, tag, a.ctl, a.timeout_ticks, t, DX_HF, abort_flag, lane, v);
+            dx_stage(stg_of(0), lane, v);
+        }
+        DST(11);
+        dx_o13<false>(AO3, stg_of(0), po3, lane, wave);
+        bar();
+        DST(12);
+        if (tid < 4 * kDxU) {
+            const int r = tid % kDxU, n = tid / kDxU;
+            const float o = dx_o13sum(po3, r, n) + cst[DC_B3 + r];
+            xpub(xg + kDxHopOff[DX_O3] + n * kDxS + kDxU * c + r, tag, o > 0.0f ? o : 0.0f);
+        }
+        DST(13);
+        // ---- R[:, S:]·h_f finishes R·h_t (the gates above have read R·h_{t-1}) → LDS partials
+        {
+            DxRide<4> po(xg + kDxHopOff[DX_O3], wave, tag, lane);
+            dx_rhalf<1>(AR, arq, stg_of(0), accR, accQ, lane, po);
+            dx_rput(accR, accQ, pr, prq, lane, wave);
+            DST(14);
+            po.finish(a.ctl, a.timeout_ticks, t, DX_O3, abort_flag);
+            dx_stage(stg_of(1), lane, po.v);
+        }
+        DST(15);
+        // ---- o3 slice → O4 → fine logits
+        dx_o24(ao4, stg_of(1), po4, lane, wave);
+        bar();
+        DST(16);
+        if (tid < 4 * kDxUO2) {
+            const int r = tid % kDxUO2, n = tid / kDxUO2;
+            xpub(xg + kDxHopOff[DX_LF] + n * kDxQ + kDxUO2 * c + r, tag, dx_o24sum(po4, r, n) + cst[DC_B4 + r]);
+        }
+        DST(17);
+        // ---- sample f_t (:149-151); combine_signal (utils/dsp.py:33); previous labels ← (c_t, f_t)
+        if (wave < RX) {
+            const int fl = sample_row(DX_LF, 1);
+            if (lane == 0) {
+                const float cl = lab[8 + wave];
+                lab[wave] = cl;
+                lab[4 + wave] = (float)fl;
+                if (c == 0) {
+                    const int v = (int)cl * 256 + fl - 32768;
+                    const size_t o = (size_t)(a.b0 + k + kXcds * wave) * a.L + t;
+                    a.out[o] = (float)v;
+                    if (a.labels) a.labels[o] = v;
+                }
+            }
+        }
+        DST(18);
+        if (more) {
+            float *slot = nzr + ((t + 1) & 1) * 4 * 2 * kDxQ;
+#pragma unroll
+            for (int i = 0; i < kNzLd; ++i) {
+                const int idx = tid + kDxThreads * i;
+                if (idx < RX * kNzF4) {
+                    const int n = idx / kNzF4, f = idx - n * kNzF4;
+                    *reinterpret_cast<f4v *>(slot + n * 2 * kDxQ + 4 * f) = nzl[i];
+                }
+            }
+        }
+        bar();
+        if (*abort_flag) return;
+    }
+    if (kDbg && a.dbg) {
+        __syncthreads();
+        for (int i = tid; i < kDxDbgSteps * kDxWaves * kDxStamps; i += kDxThreads) {
+            const int stp = i / (kDxWaves * kDxStamps), w = (i / kDxStamps) % kDxWaves, kk = i % kDxStamps;
+            a.dbg[(((size_t)blockIdx.x * kDxWaves + w) * kDxDbgSteps + stp) * kDxStamps + kk] = dbgs[i];
+        }
+    }
+    // ---- carry the recurrent state to the next time chunk
+    if (gate) {
+        st[gn * 2 * kDxU + gu] = hc;
+        st[gn * 2 * kDxU + kDxU + gu] = hf;
+    }
+    for (int i = tid; i < kDxPR; i += kDxThreads) st[8 * kDxU + i] = pr[i];
+    for (int i = tid; i < kDxPRQ; i += kDxThreads) st[8 * kDxU + kDxPR + i] = prq[i];
+    if (tid < 8) st[8 * kDxU + kDxPR + kDxPRQ + tid] = lab[tid];
+}
+
+hipError_t launch_dx(const DxArgs &a, hipStream_t st) {
+    DxArgs args = a;
+    void *params[] = {&args};
+    const bool dbg = a.dbg != nullptr;
+    const void *kf = dbg ? (const void *)deepmind_xcd_kernel<true> : (const void *)deepmind_xcd_kernel<false>;
+    return hipLaunchKernel(kf, dim3(kXcds * kXcdWgs), dim3(kDxThreads), params, dx_lds_layout(dbg).total * sizeof(float),
+                           st);
+}
+
+// set the LDS limit; *ok = the launch is co-resident (one workgroup per CU)
+hipError_t prepare_dx_kernel(int max_lds_bytes, bool *ok) {
+    *ok = false;
+    for (int dbg = 0; dbg < 2; ++dbg) {
+        const void *kf = dbg ? (const void *)deepmind_xcd_kernel<true> : (const void *)deepmind_xcd_kernel<false>;
+        const size_t lds = dx_lds_layout(dbg).total * sizeof(float);
+        if (lds > (size_t)max_lds_bytes) return hipSuccess;
+        hipError_t e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds_bytes);
+        if (e != hipSuccess) return e;
+        int n = 0;
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kf, kDxThreads, lds);
+        if (e != hipSuccess) return e;
+        if (n < 1) return hipSuccess;
+    }
+    *ok = true;
+    return hipSuccess;
+}
+
+}  // namespace wrnn

@@ -40,47 +40,11 @@
 #include "fatchord_loop.h"
 #include "fatchord_xcd.h"
 #include "fatchord_xcdm.h"
+#include "mfma_device.h"
 #include "wrnn_device.h"
 #include "xcd_device.h"
 
 namespace wrnn {
-
-// v_mfma_f32_4x4x1_16b_f32 as inline asm, so that the weights (A) stay where they are: sets
-// MS_IH2..MS_HH2 (256 values per lane) in AGPRs, read by the MFMA directly ("a"), the W_hh1 sets
-// in VGPRs — with the builtin, hipcc keeps the weights in AGPRs and copies each one to a VGPR
-// (v_accvgpr_read) in front of its MFMA.  Hazards the compiler cannot see inside asm: the
-// accumulator chain is dst == srcC (back-to-back, no wait states); the first MFMA of a chain
-// takes srcC = 0 (no VALU-written input); the weights are written once, before the loop; the B
-// operands come straight from ds_read (waitcnt, no wait states); the VALU reads of a finished
-// accumulator wait behind mfma_drain's s_nop (which ties the accumulators).
-template <bool kAgpr>
-__device__ __forceinline__ void mfma_first(f4v &d, float a, float b) {
-    if (kAgpr) asm volatile("v_mfma_f32_4x4x1_16b_f32 %0, %1, %2, 0" : "=&v"(d) : "a"(a), "v"(b));
-    else asm volatile("v_mfma_f32_4x4x1_16b_f32 %0, %1, %2, 0" : "=&v"(d) : "v"(a), "v"(b));
-}
-template <bool kAgpr>
-__device__ __forceinline__ void mfma_acc(f4v &d, float a, float b) {
-    if (kAgpr) asm volatile("v_mfma_f32_4x4x1_16b_f32 %0, %1, %2, %0" : "+v"(d) : "a"(a), "v"(b));
-    else asm volatile("v_mfma_f32_4x4x1_16b_f32 %0, %1, %2, %0" : "+v"(d) : "v"(a), "v"(b));
-}
-// the same for v_mfma_f32_16x16x4_f32 (16 weight rows × 16 batch rows × 4 columns)
-template <bool kAgpr>
-__device__ __forceinline__ void mfma16_first(f4v &d, float a, float b) {
-    if (kAgpr) asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, 0" : "=&v"(d) : "a"(a), "v"(b));
-    else asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, 0" : "=&v"(d) : "v"(a), "v"(b));
-}
-template <bool kAgpr>
-__device__ __forceinline__ void mfma16_acc(f4v &d, float a, float b) {
-    if (kAgpr) asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(d) : "a"(a), "v"(b));
-    else asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(d) : "v"(a), "v"(b));
-}
-__device__ __forceinline__ void mfma16_drain_begin() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory"); }
-
-// ≥ 8 wait states between the last MFMA writing an accumulator and any VALU read of it: one
-// s_nop pair, then an empty asm per accumulator that "redefines" it (volatile asm keep their
-// order, so every read of the accumulator comes after the nops)
-__device__ __forceinline__ void mfma_drain_begin() { asm volatile("s_nop 7\n\ts_nop 1" ::: "memory"); }
-__device__ __forceinline__ void mfma_tie(f4v &a) { asm volatile("" : "+v"(a)); }
 
 // Σ of the wave's four k-slices (lanes l, l ^ 16, l ^ 32, l ^ 48): identical bits in all four
 __device__ __forceinline__ f4v kslice_sum(f4v d) {
@@ -773,18 +737,22 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
 }
 
 // The in-kernel Philox draws of launch rows [0, nb) for steps [t0, t0 + Lc) into the injected-noise
-// layout [Lc][nb][11] (philox_noise keyed by (seed, row0 + row, step, k) exactly as the loop
-// kernels key them: bit-identical audio), so the loop only loads them
-__global__ void philox_fill_kernel(float *out, unsigned long long seed, long long row0, int nb, int t0, int Lc) {
+// layout [Lc][nb][K] (philox_noise keyed by (seed, row0 + row, step, k) exactly as the loop
+// kernels key them: bit-identical audio), so the loop only loads them.  K = 11, mol = 1: the MoL
+// uniforms; K = 2Q, mol = 0: the deepmind Exp(1) draws.
+__global__ void philox_fill_kernel(float *out, unsigned long long seed, long long row0, int nb, int t0, int Lc, int K,
+                                   int mol) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (long long)Lc * nb * 11) return;
-    const int kk = (int)(i % 11), lr = (int)((i / 11) % nb), dt = (int)(i / (11LL * nb));
-    out[i] = philox_noise(seed, (unsigned long long)(row0 + lr), (uint32_t)(t0 + dt), (uint32_t)kk, 1);
+    if (i >= (long long)Lc * nb * K) return;
+    const int kk = (int)(i % K), lr = (int)((i / K) % nb), dt = (int)(i / ((long long)K * nb));
+    out[i] = philox_noise(seed, (unsigned long long)(row0 + lr), (uint32_t)(t0 + dt), (uint32_t)kk, mol);
 }
 
-hipError_t launch_philox_fill(float *out, unsigned long long seed, long long row0, int nb, int t0, int Lc, hipStream_t st) {
-    const long long n = (long long)Lc * nb * 11;
-    hipLaunchKernelGGL(philox_fill_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out, seed, row0, nb, t0, Lc);
+hipError_t launch_philox_fill(float *out, unsigned long long seed, long long row0, int nb, int t0, int Lc, int K, int mol,
+                              hipStream_t st) {
+    const long long n = (long long)Lc * nb * K;
+    hipLaunchKernelGGL(philox_fill_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out, seed, row0, nb, t0, Lc,
+                       K, mol);
     return hipGetLastError();
 }
 

@@ -143,8 +143,10 @@ class FatchordLoop:
 
 
 class DeepmindLoop(FatchordLoop):
-    """Handle on the dual-softmax kernel (deepmind_rows.hip) replacing the per-step loop of
-    models/deepmind_version.py:generate (:98-156) for B independent rows."""
+    """Handle on the dual-softmax kernels replacing the per-step loop of
+    models/deepmind_version.py:generate (:98-156) for B independent rows: deepmind_xcd.hip
+    (hidden 896 / quantisation 256: 4 rows per XCD, 32 per launch, info["last_path"] 8) or
+    deepmind_rows.hip (other dims, or WRNN_PATH=rows: path 3)."""
     keys = DM_KEYS
 
     def __init__(self, hidden_size: int = 896, quantisation: int = 256, device: int = 0, grid: int = 0,
