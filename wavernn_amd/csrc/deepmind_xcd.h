@@ -95,7 +95,7 @@ struct DxArgs {
 };
 
 struct DxLds {
-    int stg, ao, pr, prq, po1, po3, po2, po4, lg, nz, cst, lab, misc, dbg, total;
+    int stg, ao, pr, prq, rs, po1, po3, po2, po4, nz, cst, lab, misc, dbg, total;
 };
 constexpr int kDxST = kDxKW + 4;   // staged slice row stride (floats)
 // A operands read from LDS instead of registers (the quarter set and O2 / O4: 42 per lane and
@@ -108,12 +108,12 @@ __host__ __device__ inline DxLds dx_lds_layout(bool dbg = false) {
     l.ao = o;   o += kDxWaves * kDxAL * 64;
     l.pr = o;   o += kDxPR;
     l.prq = o;  o += kDxPRQ;
+    l.rs = o;   o += 84 * 4;                       // Σ R·h of the own 84 gate rows [rr][n]
     l.po1 = o;  o += kDxWaves * 16 * 20;
     l.po3 = o;  o += kDxWaves * 16 * 20;
     l.po2 = o;  o += kDxWaves * 8 * 4 * 8;         // [wave][row 8][n 4][8 k-slices]
     l.po4 = o;  o += kDxWaves * 8 * 4 * 8;
-    l.lg = o;   o += 4 * kDxQ;                     // the logits of the 4 rows
-    l.nz = o;   o += 2 * 4 * 2 * kDxQ;             // draws of steps t, t + 1 (by parity) [2][n][2Q]
+    l.nz = o;   o += 2 * 4 * 2 * kDxQ;             // log q of steps t, t + 1 (by parity) [2][n][2Q]
     l.cst = o;  o += kDxCst + 4;
     l.lab = o;  o += 16;                           // previous coarse [4], fine [4], c_t [4]
     l.misc = o; o += 8;                            // [0] abort flag, [1] member index

@@ -15,15 +15,17 @@
 //   R[:, :S]·h_c — the coarse half of the next step's R·h (5 sets + a quarter set, accumulators
 //   kept in registers), the o1 poll riding along
 //   o1 slice → O2 (8 rows) → barrier → +b                               → publish logits [hop Lc]
-//   sample c_t: wave n polls row n's 256 logits and samples it (softmax → Categorical ≡
-//   argmax(p / q), q ~ Exp(1)) in every workgroup — no label hop
+//   sample c_t: wave n polls row n's 256 logits and samples it in every workgroup — no label
+//   hop: softmax → Categorical ≡ argmax_c p_c / q_c, q ~ Exp(1) (the reference's multinomial
+//   draw under the noise contract), taken as argmax_c l_c − log q_c (no exp, no divisions)
 //   fine gates (R·h_{t-1}, I_fine(prev, c_t))                            → publish h_f    [hop Hf]
 //   h_f slice → O3 → barrier → relu(+b)                                  → publish o3     [hop O3]
 //   R[:, S:]·h_f (finishes R·h_t; partials → LDS for step t + 1), the o3 poll riding along
 //   o3 slice → O4 → barrier → +b                                         → publish logits [hop Lf]
 //   sample f_t; workgroup 0 of the XCD writes combine_signal(c_t, f_t) (utils/dsp.py:33)
 // The draws of step t + 1 (Exp(1): injected, or Philox precomputed by philox_fill_kernel) are
-// loaded into registers after the h_c poll and stored into an LDS ring after f_t.
+// loaded into registers of waves 1..3 after the h_c poll; their logs go into an LDS ring while
+// wave 0 publishes o1.
 //
 // Membership as in fatchord_xcd.hip (XCC id + per-XCD arrival counter; bounded waits).  fp32,
 // sums re-associated; the sampled labels are checked bit-exact against the oracle.
@@ -40,6 +42,10 @@ namespace wrnn {
 namespace {
 
 __device__ __forceinline__ f2v lds2(const float *p) { return *reinterpret_cast<const f2v *>(p); }
+// log q of the Exp(1) draws (q ≥ 2^-24, normal): v_log_f32 (log2) · ln 2, monotone — the argmax
+// it feeds only compares l_c − log q_c across classes
+__device__ __forceinline__ float fast_log(float q) { return __builtin_amdgcn_logf(q) * 0.693147180559945309f; }
+__device__ __forceinline__ f4v log4(f4v q) { return f4v{fast_log(q.x), fast_log(q.y), fast_log(q.z), fast_log(q.w)}; }
 
 // wave w's slice of a 448-wide hop vector, 4 rows: 224 granule pairs, pair p = min(lane + 64i,
 // 223) (i < 4; lanes 32..63 of i = 3 repeat pairs 192..223): row p / 56, columns
@@ -285,8 +291,8 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
     const DxLds ll = dx_lds_layout(kDbg);
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     float *pr = smem + ll.pr, *prq = smem + ll.prq, *po1 = smem + ll.po1, *po3 = smem + ll.po3;
-    float *po2 = smem + ll.po2, *po4 = smem + ll.po4, *lg = smem + ll.lg, *nzr = smem + ll.nz;
-    float *cst = smem + ll.cst, *lab = smem + ll.lab;
+    float *po2 = smem + ll.po2, *po4 = smem + ll.po4, *nzr = smem + ll.nz;
+    float *cst = smem + ll.cst, *lab = smem + ll.lab, *rs = smem + ll.rs;
     int *misc = reinterpret_cast<int *>(smem + ll.misc);
     int *abort_flag = misc;
     unsigned *dbgs = reinterpret_cast<unsigned *>(smem + ll.dbg);
@@ -342,6 +348,10 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
     for (int i = tid; i < kDxPR; i += kDxThreads) pr[i] = resume ? st[8 * kDxU + i] : 0.0f;
     for (int i = tid; i < kDxPRQ; i += kDxThreads) prq[i] = resume ? st[8 * kDxU + kDxPR + i] : 0.0f;
     if (tid < 16) lab[tid] = (resume && tid < 8) ? st[8 * kDxU + kDxPR + kDxPRQ + tid] : 0.0f;   // out_coarse = out_fine = 0 (:89-90)
+    // Σ R·h of every own gate row (WG-local row rr, batch row n) → rs[rr·4 + n], from the partials
+    auto r_sums = [&](int e0, int de) {
+        for (int e = e0; e < 84 * 4; e += de) rs[e] = dx_rsum(pr, prq, e >> 2, e & 3);
+    };
     float hc = 0.0f, hf = 0.0f;   // h of (unit gu, row gn): this thread's recurrent state
     if (gate && resume) {
         hc = st[gn * 2 * kDxU + gu];
@@ -350,12 +360,16 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
     for (int i = tid; i < RX * 2 * kDxQ / 4; i += kDxThreads) {
         const int n = i / (2 * kDxQ / 4), f = i - n * (2 * kDxQ / 4);
         *reinterpret_cast<f4v *>(nzr + ((a.t0 & 1) * 4 + n) * 2 * kDxQ + 4 * f) =
-            *reinterpret_cast<const f4v *>(noise_src(a.t0, n) + 4 * f);
+            log4(*reinterpret_cast<const f4v *>(noise_src(a.t0, n) + 4 * f));
     }
+    __syncthreads();
+    r_sums(tid, kDxThreads);
     __syncthreads();
 
     constexpr int kNzF4 = 2 * kDxQ / 4;                         // float4s of one row's draws
-    constexpr int kNzLd = (kDxRowsXcd * kNzF4 + kDxThreads - 1) / kDxThreads;   // per thread
+    // draws loaded by waves 1..3 (wave 0 publishes the O1 epilogue meanwhile)
+    constexpr int kNzThreads = kDxThreads - 64;
+    constexpr int kNzLd = (kDxRowsXcd * kNzF4 + kNzThreads - 1) / kNzThreads;   // per thread
 
     for (int t = a.t0; t < t_end; ++t) {
         int tid = threadIdx.x;   // opaque per step (see fatchord_xcdm.hip)
@@ -364,6 +378,9 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         const uint32_t tag = (uint32_t)t + 1u;
         const bool more = t + 1 < t_end;
         DST(0);
+        if (kDbg && lane == 0 && (unsigned)(t - a.t0 - kDxDbgSkip) < (unsigned)kDxDbgSteps)
+            dbgs[((t - a.t0 - kDxDbgSkip) * kDxWaves + wave) * kDxStamps + kDxStamps - 1] =
+                (unsigned)__builtin_amdgcn_s_memrealtime();
         // ---- coarse gates (:106-125): R·h_{t-1} (partials of the previous step), I_coarse(prev)
         if (gate) {
             const float x0 = lab[gn] / 127.5f - 1.0f, x1 = lab[4 + gn] / 127.5f - 1.0f;
@@ -372,7 +389,7 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             for (int g = 0; g < 3; ++g) {   // separately rounded products (:111)
                 const float *wi = cst + DC_IC + (g * kDxU + gu) * 2;
                 I[g] = __fadd_rn(__fmul_rn(wi[0], x0), __fmul_rn(wi[1], x1));
-                Rg[g] = dx_rsum(pr, prq, g * kDxU + gu, gn);
+                Rg[g] = rs[(g * kDxU + gu) * 4 + gn];
             }
             const float uu = sigmoid_((Rg[0] + I[0]) + cst[DC_BU + gu]);
             const float rr = sigmoid_((Rg[1] + I[1]) + cst[DC_BR + gu]);
@@ -388,13 +405,14 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             dx_poll(hop_rsrc(xg + kDxHopOff[DX_HC]), wave, tag, a.ctl, a.timeout_ticks, t, DX_HC, abort_flag, lane, v);
             dx_stage(stg_of(0), lane, v);
         }
-        // the draws of step t + 1 → registers (stored into the ring after f_t); issued here, the
-        // first wait that covers them is the o1 poll's, one R half later
+        // the draws of step t + 1 → registers of waves 1..3; their logs go into the ring while
+        // wave 0 publishes o1 (below)
         f4v nzl[kNzLd];
-        if (more) {
+        const int lt = tid - 64;
+        if (more && lt >= 0) {
 #pragma unroll
             for (int i = 0; i < kNzLd; ++i) {
-                const int idx = tid + kDxThreads * i;
+                const int idx = lt + kNzThreads * i;
                 if (idx < RX * kNzF4) {
                     const int n = idx / kNzF4, f = idx - n * kNzF4;
                     nzl[i] = *reinterpret_cast<const f4v *>(noise_src(t + 1, n) + 4 * f);
@@ -409,6 +427,16 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             const int r = tid % kDxU, n = tid / kDxU;
             const float o = dx_o13sum(po1, r, n) + cst[DC_B1 + r];
             xpub(xg + kDxHopOff[DX_O1] + n * kDxS + kDxU * c + r, tag, o > 0.0f ? o : 0.0f);
+        } else if (more && lt >= 0) {   // log q of step t + 1 → ring slot (t + 1) & 1
+            float *slot = nzr + ((t + 1) & 1) * 4 * 2 * kDxQ;
+#pragma unroll
+            for (int i = 0; i < kNzLd; ++i) {
+                const int idx = lt + kNzThreads * i;
+                if (idx < RX * kNzF4) {
+                    const int n = idx / kNzF4, f = idx - n * kNzF4;
+                    *reinterpret_cast<f4v *>(slot + n * 2 * kDxQ + 4 * f) = log4(nzl[i]);
+                }
+            }
         }
         DST(4);
         // ---- R[:, :S]·h_c (next step's R·h, coarse half) with the o1 poll riding along
@@ -433,7 +461,7 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         // ---- sample c_t (:129-131): wave n samples row n
         auto sample_row = [&](int hop, int half) -> int {
             const __amdgpu_buffer_rsrc_t rl = hop_rsrc(xg + kDxHopOff[hop]);
-            float *l = lg + wave * kDxQ;
+            f4v lv = {0.0f, 0.0f, 0.0f, 0.0f};
             const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
             unsigned spins = 0;
             for (;;) {
@@ -441,8 +469,7 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
                 const u4v v1 = ld16_sc1(rl, (wave * kDxQ + 2 * lane + 128) * 8);
                 const bool ok = (v0.y == tag) & (v0.w == tag) & (v1.y == tag) & (v1.w == tag);
                 if (__ballot(!ok) == 0) {
-                    *reinterpret_cast<f2v *>(l + 2 * lane) = f2v{__uint_as_float(v0.x), __uint_as_float(v0.z)};
-                    *reinterpret_cast<f2v *>(l + 2 * lane + 128) = f2v{__uint_as_float(v1.x), __uint_as_float(v1.z)};
+                    lv = f4v{__uint_as_float(v0.x), __uint_as_float(v0.z), __uint_as_float(v1.x), __uint_as_float(v1.z)};
                     break;
                 }
                 if ((++spins & 63u) == 0) {
@@ -455,9 +482,16 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
                     }
                 }
             }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            const float *q = nzr + ((t & 1) * 4 + wave) * 2 * kDxQ + half * kDxQ;
-            return raw_sample<4>(l, q, kDxQ, lane);
+            // argmax_c l_c − log q_c ≡ argmax_c p_c / q_c (softmax, Categorical renormalisation and
+            // the draw's scale cancel): lane l holds classes 2l, 2l + 1, 2l + 128, 2l + 129
+            const float *lq = nzr + ((t & 1) * 4 + wave) * 2 * kDxQ + half * kDxQ;
+            const f2v q0 = lds2(lq + 2 * lane), q1 = lds2(lq + 2 * lane + 128);
+            float bv = lv.x - q0.x;
+            int bi = 2 * lane;
+            am_merge(bv, bi, lv.y - q0.y, 2 * lane + 1);
+            am_merge(bv, bi, lv.z - q1.x, 2 * lane + 128);
+            am_merge(bv, bi, lv.w - q1.y, 2 * lane + 129);
+            return wave_argmax(bv, bi);
         };
         if (wave < RX) {
             const int cl = sample_row(DX_LC, 0);
@@ -474,7 +508,7 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             for (int g = 0; g < 3; ++g) {   // (:137)
                 const float *wi = cst + DC_IF + (g * kDxU + gu) * 3;
                 I[g] = __fadd_rn(__fadd_rn(__fmul_rn(wi[0], x0), __fmul_rn(wi[1], x1)), __fmul_rn(wi[2], x2));
-                Rg[g] = dx_rsum(pr, prq, (3 + g) * kDxU + gu, gn);
+                Rg[g] = rs[((3 + g) * kDxU + gu) * 4 + gn];
             }
             const float uu = sigmoid_((Rg[0] + I[0]) + cst[DC_BU + kDxU + gu]);
             const float rr = sigmoid_((Rg[1] + I[1]) + cst[DC_BR + kDxU + gu]);
@@ -516,6 +550,8 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         if (tid < 4 * kDxUO2) {
             const int r = tid % kDxUO2, n = tid / kDxUO2;
             xpub(xg + kDxHopOff[DX_LF] + n * kDxQ + kDxUO2 * c + r, tag, dx_o24sum(po4, r, n) + cst[DC_B4 + r]);
+        } else if (tid >= 64) {
+            r_sums(tid - 64, kDxThreads - 64);   // R·h_t (complete since the barrier) for step t + 1's gates
         }
         DST(17);
         // ---- sample f_t (:149-151); combine_signal (utils/dsp.py:33); previous labels ← (c_t, f_t)
@@ -534,17 +570,6 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             }
         }
         DST(18);
-        if (more) {
-            float *slot = nzr + ((t + 1) & 1) * 4 * 2 * kDxQ;
-#pragma unroll
-            for (int i = 0; i < kNzLd; ++i) {
-                const int idx = tid + kDxThreads * i;
-                if (idx < RX * kNzF4) {
-                    const int n = idx / kNzF4, f = idx - n * kNzF4;
-                    *reinterpret_cast<f4v *>(slot + n * 2 * kDxQ + 4 * f) = nzl[i];
-                }
-            }
-        }
         bar();
         if (*abort_flag) return;
     }
