@@ -33,7 +33,7 @@ from wavernn_amd import synthetic as syn  # noqa: E402
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak (dense)
 MOL_MACS_PER_ROW_STEP = 3825152   # loop MACs per row-step, MoL rnn 512
-PMC_PROFILE = os.environ.get("WRNN_PMC_PROFILE", os.path.join(REPO, "profiles", "r03_v1_pmc_traffic.json"))
+PMC_PROFILE = os.environ.get("WRNN_PMC_PROFILE", os.path.join(REPO, "profiles", "r03_v2_pmc_traffic.json"))
 SPARSE896_BYTES_PER_STEP = 5536598   # config 4 sparse values + int16 block indices, fp32
 DM_BYTES_PER_STEP = 12200196         # config 5 deepmind weights, fp32
 
@@ -162,9 +162,12 @@ def other_configs(dev) -> dict:
     ms = loop5.elapsed_ms()
     res["config5_deepmind_32utt"] = {"samples_per_s": B5 * L5 / ms * 1e3, "rtf": B5 * L5 / ms * 1e3 / 16000.0,
                                      "rows": B5, "loop_steps": L5, "device_ms": ms, "us_per_loop_step": ms * 1e3 / L5,
+                                     "kernel_path": loop5.info["last_path"],
                                      "roofline": hbm_roofline(DM_BYTES_PER_STEP + 4 * B5, ms * 1e3 / L5,
                                                               "SURVEY.md 8(d) bytes per step (weights once + 4 B per "
-                                                              "row) / step time; weights LDS-resident, latency-bound")}
+                                                              "row) / step time; weights resident in each XCD's "
+                                                              "registers + LDS (path 8 = deepmind_xcd_kernel, 4 rows "
+                                                              "per XCD), hand-off-latency-bound")}
     loop5.close()
     return res
 

@@ -89,7 +89,9 @@ typedef struct {
     int32_t split_grid;      /* batch-1 MoL role-split kernel: GRU + FC workgroups (0: unavailable) */
     int32_t last_path;       /* kernel of the last wrnn_generate: 1 latency, 2 multi-row,
                                 3 deepmind, 4 role-split, 5 XCD-resident, 6 XCD-resident
-                                block-sparse rnn 896, 7 XCD-resident many-row (0: none yet) */
+                                block-sparse rnn 896, 7 XCD-resident many-row, 8 XCD-resident
+                                deepmind, 9 multi-row with the weights streamed from HBM (dense
+                                weights beyond LDS), 10 deepmind streamed (0: none yet) */
     int32_t xcd_rows;        /* XCD-resident kernel (dense rnn 512, or rnn 896 with block-sparse
                                 GRU weights once they are set): rows per launch (0: unavailable) */
     int32_t xcdm_rows;       /* XCD-resident many-row kernel (MoL rnn/fc 512): rows per launch

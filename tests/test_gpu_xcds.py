@@ -97,17 +97,6 @@ def test_xcds_agrees_with_rows_kernel_under_philox(monkeypatch):
     assert (res["xcd"] - res["rows"]).abs().max().item() <= 2 * gf.MOL_TOL
 
 
-def test_dense_896_weights_are_refused(monkeypatch):
-    """Unpruned rnn-896 weights are not block-sparse: no kernel holds them (the sparse XCD kernel
-    included), set_weights says so instead of running a fallback."""
-    from wavernn_amd._native import WrnnError
-    monkeypatch.delenv("WRNN_PATH", raising=False)
-    d = syn.SPARSE896_MOL
-    loop = _loop(d)
-    with pytest.raises(WrnnError, match="block-sparse"):
-        loop.set_weights(syn.make_fatchord_state(d, 660))
-
-
 def test_xcds_one_second_vs_oracle(monkeypatch):
     """A full 1 s utterance (22 275 loop steps, one row) of config 4's sparse rnn-896 model against
     the C oracle under injected noise: no drift over the utterance."""

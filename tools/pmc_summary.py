@@ -23,7 +23,8 @@ HEADLINE = ("fatchord_xcd_kernel", "fatchord_split_kernel", "fatchord_loop_kerne
 # bench.py --steps 1 --other-configs 1 run: warm-up + timed generate of that config)
 OTHER = {"fatchord_xcdm_kernel": ("config3_mol_fold_60s", 2 * 12100),
          "fatchord_xcds_kernel": ("config4_sparse896_8utt", 100 + 110275),
-         "deepmind_rows_kernel": ("config5_deepmind_32utt", 100 + 16000)}
+         "deepmind_rows_kernel": ("config5_deepmind_32utt", 100 + 16000),
+         "deepmind_xcd_kernel": ("config5_deepmind_32utt", 100 + 16000)}
 
 
 def rows(path):

@@ -104,7 +104,8 @@ struct wrnn_ctx {
     bool sparse = false;                            // GRU weights stored as nonzero 4x4 blocks
     int NT = 0, KX = 0, KA = 0;
     int KXc = 0;                                    // XCD kernels' terms-GEMM depth: [cond record | 1 0 0 0]
-    bool rows_ok = false;                           // weights fit LDS with at least one row
+    bool rows_ok = false;                           // weights fit LDS with at least one row (or stream)
+    bool rows_gw = false;                           // dense weights exceed LDS: the slab is streamed from HBM
     float *d_rslab = nullptr, *d_Wt = nullptr;      // per-workgroup slabs, terms-GEMM weights [G·NT][KX]
     float *d_X = nullptr, *d_T = nullptr, *d_act = nullptr, *d_state = nullptr;
     size_t X_cap = 0, T_cap = 0, act_cap = 0, state_cap = 0;   // floats
@@ -122,6 +123,7 @@ struct wrnn_ctx {
     DmSlab ds{};
     int dmU = 0, dmUO = 0, dmUO2 = 0;
     bool dm = false;
+    bool dm_gw = false;                             // the DM slab exceeds LDS: streamed from HBM
     float *d_dmslab = nullptr;
     DmPart dm2{};                                   // G/2 workgroups, twice the units: two row groups per launch
     unsigned *d_dmflags = nullptr;
@@ -504,7 +506,8 @@ void pack_terms_weights_composed(const wrnn_ctx &h, float *Wt) {
 }
 
 size_t rows_lds_bytes(const wrnn_ctx &h, int B, int TB, bool head_lds = true) {
-    return (size_t)rows_lds_layout(head_lds ? h.rs.total : h.rs.body, B, TB, h.cfg.rnn_dims, h.cfg.fc_dims,
+    const int slab = h.rows_gw ? 0 : head_lds ? h.rs.total : h.rs.body;
+    return (size_t)rows_lds_layout(slab, B, TB, h.cfg.rnn_dims, h.cfg.fc_dims,
                                    h.cfg.n_classes, h.NK, h.rU, h.rUF, h.rG)
                .total * sizeof(float);
 }
@@ -527,7 +530,13 @@ void set_rows_partition(wrnn_ctx &h, int nbmax) {
     h.rUC = mol ? 0 : (h.cfg.n_classes + h.rG - 1) / h.rG;
     h.NT = rows_terms(h.rU, h.rUF);
     h.rs = make_rows_slab(h, nbmax);
+    h.rows_gw = false;
     h.rows_ok = rows_tile_for(h, 1) > 0;
+    // dense weights beyond the grid's LDS: the same kernel with the slab streamed from HBM
+    if (!h.rows_ok && nbmax == 0) {
+        h.rows_gw = true;
+        h.rows_ok = rows_tile_for(h, 1) > 0;
+    }
 }
 
 // Largest tile (<= 16 rows; up to 32 with the MoL head left in HBM) that fits next to B rows of
@@ -566,7 +575,7 @@ struct PartScope {
 // The two-group partition: dense weights over G/2 workgroups (G even)
 void set_group_partition(wrnn_ctx &h) {
     h.g2 = RowsPart{};
-    if (h.G % 2 || h.G < 8) return;
+    if (h.G % 2 || h.G < 8 || h.rows_gw) return;
     RowsPart flat{};
     swap_part(h, flat);   // h.r* empty, flat holds the current partition
     const int R = h.cfg.rnn_dims, F = h.cfg.fc_dims;
@@ -719,7 +728,7 @@ void pack_dx_slab(const wrnn_ctx &h, std::vector<float> &slab) {
 
 size_t dm_lds_bytes(const wrnn_ctx &h, int B, int TB) {
     const int S = h.cfg.rnn_dims / 2;
-    return (size_t)dm_lds_layout(h.ds.total, B, TB, S, h.cfg.n_classes, h.dmU, h.G).total * sizeof(float);
+    return (size_t)dm_lds_layout(h.dm_gw ? 0 : h.ds.total, B, TB, S, h.cfg.n_classes, h.dmU, h.G).total * sizeof(float);
 }
 
 int dm_tile_for(const wrnn_ctx &h, int B) {
@@ -1321,6 +1330,7 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
             a.dbg = (b0 == 0 && t0 == 0) ? d_dbg : nullptr;
             a.dbg_steps = std::min(dbg_steps, Lc);
             a.head_lds = head_lds ? 1 : 0;
+            a.gw = h->rows_gw ? 1 : 0;
             RowsGroup g1{};
             if (grouped) {
                 g1.terms = h->d_T + T_grp;
@@ -1484,6 +1494,7 @@ int generate_dm(wrnn_t *h, int B, int L, const float *noise, uint64_t seed, int6
         a.TB = TB;
         a.KA = h->KA;
         a.s = h->ds;
+        a.gw = h->dm_gw ? 1 : 0;
         DmGroup g1{};
         if (grouped) {
             g1.act = h->d_act + act_grp;
@@ -1933,15 +1944,16 @@ int wrnn_create(const wrnn_config *cfg, int device, wrnn_t **out) {
         h->KA = round4(std::max(S, Q));
         h->NK = 2 * Q;
         h->ds = make_dm_slab(*h);
+        if (dm_tile_for(*h, 1) == 0) h->dm_gw = true;   // weights beyond LDS: stream the slab
         if (dm_tile_for(*h, 1) == 0)
-            return fail(h, WRNN_EUNSUPPORTED, "DM weight slab exceeds LDS (" + std::to_string(dm_lds_bytes(*h, 1, 1)) + " B)");
+            return fail(h, WRNN_EUNSUPPORTED, "DM: one row of state does not fit LDS (" + std::to_string(dm_lds_bytes(*h, 1, 1)) + " B)");
         HIP_TRY(h, prepare_dm_kernel(h->max_lds));
         int per_cu = 0;
         HIP_TRY(h, dm_occupancy(&per_cu, dm_lds_bytes(*h, 1, 1)));
         if (per_cu * h->num_cus < h->G)
             return fail(h, WRNN_EUNSUPPORTED, "DM persistent grid is not co-resident");
         // two row groups of G/2 workgroups (twice the units each), as the fatchord rows kernel
-        if (h->G % 2 == 0 && h->G >= 8) {
+        if (h->G % 2 == 0 && h->G >= 8 && !h->dm_gw) {
             DmPart p{};
             p.G = h->G / 2;
             p.dmU = (S + p.G - 1) / p.G;
@@ -2255,7 +2267,7 @@ int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise
     HIP_TRY(h, hipEventRecord(h->ev0, st));
     // deepmind hidden 896 / quantisation 256: the XCD-resident kernel (WRNN_PATH=rows: the multi-row one)
     const bool dx = h->dm && h->dx_ok && pe != "rows";
-    h->last_path = dx ? 8 : h->dm ? 3 : xcdm ? 7 : xcd ? 5 : xcds ? 6 : split ? 4 : rows ? 2 : 1;
+    h->last_path = dx ? 8 : h->dm ? (h->dm_gw ? 10 : 3) : xcdm ? 7 : xcd ? 5 : xcds ? 6 : split ? 4 : rows ? (h->rows_gw ? 9 : 2) : 1;
     const int rc = dx       ? generate_dx(h, B, L, noise, seed, row_offset, out, labels, st)
                    : h->dm  ? generate_dm(h, B, L, noise, seed, row_offset, out, labels, st)
                    : xcdm  ? generate_xcdm(h, cond, B, L, noise, seed, row_offset, out, st)
@@ -2285,13 +2297,13 @@ int wrnn_check(wrnn_t *h, void *stream) {
         static const char *split_hops[] = {"y", "f1", "f2", "h2", "h2", "gru1-terms", "gru1-terms"};
         static const char *xcd_hops[] = {"y", "f1", "f2", "h2", "gru1-terms", "gru1-terms"};
         static const char *xcdm_hops[] = {"h1", "y", "h2", "f1", "f2 (partial logits)", "x"};
-        const char *name = h->last_path == 8   ? (hop >= 0 && hop < 6 ? dm_hops[hop] : "?")
-                           : h->last_path == 7 ? (hop >= 0 && hop < 6 ? xcdm_hops[hop] : "?")
-                           : h->last_path >= 5 ? (hop >= 0 && hop < 6 ? xcd_hops[hop] : "?")
-                           : h->last_path == 4 ? (hop >= 0 && hop < 7 ? split_hops[hop] : "?")
-                           : h->last_path == 3 ? (hop >= 0 && hop < 8 ? dm_hops[hop] : "?")
-                           : h->last_path == 2 ? (hop >= 0 && hop < 6 ? row_hops[hop] : "?")
-                                               : (hop >= 0 && hop < 7 ? lat_hops[hop] : "?");
+        const int lp = h->last_path;
+        const char *name = lp == 8 || lp == 3 || lp == 10 ? (hop >= 0 && hop < 8 ? dm_hops[hop] : "?")
+                           : lp == 2 || lp == 9         ? (hop >= 0 && hop < 6 ? row_hops[hop] : "?")
+                           : lp == 7                    ? (hop >= 0 && hop < 6 ? xcdm_hops[hop] : "?")
+                           : lp >= 5                    ? (hop >= 0 && hop < 6 ? xcd_hops[hop] : "?")
+                           : lp == 4                    ? (hop >= 0 && hop < 7 ? split_hops[hop] : "?")
+                                                        : (hop >= 0 && hop < 7 ? lat_hops[hop] : "?");
         return fail(h, WRNN_ETIMEOUT,
                     "persistent kernel aborted: wait on hand-off '" + std::string(name) +
                         "' at step " + std::to_string(ctl[2]) + " in workgroup " + std::to_string(ctl[4]) +

@@ -50,6 +50,7 @@ struct DmArgs {
     int L, t0, Lc, B, Bt, b0;
     int H, S, Q, U, UO, UO2, G, TB, KA;
     DmSlab s;
+    int gw;                       // 1 = streamed weights: the slab stays in HBM (exceeds LDS)
 };
 
 // The per-group fields of a second row group sharing the launch (as RowsGroup, fatchord_rows.h)

@@ -27,7 +27,8 @@ namespace wrnn {
 // kS = 448 instantiates the shipped dims (hidden 896) with compile-time dot lengths.
 // Row groups as in fatchord_rows.hip: workgroups [G0, 2·G0) run a second, independent instance
 // over the rows of g1 (half the flags per hop, half the rows streamed per stage).
-template <int kS>
+// GW: the slab stays in HBM (hidden sizes whose weights exceed LDS), as fatchord_rows.hip's GW.
+template <int kS, bool GW>
 __global__ __launch_bounds__(kDmThreads) void deepmind_rows_kernel(DmArgs a, DmGroup g1, int G0) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, row = lane >> 4;
@@ -45,9 +46,9 @@ __global__ __launch_bounds__(kDmThreads) void deepmind_rows_kernel(DmArgs a, DmG
     const int w = (int)blockIdx.x - (grp1 ? G0 : 0);
     const int S = kS ? kS : a.S, H = 2 * S, Q = a.Q, U = a.U, UO = a.UO, UO2 = a.UO2, G = a.G, B = a.B;
     const int TB = a.TB, KA = a.KA;
-    const DmLds ll = dm_lds_layout(a.s.total, B, TB, S, Q, U, G);
+    const DmLds ll = dm_lds_layout(GW ? 0 : a.s.total, B, TB, S, Q, U, G);
     const DmSlab &s = a.s;
-    const float *W = smem + ll.slab;
+    const float *W = GW ? a.slab + (size_t)w * s.total : smem + ll.slab;
     float *tile = smem + ll.tile, *st = smem + ll.st, *pcv = smem + ll.pc, *pfv = smem + ll.pf;
     float *nzs = smem + ll.nz;
     int *abort_flag = reinterpret_cast<int *>(smem + ll.flag);
@@ -121,7 +122,8 @@ __global__ __launch_bounds__(kDmThreads) void deepmind_rows_kernel(DmArgs a, DmG
     {
         const float4 *src = reinterpret_cast<const float4 *>(a.slab + (size_t)w * s.total);
         float4 *dst = reinterpret_cast<float4 *>(smem + ll.slab);
-        for (int i = tid; i < s.total / 4; i += kDmThreads) dst[i] = src[i];
+        if (!GW)
+            for (int i = tid; i < s.total / 4; i += kDmThreads) dst[i] = src[i];
         const float *cs = a.state + (size_t)w * B * SW;
         for (int i = tid; i < B * SW; i += kDmThreads) st[i] = a.t0 > 0 ? cs[i] : 0.0f;
         const float *cx = a.state + (size_t)G * B * SW;
@@ -356,8 +358,13 @@ __global__ __launch_bounds__(kDmThreads) void deepmind_rows_kernel(DmArgs a, DmG
     }
 }
 
+#define WRNN_DM_KERNELS                                                                              \
+    (const void *)deepmind_rows_kernel<448, false>, (const void *)deepmind_rows_kernel<0, false>,      \
+        (const void *)deepmind_rows_kernel<0, true>
+
 static const void *pick_dm_kernel(const DmArgs &a) {
-    return a.S == 448 ? (const void *)deepmind_rows_kernel<448> : (const void *)deepmind_rows_kernel<0>;
+    if (a.gw) return (const void *)deepmind_rows_kernel<0, true>;
+    return a.S == 448 ? (const void *)deepmind_rows_kernel<448, false> : (const void *)deepmind_rows_kernel<0, false>;
 }
 
 hipError_t launch_dm(const DmArgs &a, const DmGroup *g1, size_t lds_bytes, hipStream_t st) {
@@ -369,7 +376,7 @@ hipError_t launch_dm(const DmArgs &a, const DmGroup *g1, size_t lds_bytes, hipSt
 }
 
 hipError_t prepare_dm_kernel(int max_lds_bytes) {
-    for (const void *k : {(const void *)deepmind_rows_kernel<448>, (const void *)deepmind_rows_kernel<0>}) {
+    for (const void *k : {WRNN_DM_KERNELS}) {
         hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds_bytes);
         if (e != hipSuccess) return e;
     }
@@ -378,7 +385,7 @@ hipError_t prepare_dm_kernel(int max_lds_bytes) {
 
 hipError_t dm_occupancy(int *blocks_per_cu, size_t lds_bytes) {
     int best = 1 << 30;
-    for (const void *k : {(const void *)deepmind_rows_kernel<448>, (const void *)deepmind_rows_kernel<0>}) {
+    for (const void *k : {WRNN_DM_KERNELS}) {
         int n = 0;
         hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kDmThreads, lds_bytes);
         if (e != hipSuccess) return e;

@@ -85,6 +85,7 @@ struct RowsArgs {
     unsigned *dbg;                // WRNN_DEBUG_STAMPS: [G][dbg_steps][kStamps] s_memrealtime per stage
     int dbg_steps;
     int head_lds;                 // MoL: 1 = head in LDS, 0 = samplers read it from HBM (workgroup 0's slab)
+    int gw;                       // 1 = streamed weights: the slab stays in HBM (weights exceed LDS)
 };
 
 // The per-group fields of a second row group sharing the launch (fatchord_rows.hip)

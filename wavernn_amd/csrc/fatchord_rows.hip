@@ -43,7 +43,12 @@ constexpr int kTileCpol = WRNN_TILE_CPOL;
 // instances of the loop (own rows, buffers, flags) in one launch.  With B large the activation
 // broadcast (every workgroup DMAs every row of every stage) is what limits a stage; two groups of
 // G/2 workgroups, each holding twice the weight rows, halve the rows each workgroup streams.
-template <bool MOL, int kRF, bool SPARSE>
+//
+// GW (streamed weights): the workgroup's slab stays in HBM and every weight read is a global load
+// (L2 / Infinity-Cache served after the first step).  For models whose dense weights exceed the
+// grid's LDS (e.g. rnn 896 unpruned: 32 MB of loop weights), so the drop-in accepts every size the
+// reference constructor does (models/fatchord_version.py:93-129); LDS then holds only row state.
+template <bool MOL, int kRF, bool SPARSE, bool GW>
 __global__ __launch_bounds__(kRowsThreads) void fatchord_rows_kernel(RowsArgs a, RowsGroup g1, int G0) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, row = lane >> 4;
@@ -64,12 +69,12 @@ __global__ __launch_bounds__(kRowsThreads) void fatchord_rows_kernel(RowsArgs a,
     const int w = (int)blockIdx.x - (grp1 ? G0 : 0);
     const int R = kRF ? kRF : a.R, F = kRF ? kRF : a.F, NC = a.NC, NK = a.NK, U = a.U, UF = a.UF, UC = a.UC, G = a.G, B = a.B;
     const int NT = a.NT, TB = a.TB, KA = a.KA;
-    const int slab_lds = (MOL && !a.head_lds) ? a.s.body : a.s.total;   // floats resident in LDS
+    const int slab_lds = GW ? 0 : (MOL && !a.head_lds) ? a.s.body : a.s.total;   // floats resident in LDS
     const RowsLds ll = rows_lds_layout(slab_lds, B, TB, R, F, NC, NK, U, UF, G);
     const RowsSlab &s = a.s;
-    const float *S = smem + ll.slab;
+    const float *S = GW ? a.slab + (size_t)w * s.total : smem + ll.slab;
     // MoL head [NC][F] then bias [NC]: LDS, or (large B) the HBM copy in workgroup 0's slab
-    const float *head = (MOL && !a.head_lds) ? a.slab + a.s.w3 : S + a.s.w3;
+    const float *head = (MOL && !a.head_lds && !GW) ? a.slab + a.s.w3 : S + a.s.w3;
     const int *spc = reinterpret_cast<const int *>(S + a.s.spc);     // sparse: block columns, counts
     const int *spn = reinterpret_cast<const int *>(S + a.s.spn);
     float *tile = smem + ll.tile, *st = smem + ll.st, *xs = smem + ll.x, *ring = smem + ll.ring;
@@ -156,7 +161,8 @@ __global__ __launch_bounds__(kRowsThreads) void fatchord_rows_kernel(RowsArgs a,
     {
         const float4 *src = reinterpret_cast<const float4 *>(a.slab + (size_t)w * s.total);
         float4 *dst = reinterpret_cast<float4 *>(smem + ll.slab);
-        for (int i = tid; i < slab_lds / 4; i += kRowsThreads) dst[i] = src[i];
+        if (!GW)
+            for (int i = tid; i < slab_lds / 4; i += kRowsThreads) dst[i] = src[i];
         const float *cs = a.state + (size_t)w * B * SW;
         for (int i = tid; i < B * SW; i += kRowsThreads) st[i] = a.t0 > 0 ? cs[i] : 0.0f;
         const float *cx = a.state + (size_t)G * B * SW;
@@ -576,19 +582,25 @@ hipError_t launch_pack_terms_input(const float *cond, int CD, int Bt, int b0, in
 
 // ------------------------------------------------------------------------ host launchers
 #define WRNN_ROWS_KERNELS                                                                           \
-    (const void *)fatchord_rows_kernel<true, 512, false>, (const void *)fatchord_rows_kernel<true, 0, false>,   \
-        (const void *)fatchord_rows_kernel<false, 512, false>, (const void *)fatchord_rows_kernel<false, 0, false>, \
-        (const void *)fatchord_rows_kernel<true, 0, true>, (const void *)fatchord_rows_kernel<false, 0, true>
+    (const void *)fatchord_rows_kernel<true, 512, false, false>, (const void *)fatchord_rows_kernel<true, 0, false, false>,   \
+        (const void *)fatchord_rows_kernel<false, 512, false, false>,                                           \
+        (const void *)fatchord_rows_kernel<false, 0, false, false>, (const void *)fatchord_rows_kernel<true, 0, true, false>,  \
+        (const void *)fatchord_rows_kernel<false, 0, true, false>, (const void *)fatchord_rows_kernel<true, 0, false, true>,   \
+        (const void *)fatchord_rows_kernel<false, 0, false, true>
 
 static const void *pick_rows_kernel(const RowsArgs &a) {
     const bool sparse = a.s.nbmax > 0;
     const bool d512 = a.R == 512 && a.F == 512 && !sparse;
+    if (a.gw) return a.mol ? (const void *)fatchord_rows_kernel<true, 0, false, true>
+                           : (const void *)fatchord_rows_kernel<false, 0, false, true>;
     if (a.mol) {
-        if (sparse) return (const void *)fatchord_rows_kernel<true, 0, true>;
-        return d512 ? (const void *)fatchord_rows_kernel<true, 512, false> : (const void *)fatchord_rows_kernel<true, 0, false>;
+        if (sparse) return (const void *)fatchord_rows_kernel<true, 0, true, false>;
+        return d512 ? (const void *)fatchord_rows_kernel<true, 512, false, false>
+                    : (const void *)fatchord_rows_kernel<true, 0, false, false>;
     }
-    if (sparse) return (const void *)fatchord_rows_kernel<false, 0, true>;
-    return d512 ? (const void *)fatchord_rows_kernel<false, 512, false> : (const void *)fatchord_rows_kernel<false, 0, false>;
+    if (sparse) return (const void *)fatchord_rows_kernel<false, 0, true, false>;
+    return d512 ? (const void *)fatchord_rows_kernel<false, 512, false, false>
+                : (const void *)fatchord_rows_kernel<false, 0, false, false>;
 }
 
 // one row group (g1 == nullptr) or two (workgroups [G, 2G) run group 1) in one launch
