@@ -51,9 +51,9 @@ hipError_t xcd_occupancy(int *blocks_per_cu);
 hipError_t launch_xcds(const XcdsArgs &a, hipStream_t st);
 hipError_t prepare_xcds_kernel(int max_lds_bytes);
 hipError_t xcds_occupancy(int *blocks_per_cu);
-hipError_t launch_xcdm(const XcdmArgs &a, int nq, hipStream_t st);
+hipError_t launch_xcdm(const XcdmArgs &a, int nq, bool raw, hipStream_t st);
 hipError_t prepare_xcdm_kernel(int max_lds_bytes);
-hipError_t xcdm_max_quads(int max_lds_bytes, int *nq_max);
+hipError_t xcdm_max_quads(int max_lds_bytes, bool raw, int *nq_max);
 hipError_t launch_philox_fill(float *out, unsigned long long seed, long long row0, int nb, int t0, int Lc, int K, int mol,
                               hipStream_t st);
 hipError_t launch_dx(const DxArgs &a, hipStream_t st);
@@ -1106,8 +1106,10 @@ void make_xcdm_slab(wrnn_ctx &h) {
     int o = 0;
     auto take = [&](int n) { int at = o; o += round4(n); return at; };
     XcdmSlab &x = h.xms;
+    const bool raw = h.cfg.mode == WRNN_MODE_RAW;
     x.a = take(kMWaves * kMSets * kMJ * 64);
-    x.w3 = take(32 * 16);
+    x.a3 = take(raw ? kMWaves * kMJ * 64 : 0);
+    x.w3 = take(raw ? 0 : 32 * 16);
     x.cst = take(kMCst);
     x.total = o;
 }
@@ -1137,8 +1139,16 @@ void pack_xcdm_slab(const wrnn_ctx &h, std::vector<float> &slab) {
                         out[x.a + (((size_t)w * kMSets + s) * kMJ + j) * 64 + l] =
                             set_row(s, c, 4 * g + j4)[kMK * w + kMJ * sp + j];
                     }
-        for (int jj = 0; jj < NC; ++jj)
-            for (int r = 0; r < 16; ++r) out[x.w3 + jj * 16 + r] = W("fc3.weight")[(size_t)jj * F + 16 * c + r];
+        if (h.cfg.mode == WRNN_MODE_RAW) {   // fc3 rows of the own classes 16c + r, [wave][k-chunk][lane][4]
+            for (int w = 0; w < kMWaves; ++w)
+                for (int j = 0; j < kMJ; ++j)
+                    for (int l = 0; l < 64; ++l)
+                        out[x.a3 + ((size_t)(w * (kMJ / 4) + j / 4) * 64 + l) * 4 + (j & 3)] =
+                            W("fc3.weight")[(size_t)(16 * c + (l & 15)) * F + kMK * w + kMJ * (l >> 4) + j];
+        } else {
+            for (int jj = 0; jj < NC; ++jj)
+                for (int r = 0; r < 16; ++r) out[x.w3 + jj * 16 + r] = W("fc3.weight")[(size_t)jj * F + 16 * c + r];
+        }
         for (int u = 0; u < 16; ++u) {
             const int j = 16 * c + u;
             out[x.cst + MC_WI0 + u] = IW[(size_t)j * nin];
@@ -1152,7 +1162,10 @@ void pack_xcdm_slab(const wrnn_ctx &h, std::vector<float> &slab) {
                 out[x.cst + MC_BHH2 + i] = W("rnn2.bias_hh_l0")[src];
             }
         }
-        for (int jj = 0; jj < NC; ++jj) out[x.cst + MC_B3 + jj] = W("fc3.bias")[jj];
+        if (h.cfg.mode == WRNN_MODE_RAW)
+            for (int r = 0; r < 16; ++r) out[x.cst + MC_B3 + r] = W("fc3.bias")[16 * c + r];
+        else
+            for (int jj = 0; jj < NC; ++jj) out[x.cst + MC_B3 + jj] = W("fc3.bias")[jj];
     }
 }
 
@@ -1734,8 +1747,10 @@ int generate_xcds(wrnn_t *h, const float *cond, int B, int L, const float *noise
 // r on XCD r % 8, its row r / 8 there), time chunks sized so terms + GEMM input stay within
 // WRNN_TERMS_MB (default 8192 MiB); the recurrent state is carried per workgroup in d_xmstate.
 int generate_xcdm(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed, int64_t row_offset,
-                  float *out, hipStream_t st) {
+                  float *out, int32_t *labels, hipStream_t st) {
     const int N = kXcdWgs * kXTerms;
+    const bool raw = h->cfg.mode == WRNN_MODE_RAW;
+    const int NK = raw ? kMRawNC : 11;              // draws per row-step: Exp(1) per class / MoL uniforms
     if (!h->blas && rocblas_create_handle(&h->blas) != rocblas_status_success)
         return fail(h, WRNN_EHIP, "rocblas_create_handle failed");
     if (rocblas_set_stream(h->blas, st) != rocblas_status_success) return fail(h, WRNN_EHIP, "rocblas_set_stream failed");
@@ -1750,7 +1765,7 @@ int generate_xcdm(wrnn_t *h, const float *cond, int B, int L, const float *noise
     // diagnostics: WRNN_DEBUG_STAMPS=1 WRNN_DEBUG_FILE=<path>: per-wave phase stamps of the first
     // launch ([256 · kMWaves][kMDbgSteps][kMStamps] shader clocks, int32 header)
     const char *dbg_env = std::getenv("WRNN_DEBUG_STAMPS");
-    const int dbg_steps = (dbg_env && std::atoi(dbg_env) > 0 && L >= kMDbgSkip + kMDbgSteps) ? kMDbgSteps : 0;
+    const int dbg_steps = (!raw && dbg_env && std::atoi(dbg_env) > 0 && L >= kMDbgSkip + kMDbgSteps) ? kMDbgSteps : 0;
     const size_t dbg_n = (size_t)kXcds * kXcdWgs * kMWaves * dbg_steps * kMStamps;
     unsigned *d_dbg = nullptr;
     if (dbg_steps > 0) {
@@ -1760,9 +1775,9 @@ int generate_xcdm(wrnn_t *h, const float *cond, int B, int L, const float *noise
     for (int b0 = 0; b0 < B; b0 += rows_max) {
         const int nb = std::min(rows_max, B - b0);
         const int nq = (((nb + kXcds - 1) / kXcds) + 3) / 4;   // quads on the fullest XCD
-        const int Lc_max = (int)std::max(1.0, std::min((double)L, budget / ((double)nb * (N + h->KXc))));
+        const int Lc_max = (int)std::max(1.0, std::min((double)L, budget / ((double)nb * (N + h->KXc + (noise ? 0 : NK)))));
         if (grow(h, h->d_X, h->X_cap, (size_t)Lc_max * nb * h->KXc) || grow(h, h->d_T, h->T_cap, (size_t)Lc_max * nb * N) ||
-            (!noise && grow(h, h->d_xmnoise, h->xmnoise_cap, (size_t)Lc_max * nb * 11)))
+            (!noise && grow(h, h->d_xmnoise, h->xmnoise_cap, (size_t)Lc_max * nb * NK)))
             return WRNN_EHIP;
         HIP_TRY(h, hipMemsetAsync(h->d_xmxg, 0, xg_words * 8, st));   // tags restart at 1
         for (int t0 = 0; t0 < L; t0 += Lc_max) {
@@ -1777,19 +1792,20 @@ int generate_xcdm(wrnn_t *h, const float *cond, int B, int L, const float *noise
             XcdmArgs a{};
             a.slab = h->d_xmslab;
             a.terms = h->d_T;
-            if (noise) {   // injected [L][B][11]
+            if (noise) {   // injected [L][B][NK]
                 a.noise = noise;
                 a.nz_t0 = 0;
                 a.nz_ts = B;
                 a.nz_b0 = b0;
-            } else {       // Philox, drawn for this chunk by a small kernel first ([Lc][nb][11])
-                HIP_TRY(h, launch_philox_fill(h->d_xmnoise, seed, row_offset + b0, nb, t0, Lc, 11, 1, st));
+            } else {       // Philox, drawn for this chunk by a small kernel first ([Lc][nb][NK])
+                HIP_TRY(h, launch_philox_fill(h->d_xmnoise, seed, row_offset + b0, nb, t0, Lc, NK, raw ? 0 : 1, st));
                 a.noise = h->d_xmnoise;
                 a.nz_t0 = t0;
                 a.nz_ts = nb;
                 a.nz_b0 = 0;
             }
             a.out = out;
+            a.labels = labels;
             a.state = h->d_xmstate;
             a.xg = h->d_xmxg;
             a.members = h->d_members;
@@ -1805,7 +1821,7 @@ int generate_xcdm(wrnn_t *h, const float *cond, int B, int L, const float *noise
             a.nb = nb;
             a.s = h->xms;
             a.dbg = (b0 == 0 && t0 == 0 && Lc >= kMDbgSkip + kMDbgSteps) ? d_dbg : nullptr;
-            HIP_TRY(h, launch_xcdm(a, nq, st));
+            HIP_TRY(h, launch_xcdm(a, nq, raw, st));
         }
     }
     if (d_dbg) {
@@ -2058,9 +2074,17 @@ int wrnn_create(const wrnn_config *cfg, int device, wrnn_t **out) {
         if (h->xcd_ok) {
             make_xcdm_slab(*h);
             HIP_TRY(h, prepare_xcdm_kernel(h->max_lds));
-            HIP_TRY(h, xcdm_max_quads(h->max_lds, &h->xcdm_nq));
+            HIP_TRY(h, xcdm_max_quads(h->max_lds, false, &h->xcdm_nq));
             h->xcdm_ok = h->xcdm_nq >= 1;
         }
+    }
+    // RAW 9-bit, rnn / fc 512: the many-row XCD-resident kernel with the softmax head (every row count)
+    if (!mol && c.grid <= 0 && R == 512 && F == 512 && c.aux_dims == 32 && c.n_classes == kMRawNC &&
+        h->num_cus == kXcds * kXcdWgs) {
+        make_xcdm_slab(*h);
+        HIP_TRY(h, prepare_xcdm_kernel(h->max_lds));
+        HIP_TRY(h, xcdm_max_quads(h->max_lds, true, &h->xcdm_nq));
+        h->xcdm_ok = h->xcdm_nq >= 1;
     }
     // MoL rnn 896 / fc 512: the XCD-resident block-sparse kernel, if the weights turn out
     // block-sparse (decided at wrnn_set_weights)
@@ -2194,9 +2218,10 @@ int wrnn_set_weights(wrnn_t *h, const wrnn_tensor *tensors, int n) {
             HIP_TRY(h, hipMemcpy(*pr.first, pr.second->data(), pr.second->size() * 4, hipMemcpyHostToDevice));
         }
     }
-    if (h->xcd_ok) {
+    if (h->xcd_ok || h->xcdm_ok) {   // (the many-row kernel shares the terms GEMM; RAW has no xcd slab)
         std::vector<float> slab, Wt;
-        pack_xcd_slab(*h, slab);
+        if (h->xcd_ok) pack_xcd_slab(*h, slab);
+        else slab.assign(4, 0.0f);
         pack_xcd_terms_weights(*h, Wt);
         for (auto pr : {std::make_pair(&h->d_xslab, &slab), std::make_pair(&h->d_xWt, &Wt)}) {
             if (*pr.first) HIP_TRY(h, hipFree(*pr.first));
@@ -2258,7 +2283,9 @@ int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise
     // MoL rnn / fc 512 up to kXcdDefaultRows rows: the XCD-resident kernel (8 rows per launch;
     // beyond that the multi-row kernel's throughput wins)
     // MoL rnn / fc 512, more than kXcdmMinRows rows: the many-row XCD-resident kernel (MFMA)
-    const bool xcdm = h->xcdm_ok && (pe == "xcdm" || (pe.empty() && B >= kXcdmMinRows));
+    // (RAW 512-class: the many-row kernel for every row count — it is the only XCD-resident RAW one)
+    const bool xcdm = h->xcdm_ok &&
+                      (pe == "xcdm" || (pe.empty() && (B >= kXcdmMinRows || h->cfg.mode == WRNN_MODE_RAW)));
     const bool xcd = !xcdm && h->xcd_ok && (pe == "xcd" || (pe.empty() && B <= kXcdDefaultRows));
     // MoL rnn 896 with block-sparse GRU weights likewise: the XCD-resident sparse kernel
     const bool xcds = !xcd && h->xcds_ok && (pe == "xcd" || (pe.empty() && B <= kXcdDefaultRows));
@@ -2270,7 +2297,7 @@ int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise
     h->last_path = dx ? 8 : h->dm ? (h->dm_gw ? 10 : 3) : xcdm ? 7 : xcd ? 5 : xcds ? 6 : split ? 4 : rows ? (h->rows_gw ? 9 : 2) : 1;
     const int rc = dx       ? generate_dx(h, B, L, noise, seed, row_offset, out, labels, st)
                    : h->dm  ? generate_dm(h, B, L, noise, seed, row_offset, out, labels, st)
-                   : xcdm  ? generate_xcdm(h, cond, B, L, noise, seed, row_offset, out, st)
+                   : xcdm  ? generate_xcdm(h, cond, B, L, noise, seed, row_offset, out, labels, st)
                    : xcd   ? generate_xcd(h, cond, B, L, noise, seed, row_offset, out, st)
                    : xcds  ? generate_xcds(h, cond, B, L, noise, seed, row_offset, out, st)
                    : split ? generate_split(h, cond, B, L, noise, seed, row_offset, out, st)

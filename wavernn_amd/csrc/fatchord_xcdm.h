@@ -4,7 +4,9 @@
 // (v_mfma_f32_4x4x1_16b_f32: 16 blocks of 4 weight rows × 4 rows of the batch), every hand-off
 // kept in the XCD's L2.
 //
-// Shapes: rnn 512, fc 512, aux 32, MoL (30 classes) — BASELINE configs 2 (fold-batched) and 3.
+// Shapes: rnn 512, fc 512, aux 32, MoL (30 classes) — BASELINE configs 2 (fold-batched) and 3 —
+// or RAW 9-bit (512 classes, fatchord_version.py:231-237): fc3 is then a twelfth 16-row set (the
+// own classes 16c..16c+15, A operands in LDS), f2 a full hop vector and the logits a sixth one.
 #pragma once
 #include <stdint.h>
 
@@ -35,20 +37,24 @@ enum MSet { MS_IH2 = 0, MS_FC1 = 3, MS_FC2 = 4, MS_HH2 = 5, MS_HH1 = 8, kMSets =
 // Hand-off vectors of one XCD.  Row n (0..15) of the XCD = launch row k + 8n.  Granules
 // {tag = step + 1, value}: H1 / Y / H2 / F1 at n·512 + j (unit or fc row j); F2 (partial logits
 // of producer c) at (n·32 + c)·32 + j, j < 32 (30, 31 zero); X (two-level sampler) at n.
-enum MHop { MH_H1 = 0, MH_Y = 1, MH_H2 = 2, MH_F1 = 3, MH_F2 = 4, MH_X = 5, kMHops = 6 };
+// RAW: F2 holds the f2 vectors (n·512 + j) and LG the logits (n·512 + class).
+enum MHop { MH_H1 = 0, MH_Y = 1, MH_H2 = 2, MH_F1 = 3, MH_F2 = 4, MH_X = 5, MH_LG = 6, kMHops = 7 };
 constexpr long long kMVec = (long long)kMRowsXcd * 512;
-constexpr long long kMF2 = (long long)kMRowsXcd * kXcdWgs * 32;
-constexpr long long kMHopOff[kMHops] = {0, kMVec, 2 * kMVec, 3 * kMVec, 4 * kMVec, 4 * kMVec + kMF2};
-constexpr long long kMXcdStride = 4 * kMVec + kMF2 + 64;   // granules per XCD
+constexpr long long kMF2 = (long long)kMRowsXcd * kXcdWgs * 32;   // >= kMVec
+constexpr long long kMHopOff[kMHops] = {0, kMVec, 2 * kMVec, 3 * kMVec, 4 * kMVec, 4 * kMVec + kMF2,
+                                        4 * kMVec + kMF2 + 64};
+constexpr long long kMXcdStride = 5 * kMVec + kMF2 + 64;   // granules per XCD
+constexpr int kMRawNC = 512;        // RAW classes (bits = 9)
 
 // Per-workgroup constants (LDS), gate-major: index q·16 + u
 enum MCst { MC_Q1 = 0, MC_Q2 = 48, MC_BIH1 = 96, MC_BHH1 = 144, MC_BIH2 = 192, MC_BHH2 = 240, MC_WI0 = 288,
             MC_B3 = 304, kMCst = 336 };
 //   q1 / q2: W_ih1 / W_ih2[:, :R] · W_I[:, 0] (the x column of the I layer folded into the gates),
-//   biases of both GRUs, W_I[:, 0] of the own units, b3 (padded to 32)
+//   biases of both GRUs, W_I[:, 0] of the own units, b3 (padded to 32; RAW: of the own classes)
 
 struct XcdmSlab {
     int a;       // [kMWaves][kMSets][16][64]   MFMA A operands
+    int a3;      // RAW: [kMWaves][kMJ / 4][64][4] fc3 A operands (own classes), copied to LDS
     int w3;      // [32][16]                     W3[j][16c + r] (j >= 30: 0)
     int cst;     // [kMCst]
     int total;
@@ -71,6 +77,7 @@ struct XcdmArgs {
     long long nz_ts;
     int nz_t0, nz_b0;
     float *out;                   // [Bt][L]
+    int32_t *labels;              // RAW: [Bt][L] class labels, or nullptr
     float *state;                 // [kXcds][kXcdWgs][kMStateW]
     unsigned long long *xg;       // [kXcds][kMXcdStride] granules
     int *members;                 // [kXcds] arrival counters (zeroed before the launch)
@@ -85,7 +92,7 @@ struct XcdmArgs {
 constexpr int kMStamps = 24, kMDbgSteps = 48, kMDbgSkip = 16;
 
 struct XcdmLds {
-    int stg_h1, stg, pbig, phh1, pfc1, pfc2, gh1, gh2, f2, ring, nz, cst, w3, xs, misc, dbg, total;
+    int stg_h1, stg, pbig, phh1, pfc1, pfc2, gh1, gh2, f2, ring, nz, cst, w3, a3, xs, misc, dbg, total;
 };
 
 // staging of a polled vector slice, per wave: [quad][4 rows][64], value k of row j4 at
@@ -116,7 +123,7 @@ __host__ __device__ constexpr int xcdm_pset(int nq) {
     return xcdm_big(nq) ? 16 * 4 * nq * kMWaves : kMWaves * 16 * xcdm_pstride_row(nq);
 }
 
-__host__ __device__ inline XcdmLds xcdm_lds_layout(int nq, bool dbg = false) {
+__host__ __device__ inline XcdmLds xcdm_lds_layout(int nq, bool dbg = false, bool raw = false) {
     const int nr = 4 * nq, nq_stg = xcdm_big(nq) ? kMQuadMax : nq;
     XcdmLds l;
     int o = 0;
@@ -128,11 +135,12 @@ __host__ __device__ inline XcdmLds xcdm_lds_layout(int nq, bool dbg = false) {
     l.pfc2 = o;   o += xcdm_pset(nq);
     l.gh1 = o;    o += 3 * 16 * nr;                    // Σ W_hh1·h1 (next step's GRU1)
     l.gh2 = o;    o += 3 * 16 * nr;                    // Σ W_hh2·h2 (next step's GRU2)
-    l.f2 = o;     o += 16 * nr;
+    l.f2 = o;     o += raw ? 0 : 16 * nr;              // MoL: f2 of the own rows (fc3 partials)
     l.ring = o;   o += 2 * nr * kMRing;                // terms of steps t, t + 1 (by parity)
-    l.nz = o;     o += 2 * nr * kMNoise;
+    l.nz = o;     o += raw ? 0 : 2 * nr * kMNoise;
     l.cst = o;    o += kMCst;
-    l.w3 = o;     o += 32 * 16;
+    l.w3 = o;     o += raw ? 0 : 32 * 16;
+    l.a3 = o;     o += raw ? kMWaves * kMJ * 64 : 0;   // RAW: fc3 A operands (LDS-resident)
     l.xs = o;     o += 16;
     l.misc = o;   o += 8;                              // [0] abort flag, [1] member index
     l.dbg = o;    o += dbg ? kMDbgSteps * kMWaves * kMStamps : 0;

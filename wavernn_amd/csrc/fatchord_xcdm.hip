@@ -196,12 +196,16 @@ __device__ __forceinline__ float mpart(const float *P, int i, int n) {
 // (quad, set) (column j → chain j % NC) so that ≥ 8 independent chains interleave — the
 // dependent-accumulator latency of v_mfma_f32_4x4x1_16b_f32 is ≈ 52 cycles for an 8-cycle issue
 // (tools/mfma4_bench.hip), and one wave per SIMD has no partner to hide it.
-template <int NQ, int S0, int NS, int NC, typename Hook = MPollNone>
+// kLdsA (RAW fc3, NS = 1): the set's A operands come from LDS ([kMJ / 4][64 lanes][4], AL = the
+// wave's image), read a k-chunk ahead like B.
+template <int NQ, int S0, int NS, int NC, typename Hook = MPollNone, bool kLdsA = false>
 __device__ __forceinline__ void mlayer(const float (&A)[kMSets][kMJ], const float *stg, float *P, int lane, int wave,
-                                       Hook &&hook = Hook{}) {
-    constexpr bool kAgpr = S0 < MS_HH1;
+                                       Hook &&hook = Hook{}, const float *AL = nullptr) {
+    constexpr bool kAgpr = !kLdsA && S0 < MS_HH1;
     const int j4 = lane & 3, sp = lane >> 4;
     f4v acc[NQ][NS][NC];
+    f4v al[2];
+    if constexpr (kLdsA) al[0] = lds4(AL + lane * 4);
     // B operands double-buffered: chunk jc + 1's LDS reads are in flight during chunk jc's MFMAs
     // (the asm MFMAs are volatile, so hipcc would not hoist a read above them by itself)
     f4v b[2][NQ];
@@ -213,6 +217,7 @@ __device__ __forceinline__ void mlayer(const float (&A)[kMSets][kMJ], const floa
         if (jc + 1 < kMJ / 4) {
 #pragma unroll
             for (int q = 0; q < NQ; ++q) b[(jc + 1) & 1][q] = lds4(stg + q * kMStg + mstg_at(j4, kMJ * sp + 4 * (jc + 1)));
+            if constexpr (kLdsA) al[(jc + 1) & 1] = lds4(AL + ((jc + 1) * 64 + lane) * 4);
         }
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
@@ -221,8 +226,11 @@ __device__ __forceinline__ void mlayer(const float (&A)[kMSets][kMJ], const floa
             for (int q = 0; q < NQ; ++q)
 #pragma unroll
                 for (int s = 0; s < NS; ++s) {
-                    if (j < NC) mfma_first<kAgpr>(acc[q][s][j % NC], A[S0 + s][j], b[jc & 1][q][jj]);
-                    else mfma_acc<kAgpr>(acc[q][s][j % NC], A[S0 + s][j], b[jc & 1][q][jj]);
+                    float av;
+                    if constexpr (kLdsA) av = al[jc & 1][jj];
+                    else av = A[S0 + s][j];
+                    if (j < NC) mfma_first<kAgpr>(acc[q][s][j % NC], av, b[jc & 1][q][jj]);
+                    else mfma_acc<kAgpr>(acc[q][s][j % NC], av, b[jc & 1][q][jj]);
                 }
         }
     }
@@ -241,26 +249,33 @@ __device__ __forceinline__ void mlayer(const float (&A)[kMSets][kMJ], const floa
 // columns kMK·w + kMJ·g + i of MFMA i (the A operands are the 4x4x1 form's, lane for lane: row
 // l & 15, column kMK·w + kMJ·(l >> 4) + i); the K reduction happens inside the MFMA, so lane l
 // ends with rows 4(l >> 4) + r, r = 0..3, of batch row n, summed over the wave's whole window.
-template <int NQ, int S0, int NS, int NC, typename Hook = MPollNone>
+template <int NQ, int S0, int NS, int NC, typename Hook = MPollNone, bool kLdsA = false>
 __device__ __forceinline__ void mlayer16(const float (&A)[kMSets][kMJ], const float *stg, float *P, int lane, int wave,
-                                         Hook &&hook = Hook{}) {
-    constexpr bool kAgpr = S0 < MS_HH1;
+                                         Hook &&hook = Hook{}, const float *AL = nullptr) {
+    constexpr bool kAgpr = !kLdsA && S0 < MS_HH1;
     constexpr int NR = 4 * NQ;
     const int n = lane & 15, g = lane >> 4;
     f4v acc[NS][NC];
-    f4v b[2];
+    f4v b[2], al[2];
     b[0] = lds4(stg + mstg16_at(n, kMJ * g));
+    if constexpr (kLdsA) al[0] = lds4(AL + lane * 4);
 #pragma unroll
     for (int ic = 0; ic < kMJ / 4; ++ic) {
         hook.step(ic);
-        if (ic + 1 < kMJ / 4) b[(ic + 1) & 1] = lds4(stg + mstg16_at(n, kMJ * g + 4 * (ic + 1)));
+        if (ic + 1 < kMJ / 4) {
+            b[(ic + 1) & 1] = lds4(stg + mstg16_at(n, kMJ * g + 4 * (ic + 1)));
+            if constexpr (kLdsA) al[(ic + 1) & 1] = lds4(AL + ((ic + 1) * 64 + lane) * 4);
+        }
 #pragma unroll
         for (int ii = 0; ii < 4; ++ii) {
             const int i = 4 * ic + ii;
 #pragma unroll
             for (int s = 0; s < NS; ++s) {
-                if (i < NC) mfma16_first<kAgpr>(acc[s][i % NC], A[S0 + s][i], b[ic & 1][ii]);
-                else mfma16_acc<kAgpr>(acc[s][i % NC], A[S0 + s][i], b[ic & 1][ii]);
+                float av;
+                if constexpr (kLdsA) av = al[ic & 1][ii];
+                else av = A[S0 + s][i];
+                if (i < NC) mfma16_first<kAgpr>(acc[s][i % NC], av, b[ic & 1][ii]);
+                else mfma16_acc<kAgpr>(acc[s][i % NC], av, b[ic & 1][ii]);
             }
         }
     }
@@ -299,6 +314,13 @@ __device__ __forceinline__ void mlayer_any(const float (&A)[kMSets][kMJ], const 
     // (16x16x4: ≥ 3 sets interleaved already cover its ≈ 40-cycle dependent latency)
     if constexpr (xcdm_big(NQ)) mlayer16<NQ, S0, NS, 2>(A, stg, P, lane, wave, hook);
     else mlayer<NQ, S0, NS, MChains<NQ, NS>::v>(A, stg, P, lane, wave, hook);
+}
+// one set whose A operands are in LDS (RAW fc3); partials in the set-0 slot of P
+template <int NQ>
+__device__ __forceinline__ void mlayer_lds(const float (&A)[kMSets][kMJ], const float *AL, const float *stg, float *P,
+                                           int lane, int wave) {
+    if constexpr (xcdm_big(NQ)) mlayer16<NQ, 0, 1, 2, MPollNone, true>(A, stg, P, lane, wave, MPollNone{}, AL);
+    else mlayer<NQ, 0, 1, MChains<NQ, 1>::v, MPollNone, true>(A, stg, P, lane, wave, MPollNone{}, AL);
 }
 
 // quads polled beside an off-critical layer (none above one quad: the registers are not there),
@@ -376,6 +398,72 @@ __device__ __forceinline__ float msample(const unsigned long long *f2, int n, ui
     return mol_sample_pairs(la, lb, ua, ub, u10, jp);
 }
 
+// RAW sample of XCD row n by one wave (fatchord_version.py:231-237): the row's 512 logits (32
+// producers × 16 own classes, published as granules n·512 + class) polled as pairs — lane l holds
+// classes 2(l + 64i) + {0, 1}, i < 4 — then softmax → Categorical renormalisation → argmax(p / q)
+// with the row's Exp(1) draws q (the fp32 operations of wrnn_device.h:raw_sample; first index on
+// ties).  Returns the label, wave-uniform.
+__device__ __forceinline__ int rsample(const unsigned long long *lg, int n, uint32_t tag, const f2v (&q)[4], int *ctl,
+                                       long long timeout, int step, int *lds_abort, int lane) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const __amdgpu_buffer_rsrc_t rf = hop_rsrc(lg);
+    const int goff = (n * kMRawNC + 2 * lane) * 8;
+    const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
+    unsigned spins = 0;
+    float e[8];
+    for (;;) {
+        u4v v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = ld16_sc1(rf, goff + i * 128 * 8);
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ok &= (v[i].y == tag) & (v[i].w == tag);
+        if (__ballot(!ok) == 0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                e[2 * i] = __uint_as_float(v[i].x);
+                e[2 * i + 1] = __uint_as_float(v[i].z);
+            }
+            break;
+        }
+        if ((++spins & 63u) == 0) {
+            const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - c0) > timeout;
+            const bool other = __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+            if (late || other) {
+                if (late) record_abort(ctl, -4, step, MH_LG, blockIdx.x);
+                *lds_abort = 1;
+                return 0;
+            }
+        }
+    }
+    float m = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m = fmaxf(m, e[k]);
+    m = wave_max(m);
+    float s1 = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        e[k] = expf(e[k] - m);
+        s1 += e[k];
+    }
+    s1 = wave_sum(s1);
+    float s2 = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        e[k] = e[k] / s1;
+        s2 += e[k];
+    }
+    s2 = wave_sum(s2);
+    float bv = -INFINITY;
+    int bi = 0x7FFFFFFF;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        am_merge(bv, bi, (e[2 * i] / s2) / q[i].x, 2 * (lane + 64 * i));
+        am_merge(bv, bi, (e[2 * i + 1] / s2) / q[i].y, 2 * (lane + 64 * i) + 1);
+    }
+    return wave_argmax(bv, bi);
+}
+
 // diagnostics (template kDbg, WRNN_DEBUG_STAMPS=1): lane 0 of every wave stamps the shader clock
 // at the phase boundaries below into LDS for kMDbgSteps steps from t0 + kMDbgSkip (global stores
 // would sit in vmcnt ahead of the polls); copied out after the loop; tools/stamps_xcdm.py reads them
@@ -386,19 +474,22 @@ __device__ __forceinline__ float msample(const unsigned long long *f2, int n, ui
                 (unsigned)__builtin_amdgcn_s_memtime();                                                      \
     } while (0)
 
-template <int NQ, bool kDbg>
+// kRaw: the RAW (9-bit softmax) head — f2 published as a hop vector, fc3 (own 16 classes, A
+// operands in LDS) on the gathered f2 slice, the logits a sixth hop, rsample instead of msample;
+// the Exp(1) draws always come from `noise` (Philox pre-filled by the host).
+template <int NQ, bool kDbg, bool kRaw>
 __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm_kernel(XcdmArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int NR = 4 * NQ;
     constexpr bool kTwoLevel = NQ >= 2;
     constexpr int N = kXcdWgs * kXTerms;
-    const XcdmLds ll = xcdm_lds_layout(NQ, kDbg);
+    const XcdmLds ll = xcdm_lds_layout(NQ, kDbg, kRaw);
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     constexpr int kStgQ = xcdm_big(NQ) ? kMQuadMax : NQ;   // staged quads per wave
     float *stg_h1 = smem + ll.stg_h1 + wave * kStgQ * kMStg, *stg = smem + ll.stg + wave * kStgQ * kMStg;
     float *pbig = smem + ll.pbig, *phh1 = smem + ll.phh1, *pfc1 = smem + ll.pfc1, *pfc2 = smem + ll.pfc2;
     float *gh1 = smem + ll.gh1, *gh2 = smem + ll.gh2, *f2s = smem + ll.f2, *ring = smem + ll.ring, *nzr = smem + ll.nz;
-    float *cst = smem + ll.cst, *w3s = smem + ll.w3, *xs = smem + ll.xs;
+    float *cst = smem + ll.cst, *w3s = smem + ll.w3, *xs = smem + ll.xs, *a3s = smem + ll.a3;
     int *misc = reinterpret_cast<int *>(smem + ll.misc);
     int *abort_flag = misc;
     unsigned *dbgs = reinterpret_cast<unsigned *>(smem + ll.dbg);
@@ -458,9 +549,13 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
 
     // ---- prologue: constants, zeroed accumulators / ring, state, the terms of step t0
     for (int i = tid; i < kMCst; i += kMThreads) cst[i] = S[a.s.cst + i];
-    for (int i = tid; i < 32 * 16; i += kMThreads) w3s[i] = S[a.s.w3 + i];
+    if constexpr (kRaw) {
+        for (int i = tid; i < kMWaves * kMJ * 64; i += kMThreads) a3s[i] = S[a.s.a3 + i];
+    } else {
+        for (int i = tid; i < 32 * 16; i += kMThreads) w3s[i] = S[a.s.w3 + i];
+        for (int i = tid; i < 2 * NR * kMNoise; i += kMThreads) nzr[i] = 0.0f;
+    }
     for (int i = tid; i < 2 * NR * kMRing; i += kMThreads) ring[i] = 0.0f;
-    for (int i = tid; i < 2 * NR * kMNoise; i += kMThreads) nzr[i] = 0.0f;
     for (int i = tid; i < 3 * 16 * NR; i += kMThreads) gh1[i] = gh2[i] = 0.0f;
     if (tid < 16) xs[tid] = 0.0f;
     __syncthreads();
@@ -483,10 +578,11 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         const int n = i / kRingF4, f = i - n * kRingF4;
         *reinterpret_cast<f4v *>(ring_at(a.t0) + n * kMRing + 4 * f) = *reinterpret_cast<const f4v *>(TERMS(a.t0, n) + 4 * f);
     }
-    for (int i = tid; i < 11 * RX; i += kMThreads) {
-        const int n = i / 11, kk = i - 11 * n;
-        nz_at(a.t0)[n * kMNoise + kk] = mol_noise_term(noise_uu(a.t0, n, kk), kk);
-    }
+    if constexpr (!kRaw)
+        for (int i = tid; i < 11 * RX; i += kMThreads) {
+            const int n = i / 11, kk = i - 11 * n;
+            nz_at(a.t0)[n * kMNoise + kk] = mol_noise_term(noise_uu(a.t0, n, kk), kk);
+        }
     __syncthreads();
 
     for (int t = a.t0; t < t_end; ++t) {
@@ -610,9 +706,21 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
                     rl[i] = *reinterpret_cast<const f4v *>(TERMS(t + 1, n) + 4 * f);
                 }
             }
-            if (lt < 11 * RX) {
+            if (!kRaw && lt < 11 * RX) {
                 const int n = lt / 11, kk = lt - 11 * n;
                 uu = noise_uu(t + 1, n, kk);
+            }
+        }
+        // RAW: the Exp(1) draws of the row this wave samples (step t), pairs of classes
+        // 2(lane + 64i) + {0, 1} — issued here, landed by the logits poll
+        f2v qv[4];
+        const int sn = kTwoLevel ? c : wave;                          // sampled row
+        const bool smp = kTwoLevel ? (wave == 0 && c < RX) : (wave < RX);
+        if constexpr (kRaw) {
+            if (smp) {
+                const float *qr = a.noise + ((size_t)(t - a.nz_t0) * a.nz_ts + a.nz_b0 + k + kXcds * sn) * kMRawNC;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) qv[i] = *reinterpret_cast<const f2v *>(qr + 2 * (lane + 64 * i));
             }
         }
         auto ring_store = [&]() {
@@ -626,7 +734,7 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
                         *reinterpret_cast<f4v *>(rn + n * kMRing + 4 * f) = rl[i];
                     }
                 }
-                if (lt < 11 * RX) {
+                if (!kRaw && lt < 11 * RX) {
                     const int n = lt / 11, kk = lt - 11 * n;
                     nz_at(t + 1)[n * kMNoise + kk] = mol_noise_term(uu, kk);
                 }
@@ -635,7 +743,8 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         // ---- I: fc2 epilogue → f2 (LDS); Σ W_hh2·h2 for the next GRU2
         if (gru) {
             const float f = mpart<NQ>(pfc2, gu, gn) + rg[gn * kMRing + XT_V2 + gu];
-            f2s[gu * NR + gn] = f > 0.0f ? f : 0.0f;
+            if constexpr (kRaw) xpub(xg + kMHopOff[MH_F2] + gn * 512 + 16 * c + gu, tag, f > 0.0f ? f : 0.0f);
+            else f2s[gu * NR + gn] = f > 0.0f ? f : 0.0f;
             if (aux_w0 >= kMWaves) {
 #pragma unroll
                 for (int q = 0; q < 3; ++q) {
@@ -645,16 +754,26 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
             }
         }
         MST(16);
-        bar();
-        MST(17);
-        // fc3 (:223) partial logits of the own 16 f2 rows: logit fj of row fn
+        if constexpr (kRaw) {
+            // fc3 (:223) rows of the own 16 classes on the gathered f2 slice → logits [hop LG]
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            mgather<NQ>(xg + kMHopOff[MH_F2], stg, wave, tag, a.ctl, a.timeout_ticks, t, MH_F2, abort_flag, lane);
+            MST(17);
+            mlayer_lds<NQ>(A, a3s + wave * kMJ * 64, stg, pfc1, lane, wave);
+            bar();
+            if (gru) xpub(xg + kMHopOff[MH_LG] + gn * 512 + 16 * c + gu, tag, mpart<NQ>(pfc1, gu, gn) + cst[MC_B3 + gu]);
+        } else {
+            bar();
+            MST(17);
+            // fc3 (:223) partial logits of the own 16 f2 rows: logit fj of row fn
 #pragma unroll
-        for (int i = tid; i < 32 * NR; i += kMThreads) {
-            const int fj = i & 31, fn = i >> 5;
-            float p = 0.0f;
+            for (int i = tid; i < 32 * NR; i += kMThreads) {
+                const int fj = i & 31, fn = i >> 5;
+                float p = 0.0f;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) p = fmaf(w3s[fj * 16 + r], f2s[r * NR + fn], p);
-            xpub(xg + kMHopOff[MH_F2] + (fn * kXcdWgs + c) * 32 + fj, tag, p);
+                for (int r = 0; r < 16; ++r) p = fmaf(w3s[fj * 16 + r], f2s[r * NR + fn], p);
+                xpub(xg + kMHopOff[MH_F2] + (fn * kXcdWgs + c) * 32 + fj, tag, p);
+            }
         }
         MST(18);
         if (kTwoLevel || wave >= RX) ring_store();
@@ -667,12 +786,22 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
             }
         }
         MST(19);
-        // ---- J: sample (:225-229)
+        // ---- J: sample (:225-229; RAW :231-237) row n of this XCD, wave-uniform x
         const float *nz = nz_at(t);
+        auto sample_row = [&](int n) -> float {
+            if constexpr (kRaw) {
+                const int lab = rsample(xg + kMHopOff[MH_LG], n, tag, qv, a.ctl, a.timeout_ticks, t, abort_flag, lane);
+                if (lane == 0 && a.labels && (kTwoLevel || c == 0))
+                    a.labels[(size_t)(a.b0 + k + kXcds * n) * a.L + t] = lab;
+                return label_to_x(lab, kMRawNC);
+            } else {
+                return msample(xg + kMHopOff[MH_F2], n, tag, nz + n * kMNoise, cst, a.ctl, a.timeout_ticks, t, abort_flag,
+                               lane);
+            }
+        };
         if (!kTwoLevel) {
             if (wave < RX) {
-                const float xn = msample(xg + kMHopOff[MH_F2], wave, tag, nz + wave * kMNoise, cst, a.ctl, a.timeout_ticks,
-                                         t, abort_flag, lane);
+                const float xn = sample_row(wave);
                 if (lane == 0) {
                     xs[wave] = xn;
                     if (c == 0) a.out[(size_t)(a.b0 + k + kXcds * wave) * a.L + t] = xn;
@@ -680,8 +809,7 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
             }
         } else if (wave == 0) {
             if (c < RX) {   // this workgroup samples row c and publishes its x
-                const float xn = msample(xg + kMHopOff[MH_F2], c, tag, nz + c * kMNoise, cst, a.ctl, a.timeout_ticks, t,
-                                         abort_flag, lane);
+                const float xn = sample_row(c);
                 if (lane == 0) {
                     xpub(xg + kMHopOff[MH_X] + c, tag, xn);
                     a.out[(size_t)(a.b0 + k + kXcds * c) * a.L + t] = xn;
@@ -756,41 +884,46 @@ hipError_t launch_philox_fill(float *out, unsigned long long seed, long long row
     return hipGetLastError();
 }
 
-static const void *xcdm_kernel(int nq, bool dbg) {
-    static const void *k[2][kMQuadMax] = {
-        {(const void *)fatchord_xcdm_kernel<1, false>, (const void *)fatchord_xcdm_kernel<2, false>,
-         (const void *)fatchord_xcdm_kernel<3, false>, (const void *)fatchord_xcdm_kernel<4, false>},
-        {(const void *)fatchord_xcdm_kernel<1, true>, (const void *)fatchord_xcdm_kernel<2, true>,
-         (const void *)fatchord_xcdm_kernel<3, true>, (const void *)fatchord_xcdm_kernel<4, true>}};
-    return k[dbg ? 1 : 0][nq < 1 ? 0 : nq > kMQuadMax ? kMQuadMax - 1 : nq - 1];
+// RAW kernels have no stamp variant (the stamp buffer does not fit LDS beside the fc3 operands)
+static const void *xcdm_kernel(int nq, bool dbg, bool raw) {
+    static const void *k[3][kMQuadMax] = {
+        {(const void *)fatchord_xcdm_kernel<1, false, false>, (const void *)fatchord_xcdm_kernel<2, false, false>,
+         (const void *)fatchord_xcdm_kernel<3, false, false>, (const void *)fatchord_xcdm_kernel<4, false, false>},
+        {(const void *)fatchord_xcdm_kernel<1, true, false>, (const void *)fatchord_xcdm_kernel<2, true, false>,
+         (const void *)fatchord_xcdm_kernel<3, true, false>, (const void *)fatchord_xcdm_kernel<4, true, false>},
+        {(const void *)fatchord_xcdm_kernel<1, false, true>, (const void *)fatchord_xcdm_kernel<2, false, true>,
+         (const void *)fatchord_xcdm_kernel<3, false, true>, (const void *)fatchord_xcdm_kernel<4, false, true>}};
+    return k[raw ? 2 : dbg ? 1 : 0][nq < 1 ? 0 : nq > kMQuadMax ? kMQuadMax - 1 : nq - 1];
 }
 
-hipError_t launch_xcdm(const XcdmArgs &a, int nq, hipStream_t st) {
+hipError_t launch_xcdm(const XcdmArgs &a, int nq, bool raw, hipStream_t st) {
     XcdmArgs args = a;
     void *params[] = {&args};
-    const void *kf = xcdm_kernel(nq, a.dbg != nullptr);
+    const bool dbg = !raw && a.dbg != nullptr;
+    const void *kf = xcdm_kernel(nq, dbg, raw);
     return hipLaunchKernel(kf, dim3(kXcds * kXcdWgs), dim3(kMThreads), params,
-                           xcdm_lds_layout(nq, a.dbg != nullptr).total * sizeof(float), st);
+                           xcdm_lds_layout(nq, dbg, raw).total * sizeof(float), st);
 }
 
 hipError_t prepare_xcdm_kernel(int max_lds_bytes) {
-    for (int dbg = 0; dbg < 2; ++dbg)
+    for (int v = 0; v < 3; ++v)
         for (int nq = 1; nq <= kMQuadMax; ++nq) {
-            hipError_t e = hipFuncSetAttribute(xcdm_kernel(nq, dbg), hipFuncAttributeMaxDynamicSharedMemorySize, max_lds_bytes);
+            hipError_t e = hipFuncSetAttribute(xcdm_kernel(nq, v == 1, v == 2), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               max_lds_bytes);
             if (e != hipSuccess) return e;
         }
     return hipSuccess;
 }
 
 // largest quad count whose launch is co-resident (one workgroup per CU); 0 if none
-hipError_t xcdm_max_quads(int max_lds_bytes, int *nq_max) {
+hipError_t xcdm_max_quads(int max_lds_bytes, bool raw, int *nq_max) {
     *nq_max = 0;
     for (int nq = 1; nq <= kMQuadMax; ++nq) {
-        if (xcdm_lds_layout(nq, true).total * sizeof(float) > (size_t)max_lds_bytes) break;
+        if (xcdm_lds_layout(nq, !raw, raw).total * sizeof(float) > (size_t)max_lds_bytes) break;
         int n = 0;
-        for (int dbg = 0; dbg < 2; ++dbg) {
-            const size_t lds = xcdm_lds_layout(nq, dbg).total * sizeof(float);
-            hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xcdm_kernel(nq, dbg), kMThreads, lds);
+        for (int dbg = 0; dbg < (raw ? 1 : 2); ++dbg) {
+            const size_t lds = xcdm_lds_layout(nq, dbg, raw).total * sizeof(float);
+            hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xcdm_kernel(nq, dbg, raw), kMThreads, lds);
             if (e != hipSuccess) return e;
             if (n < 1) return hipSuccess;
         }
