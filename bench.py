@@ -104,6 +104,27 @@ def other_configs(dev) -> dict:
                                         "excluded), incl. the conditioning-terms GEMM"}
     del cond
     loop.close()
+    # config 1's model (RAW 9-bit, rnn 512) on the GPU through the drop-in generate(): 1 s unbatched
+    # (the reference runs it on the CPU) and a 5 s utterance fold-batched
+    dr = syn.DEFAULT_RAW
+    model = WaveRNN(**dr.ctor_kwargs()).to(dev)
+    model.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in syn.make_fatchord_state(dr, 0).items()})
+    for key, sec, batched in (("config1_raw_1s_unbatched", 1.0, False), ("config1_raw_5s_fold_batched", 5.0, True)):
+        mel = torch.from_numpy(syn.make_mel(dr.feat_dims, syn.frames_for_seconds(sec, dr.sample_rate, dr.hop_length),
+                                            5))[None]
+        model.generate(mel, None, batched, 11000, 550, True, seed=1, verbose=False)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        out = model.generate(mel, None, batched, 11000, 550, True, seed=2, verbose=False)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t
+        h = model.loop_handle()
+        ms = h.elapsed_ms()
+        res[key] = {"samples_per_s": out.shape[0] / dt, "rtf": out.shape[0] / dt / dr.sample_rate, "wall_s": dt,
+                    "device_ms": ms, "kernel_path": h.info["last_path"],
+                    "note": "RAW 9-bit (bits mode, mu-law) generate() of a synthetic mel on the drop-in; path 7 = "
+                            "fatchord_xcdm_kernel's softmax head; rate over the whole generate() wall time"}
+    del model
     # config 3
     d = syn.DEFAULT_MOL
     model = WaveRNN(**d.ctor_kwargs()).to(dev)
