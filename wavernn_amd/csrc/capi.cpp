@@ -1606,10 +1606,16 @@ int generate_split(wrnn_t *h, const float *cond, int B, int L, const float *nois
 // chunks sized so terms + GEMM input stay within WRNN_TERMS_MB (default 8192 MiB).  Each chunk's
 // terms cover one step past its end (step t publishes the GRU1 terms of t + 1); the recurrent
 // state is carried per workgroup in d_xstate.
-int generate_xcd(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed, int64_t row_offset,
-                 float *out, hipStream_t st) {
-    const wrnn_config &c = h->cfg;
-    const int R = c.rnn_dims, A = c.aux_dims, N = kXcdWgs * kXTerms;
+// The one-row-per-XCD kernels (fatchord_xcd: dense rnn 512, fatchord_xcds: block-sparse rnn 896)
+// share this launch loop: rows in groups of 8 (one per XCD), time chunks whose precomputed terms
+// fit the WRNN_TERMS_MB budget, one terms GEMM per chunk (one step ahead: the kernels prefetch
+// the terms of step t + 1), the recurrent state carried per workgroup between chunks.
+// n_terms = terms per workgroup and step, state_w = carried floats per workgroup.
+template <typename Args, typename Slab>
+int generate_xcd_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed,
+                      int64_t row_offset, float *out, hipStream_t st, int n_terms, int state_w, const Slab &slab,
+                      hipError_t (*launch)(const Args &, hipStream_t)) {
+    const int N = kXcdWgs * n_terms;
     if (!h->blas && rocblas_create_handle(&h->blas) != rocblas_status_success)
         return fail(h, WRNN_EHIP, "rocblas_create_handle failed");
     if (rocblas_set_stream(h->blas, st) != rocblas_status_success) return fail(h, WRNN_EHIP, "rocblas_set_stream failed");
@@ -1622,7 +1628,13 @@ int generate_xcd(wrnn_t *h, const float *cond, int B, int L, const float *noise,
     }
     const char *dbg_env = std::getenv("WRNN_DEBUG_STAMPS");
     const int dbg_steps = dbg_env ? std::min(L, std::atoi(dbg_env)) : 0;
-    unsigned *d_dbg = nullptr;
+    // the stamp buffer is freed on every exit (dump_stamps frees it itself on success)
+    struct DbgBuf {
+        unsigned *p = nullptr;
+        ~DbgBuf() {
+            if (p) (void)hipFree(p);
+        }
+    } dbg;
     int dbg_G = 0;
     const float one = 1.0f, zero = 0.0f;
     for (int b0 = 0; b0 < B; b0 += kXcds) {
@@ -1630,12 +1642,12 @@ int generate_xcd(wrnn_t *h, const float *cond, int B, int L, const float *noise,
         const int Lc_max = (int)std::max(1.0, std::min((double)L, budget / ((double)nb * (N + h->KXc)) - 1.0));
         if (grow(h, h->d_X, h->X_cap, (size_t)(Lc_max + 1) * nb * h->KXc) ||
             grow(h, h->d_T, h->T_cap, (size_t)(Lc_max + 1) * nb * N) ||
-            grow(h, h->d_xstate, h->xstate_cap, (size_t)nb * kXcdWgs * kXStateW))
+            grow(h, h->d_xstate, h->xstate_cap, (size_t)nb * kXcdWgs * state_w))
             return WRNN_EHIP;
-        if (dbg_steps > 0 && !d_dbg) {
+        if (dbg_steps > 0 && !dbg.p) {
             dbg_G = nb * kXcdWgs;
-            HIP_TRY(h, hipMalloc(&d_dbg, (size_t)dbg_G * dbg_steps * kStamps * 4));
-            HIP_TRY(h, hipMemsetAsync(d_dbg, 0, (size_t)dbg_G * dbg_steps * kStamps * 4, st));
+            HIP_TRY(h, hipMalloc(&dbg.p, (size_t)dbg_G * dbg_steps * kStamps * 4));
+            HIP_TRY(h, hipMemsetAsync(dbg.p, 0, (size_t)dbg_G * dbg_steps * kStamps * 4, st));
         }
         HIP_TRY(h, hipMemsetAsync(h->d_xgx, 0, (size_t)nb * kXXcdStride * 8, st));   // tags restart at 1
         for (int t0 = 0; t0 < L; t0 += Lc_max) {
@@ -1646,7 +1658,7 @@ int generate_xcd(wrnn_t *h, const float *cond, int B, int L, const float *noise,
                               h->d_xWt, h->KXc, h->d_X, h->KXc, &zero, h->d_T, N) != rocblas_status_success)
                 return fail(h, WRNN_EHIP, "rocblas_sgemm (conditioning terms) failed");
             HIP_TRY(h, hipMemsetAsync(h->d_members, 0, kXcds * sizeof(int), st));
-            XcdArgs a{};
+            Args a{};
             a.slab = h->d_xslab;
             a.terms = h->d_T;
             a.noise = noise;
@@ -1664,83 +1676,30 @@ int generate_xcd(wrnn_t *h, const float *cond, int B, int L, const float *noise,
             a.Bt = B;
             a.b0 = b0;
             a.nb = nb;
-            a.s = h->xs;
-            a.dbg = (b0 == 0 && t0 == 0) ? d_dbg : nullptr;
+            a.s = slab;
+            a.dbg = (b0 == 0 && t0 == 0) ? dbg.p : nullptr;
             a.dbg_steps = std::min(dbg_steps, Lc);
-            HIP_TRY(h, launch_xcd(a, st));
+            HIP_TRY(h, launch(a, st));
         }
     }
-    if (d_dbg) return dump_stamps(h, d_dbg, dbg_steps, st, dbg_G);
+    if (dbg.p) {
+        unsigned *p = dbg.p;
+        dbg.p = nullptr;
+        return dump_stamps(h, p, dbg_steps, st, dbg_G);
+    }
     return WRNN_OK;
 }
 
-// MoL rows (rnn 896, block-sparse GRU) through the XCD-resident sparse kernel: as generate_xcd.
+int generate_xcd(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed, int64_t row_offset,
+                 float *out, hipStream_t st) {
+    return generate_xcd_rows<XcdArgs>(h, cond, B, L, noise, seed, row_offset, out, st, kXTerms, kXStateW, h->xs,
+                                      launch_xcd);
+}
+
 int generate_xcds(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed, int64_t row_offset,
                   float *out, hipStream_t st) {
-    const wrnn_config &c = h->cfg;
-    const int R = c.rnn_dims, A = c.aux_dims, N = kXcdWgs * kSTerms;
-    if (!h->blas && rocblas_create_handle(&h->blas) != rocblas_status_success)
-        return fail(h, WRNN_EHIP, "rocblas_create_handle failed");
-    if (rocblas_set_stream(h->blas, st) != rocblas_status_success) return fail(h, WRNN_EHIP, "rocblas_set_stream failed");
-    const char *mb_env = std::getenv("WRNN_TERMS_MB");
-    const double budget = (mb_env ? std::atof(mb_env) : 8192.0) * (1 << 20) / 4.0;   // floats
-    const size_t xg_words = (size_t)kXcds * kXXcdStride;
-    if (!h->d_members) {
-        HIP_TRY(h, hipMalloc(&h->d_members, kXcds * sizeof(int)));
-        HIP_TRY(h, hipMalloc(&h->d_xgx, xg_words * 8));
-    }
-    const char *dbg_env = std::getenv("WRNN_DEBUG_STAMPS");
-    const int dbg_steps = dbg_env ? std::min(L, std::atoi(dbg_env)) : 0;
-    unsigned *d_dbg = nullptr;
-    int dbg_G = 0;
-    const float one = 1.0f, zero = 0.0f;
-    for (int b0 = 0; b0 < B; b0 += kXcds) {
-        const int nb = std::min(kXcds, B - b0);
-        const int Lc_max = (int)std::max(1.0, std::min((double)L, budget / ((double)nb * (N + h->KXc)) - 1.0));
-        if (grow(h, h->d_X, h->X_cap, (size_t)(Lc_max + 1) * nb * h->KXc) ||
-            grow(h, h->d_T, h->T_cap, (size_t)(Lc_max + 1) * nb * N) ||
-            grow(h, h->d_xstate, h->xstate_cap, (size_t)nb * kXcdWgs * kSStateW))
-            return WRNN_EHIP;
-        if (dbg_steps > 0 && !d_dbg) {
-            dbg_G = nb * kXcdWgs;
-            HIP_TRY(h, hipMalloc(&d_dbg, (size_t)dbg_G * dbg_steps * kStamps * 4));
-            HIP_TRY(h, hipMemsetAsync(d_dbg, 0, (size_t)dbg_G * dbg_steps * kStamps * 4, st));
-        }
-        HIP_TRY(h, hipMemsetAsync(h->d_xgx, 0, (size_t)nb * kXXcdStride * 8, st));   // tags restart at 1
-        for (int t0 = 0; t0 < L; t0 += Lc_max) {
-            const int Lc = std::min(Lc_max, L - t0);
-            const int rows = std::min(Lc + 1, L - t0);     // terms rows: steps [t0, t0 + rows)
-            HIP_TRY(h, launch_pack_cond_input(cond, h->CD, B, b0, nb, t0, rows, h->KXc, h->d_X, st));
-            if (rocblas_sgemm(h->blas, rocblas_operation_transpose, rocblas_operation_none, N, rows * nb, h->KXc, &one,
-                              h->d_xWt, h->KXc, h->d_X, h->KXc, &zero, h->d_T, N) != rocblas_status_success)
-                return fail(h, WRNN_EHIP, "rocblas_sgemm (conditioning terms) failed");
-            HIP_TRY(h, hipMemsetAsync(h->d_members, 0, kXcds * sizeof(int), st));
-            XcdsArgs a{};
-            a.slab = h->d_xslab;
-            a.terms = h->d_T;
-            a.noise = noise;
-            a.out = out;
-            a.state = h->d_xstate;
-            a.xg = h->d_xgx;
-            a.members = h->d_members;
-            a.ctl = h->d_ctl;
-            a.seed = seed;
-            a.row0 = row_offset + b0;
-            a.timeout_ticks = h->timeout_ticks;
-            a.L = L;
-            a.t0 = t0;
-            a.Lc = Lc;
-            a.Bt = B;
-            a.b0 = b0;
-            a.nb = nb;
-            a.s = h->xss;
-            a.dbg = (b0 == 0 && t0 == 0) ? d_dbg : nullptr;
-            a.dbg_steps = std::min(dbg_steps, Lc);
-            HIP_TRY(h, launch_xcds(a, st));
-        }
-    }
-    if (d_dbg) return dump_stamps(h, d_dbg, dbg_steps, st, dbg_G);
-    return WRNN_OK;
+    return generate_xcd_rows<XcdsArgs>(h, cond, B, L, noise, seed, row_offset, out, st, kSTerms, kSStateW, h->xss,
+                                       launch_xcds);
 }
 
 // MoL rows through the XCD-resident many-row kernel: up to kMRowsMax rows per launch (launch row
