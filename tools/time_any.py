@@ -13,8 +13,12 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from wavernn_amd import _native  # noqa: E402
 from wavernn_amd import synthetic as syn  # noqa: E402
 from wavernn_amd.loop import FatchordLoop  # noqa: E402
+
+if os.environ.get("TIME_DM_LIB"):   # A/B of two builds of the library (diagnostics only)
+    _native.LIB_PATH = os.environ["TIME_DM_LIB"]
 
 
 def main():

@@ -55,7 +55,7 @@ enum MCst { MC_Q1 = 0, MC_Q2 = 48, MC_BIH1 = 96, MC_BHH1 = 144, MC_BIH2 = 192, M
 struct XcdmSlab {
     int a;       // [kMWaves][kMSets][16][64]   MFMA A operands
     int a3;      // RAW: [kMWaves][kMJ / 4][64][4] fc3 A operands (own classes), copied to LDS
-    int w3;      // [32][16]                     W3[j][16c + r] (j >= 30: 0)
+    int w3;      // [16][32]                     W3[j][16c + r] at r·32 + j (j >= 30: 0; lanes j read distinct banks)
     int cst;     // [kMCst]
     int total;
 };

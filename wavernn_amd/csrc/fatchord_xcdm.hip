@@ -771,7 +771,7 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
                 const int fj = i & 31, fn = i >> 5;
                 float p = 0.0f;
 #pragma unroll
-                for (int r = 0; r < 16; ++r) p = fmaf(w3s[fj * 16 + r], f2s[r * NR + fn], p);
+                for (int r = 0; r < 16; ++r) p = fmaf(w3s[r * 32 + fj], f2s[r * NR + fn], p);
                 xpub(xg + kMHopOff[MH_F2] + (fn * kXcdWgs + c) * 32 + fj, tag, p);
             }
         }

@@ -518,7 +518,13 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
                     gh2_dots();
                 }
             } else {
+                // wave 4 sets the flag on every path (its poll is bounded); the abort word ends the
+                // wait too should that ever change
+                unsigned spin = 0;
                 while (__hip_atomic_load(f2ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)tag) {
+                    if ((++spin & 255u) == 0 &&
+                        __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+                        break;
                 }
                 asm volatile("" ::: "memory");
                 if (lane < kXF2Line) xpub_b(xgr, XGI(XH_F2) + c * kXF2Line + lane, tag, p + f2x[lane]);   // 30, 31: zero weights
