@@ -97,3 +97,39 @@ def test_deepmind_streamed_weights_bit_exact():
     out, comb = loop.generate(B, L, noise=torch.from_numpy(noise).to(DEV))
     assert loop.info["last_path"] == 10
     np.testing.assert_array_equal(comb.cpu().numpy().astype(np.int64), ref)
+
+
+@pytest.mark.parametrize("mode", ["MOL", "RAW"])
+def test_dims_not_multiple_of_4(mode, monkeypatch):
+    """rnn 30 / fc 37 / aux 5 (res_out 20): the host handle zero-pads to 32 / 40 / 8 (exact,
+    tests/test_padding.py) — MoL within MOL_TOL and RAW labels bit-exact vs the oracle on the
+    original dims, at 1 and 3 rows."""
+    from oracle import oracle
+    monkeypatch.delenv("WRNN_PATH", raising=False)
+    d = syn.FatchordDims(rnn_dims=30, fc_dims=37, bits=6, compute_dims=16, res_out_dims=20, res_blocks=1, mode=mode)
+    state = syn.make_fatchord_state(d, 750)
+    for B in (1, 3):
+        mels, aux = syn.make_conditioning(B, 200, d.feat_dims, d.res_out_dims, 751 + B)
+        noise = syn.make_noise(mode, B, 200, d.n_classes, 753 + B)
+        ref, ref_lab = oracle.fatchord_loop(state, mode, mels, aux, noise)
+        loop = _loop(d)
+        loop.set_weights(state)
+        out, lab = loop.generate(_cond(mels, aux), noise=torch.from_numpy(noise).to(DEV), want_labels=True)
+        if mode == "RAW":
+            np.testing.assert_array_equal(lab.cpu().numpy(), ref_lab)
+        else:
+            assert np.abs(out.cpu().numpy() - ref).max() <= gf.MOL_TOL
+        loop.close()
+
+
+def test_dims_not_multiple_of_4_dropin_generate():
+    """The same odd dims through the drop-in WaveRNN.generate() (upsample, fold, loop, post): the
+    reference output length (T − 1)·hop (fatchord_version.py:242) of finite samples in [−1, 1]."""
+    from wavernn_amd.fatchord_version import WaveRNN
+    d = syn.FatchordDims(rnn_dims=30, fc_dims=37, bits=9, compute_dims=16, res_out_dims=20, res_blocks=1,
+                         mode="MOL")
+    m = WaveRNN(**d.ctor_kwargs()).to(DEV)
+    m.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in syn.make_fatchord_state(d, 760).items()})
+    mel = torch.from_numpy(syn.make_mel(d.feat_dims, 40, 761))[None]
+    out = m.generate(mel, None, False, 11000, 550, False, seed=3, verbose=False)
+    assert out.shape[0] == (40 - 1) * d.hop_length and np.isfinite(out).all() and np.abs(out).max() <= 1.0

@@ -1109,7 +1109,7 @@ void make_xcdm_slab(wrnn_ctx &h) {
     const bool raw = h.cfg.mode == WRNN_MODE_RAW;
     x.a = take(kMWaves * kMSets * kMJ * 64);
     x.a3 = take(raw ? kMWaves * kMJ * 64 : 0);
-    x.w3 = take(raw ? 0 : 32 * 16);
+    x.w3 = take(raw ? 0 : 32 * kMW3Stride);
     x.cst = take(kMCst);
     x.total = o;
 }
@@ -1147,7 +1147,7 @@ void pack_xcdm_slab(const wrnn_ctx &h, std::vector<float> &slab) {
                             W("fc3.weight")[(size_t)(16 * c + (l & 15)) * F + kMK * w + kMJ * (l >> 4) + j];
         } else {
             for (int jj = 0; jj < NC; ++jj)
-                for (int r = 0; r < 16; ++r) out[x.w3 + r * 32 + jj] = W("fc3.weight")[(size_t)jj * F + 16 * c + r];
+                for (int r = 0; r < 16; ++r) out[x.w3 + jj * kMW3Stride + r] = W("fc3.weight")[(size_t)jj * F + 16 * c + r];
         }
         for (int u = 0; u < 16; ++u) {
             const int j = 16 * c + u;

@@ -45,6 +45,9 @@ constexpr long long kMHopOff[kMHops] = {0, kMVec, 2 * kMVec, 3 * kMVec, 4 * kMVe
                                         4 * kMVec + kMF2 + 64};
 constexpr long long kMXcdStride = 5 * kMVec + kMF2 + 64;   // granules per XCD
 constexpr int kMRawNC = 512;        // RAW classes (bits = 9)
+// MoL fc3 partials: the 16 fc3 columns of a logit and the 16 own f2 rows of a batch row are each
+// read as four ds_read_b128; rows padded to 20 floats so the 16 lanes of a b128 phase hit distinct banks
+constexpr int kMW3Stride = 20;
 
 // Per-workgroup constants (LDS), gate-major: index q·16 + u
 enum MCst { MC_Q1 = 0, MC_Q2 = 48, MC_BIH1 = 96, MC_BHH1 = 144, MC_BIH2 = 192, MC_BHH2 = 240, MC_WI0 = 288,
@@ -55,7 +58,7 @@ enum MCst { MC_Q1 = 0, MC_Q2 = 48, MC_BIH1 = 96, MC_BHH1 = 144, MC_BIH2 = 192, M
 struct XcdmSlab {
     int a;       // [kMWaves][kMSets][16][64]   MFMA A operands
     int a3;      // RAW: [kMWaves][kMJ / 4][64][4] fc3 A operands (own classes), copied to LDS
-    int w3;      // [16][32]                     W3[j][16c + r] at r·32 + j (j >= 30: 0; lanes j read distinct banks)
+    int w3;      // [32][kMW3Stride]             W3[j][16c + r] at j·20 + r (j >= 30: 0)
     int cst;     // [kMCst]
     int total;
 };
@@ -135,11 +138,11 @@ __host__ __device__ inline XcdmLds xcdm_lds_layout(int nq, bool dbg = false, boo
     l.pfc2 = o;   o += xcdm_pset(nq);
     l.gh1 = o;    o += 3 * 16 * nr;                    // Σ W_hh1·h1 (next step's GRU1)
     l.gh2 = o;    o += 3 * 16 * nr;                    // Σ W_hh2·h2 (next step's GRU2)
-    l.f2 = o;     o += raw ? 0 : 16 * nr;              // MoL: f2 of the own rows (fc3 partials)
+    l.f2 = o;     o += raw ? 0 : kMW3Stride * nr;      // MoL: f2 of the own rows (fc3 partials), [row][20]
     l.ring = o;   o += 2 * nr * kMRing;                // terms of steps t, t + 1 (by parity)
     l.nz = o;     o += raw ? 0 : 2 * nr * kMNoise;
     l.cst = o;    o += kMCst;
-    l.w3 = o;     o += raw ? 0 : 32 * 16;
+    l.w3 = o;     o += raw ? 0 : 32 * kMW3Stride;
     l.a3 = o;     o += raw ? kMWaves * kMJ * 64 : 0;   // RAW: fc3 A operands (LDS-resident)
     l.xs = o;     o += 16;
     l.misc = o;   o += 8;                              // [0] abort flag, [1] member index

@@ -552,7 +552,7 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
     if constexpr (kRaw) {
         for (int i = tid; i < kMWaves * kMJ * 64; i += kMThreads) a3s[i] = S[a.s.a3 + i];
     } else {
-        for (int i = tid; i < 32 * 16; i += kMThreads) w3s[i] = S[a.s.w3 + i];
+        for (int i = tid; i < 32 * kMW3Stride; i += kMThreads) w3s[i] = S[a.s.w3 + i];
         for (int i = tid; i < 2 * NR * kMNoise; i += kMThreads) nzr[i] = 0.0f;
     }
     for (int i = tid; i < 2 * NR * kMRing; i += kMThreads) ring[i] = 0.0f;
@@ -744,7 +744,7 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         if (gru) {
             const float f = mpart<NQ>(pfc2, gu, gn) + rg[gn * kMRing + XT_V2 + gu];
             if constexpr (kRaw) xpub(xg + kMHopOff[MH_F2] + gn * 512 + 16 * c + gu, tag, f > 0.0f ? f : 0.0f);
-            else f2s[gu * NR + gn] = f > 0.0f ? f : 0.0f;
+            else f2s[gn * kMW3Stride + gu] = f > 0.0f ? f : 0.0f;
             if (aux_w0 >= kMWaves) {
 #pragma unroll
                 for (int q = 0; q < 3; ++q) {
@@ -769,9 +769,20 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
 #pragma unroll
             for (int i = tid; i < 32 * NR; i += kMThreads) {
                 const int fj = i & 31, fn = i >> 5;
+                f4v wv[4], fv[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    wv[q] = lds4(w3s + fj * kMW3Stride + 4 * q);
+                    fv[q] = lds4(f2s + fn * kMW3Stride + 4 * q);
+                }
                 float p = 0.0f;
 #pragma unroll
-                for (int r = 0; r < 16; ++r) p = fmaf(w3s[r * 32 + fj], f2s[r * NR + fn], p);
+                for (int q = 0; q < 4; ++q) {
+                    p = fmaf(wv[q].x, fv[q].x, p);
+                    p = fmaf(wv[q].y, fv[q].y, p);
+                    p = fmaf(wv[q].z, fv[q].z, p);
+                    p = fmaf(wv[q].w, fv[q].w, p);
+                }
                 xpub(xg + kMHopOff[MH_F2] + (fn * kXcdWgs + c) * 32 + fj, tag, p);
             }
         }

@@ -24,6 +24,59 @@ DM_KEYS = ("R.weight", "O1.weight", "O1.bias", "O2.weight", "O2.bias", "O3.weigh
            "O4.bias", "I_coarse.weight", "I_fine.weight", "bias_u", "bias_r", "bias_e")
 
 
+def _round4(n: int) -> int:
+    return (n + 3) // 4 * 4
+
+
+def pad_loop_state(state: Mapping[str, np.ndarray], R: int, F: int, A: int, M: int, Rp: int, Fp: int,
+                   Ap: int) -> dict:
+    """Zero-pad the loop tensors of a WaveRNN with rnn / fc / aux dims R, F, A to Rp, Fp, Ap (the
+    kernels' float4 layouts need multiples of 4).  Exact: a padded GRU unit has zero weights and
+    biases, so r = z = ½, n = tanh(0) = 0 and h' = h / 2 stays 0 from h = 0; a padded fc row is
+    relu(0) = 0; every padded column multiplies such a zero (or a zero-padded aux channel), so the
+    real units, rows and logits see only added zero terms (fatchord_version.py:97-123 shapes)."""
+    def gates(w, rows, rows_p, cols_map, ncols_p):
+        out = np.zeros((3 * rows_p, ncols_p), np.float32)
+        for g in range(3):
+            for (c0, c1, d0) in cols_map:
+                out[g * rows_p:g * rows_p + rows, d0:d0 + c1 - c0] = w[g * rows:(g + 1) * rows, c0:c1]
+        return out
+
+    def vec3(b, n, n_p):
+        out = np.zeros(3 * n_p, np.float32)
+        for g in range(3):
+            out[g * n_p:g * n_p + n] = b[g * n:(g + 1) * n]
+        return out
+
+    def mat(w, rows_p, cols_map, ncols_p):
+        out = np.zeros((rows_p, ncols_p), np.float32)
+        for (c0, c1, d0) in cols_map:
+            out[:w.shape[0], d0:d0 + c1 - c0] = w[:, c0:c1]
+        return out
+
+    def vec(b, n_p):
+        out = np.zeros(n_p, np.float32)
+        out[:b.shape[0]] = b
+        return out
+
+    st = {k: np.asarray(v.detach().cpu().numpy() if isinstance(v, torch.Tensor) else v, np.float32)
+          for k, v in state.items() if k in LOOP_KEYS}
+    o = dict(st)
+    o["I.weight"] = mat(st["I.weight"], Rp, [(0, 1 + M, 0), (1 + M, 1 + M + A, 1 + M)], 1 + M + Ap)
+    o["I.bias"] = vec(st["I.bias"], Rp)
+    for k in ("rnn1.weight_ih_l0", "rnn1.weight_hh_l0", "rnn2.weight_hh_l0"):
+        o[k] = gates(st[k], R, Rp, [(0, R, 0)], Rp)
+    o["rnn2.weight_ih_l0"] = gates(st["rnn2.weight_ih_l0"], R, Rp, [(0, R, 0), (R, R + A, Rp)], Rp + Ap)
+    for k in ("rnn1.bias_ih_l0", "rnn1.bias_hh_l0", "rnn2.bias_ih_l0", "rnn2.bias_hh_l0"):
+        o[k] = vec3(st[k], R, Rp)
+    o["fc1.weight"] = mat(st["fc1.weight"], Fp, [(0, R, 0), (R, R + A, Rp)], Rp + Ap)
+    o["fc1.bias"] = vec(st["fc1.bias"], Fp)
+    o["fc2.weight"] = mat(st["fc2.weight"], Fp, [(0, F, 0), (F, F + A, Fp)], Fp + Ap)
+    o["fc2.bias"] = vec(st["fc2.bias"], Fp)
+    o["fc3.weight"] = mat(st["fc3.weight"], st["fc3.weight"].shape[0], [(0, F, 0)], Fp)
+    return o
+
+
 def noise_width(mode: str, n_classes: int) -> int:
     """K of the injected-noise layout [L][B][K] (reference draw order)."""
     return 11 if mode == "MOL" else n_classes
@@ -41,8 +94,12 @@ class FatchordLoop:
         self.device = device
         self.cond_dims = feat_dims + 4 * aux_dims
         self.noise_k = noise_width(mode, n_classes)
-        self._create(nat.Config(nat.ABI_VERSION, nat.MODE_MOL if mode == "MOL" else nat.MODE_RAW, rnn_dims,
-                                fc_dims, aux_dims, feat_dims, n_classes, grid, timeout_ms), device)
+        # dims that are not multiples of 4 run zero-padded (pad_loop_state; exact)
+        self._dims_p = (_round4(rnn_dims), _round4(fc_dims), _round4(aux_dims))
+        self._padded = self._dims_p != (rnn_dims, fc_dims, aux_dims)
+        Rp, Fp, Ap = self._dims_p
+        self._create(nat.Config(nat.ABI_VERSION, nat.MODE_MOL if mode == "MOL" else nat.MODE_RAW, Rp,
+                                Fp, Ap, feat_dims, n_classes, grid, timeout_ms), device)
 
     def _create(self, cfg, device: int) -> None:
         L = nat.lib()
@@ -59,6 +116,8 @@ class FatchordLoop:
     # ------------------------------------------------------------------ weights
     def set_weights(self, state: Mapping[str, object]) -> None:
         """Pack the loop's tensors (reference state_dict names) into the kernel layout."""
+        if getattr(self, "_padded", False):
+            state = pad_loop_state(state, self.rnn_dims, self.fc_dims, self.aux_dims, self.feat_dims, *self._dims_p)
         keep = []
         arr = (nat.Tensor * len(self.keys))()
         n = 0
@@ -92,6 +151,13 @@ class FatchordLoop:
         L, B, C = cond.shape
         if C != self.cond_dims:
             raise ValueError(f"cond has {C} features, expected {self.cond_dims}")
+        if getattr(self, "_padded", False) and self._dims_p[2] != self.aux_dims:   # aux chunks a1..a4 zero-padded
+            A, Ap, M = self.aux_dims, self._dims_p[2], self.feat_dims
+            cp = torch.zeros(L, B, M + 4 * Ap, dtype=cond.dtype, device=cond.device)
+            cp[:, :, :M] = cond[:, :, :M]
+            for j in range(4):
+                cp[:, :, M + j * Ap:M + j * Ap + A] = cond[:, :, M + j * A:M + (j + 1) * A]
+            cond = cp
         if noise is not None:
             if not (noise.is_cuda and noise.dtype == torch.float32 and noise.is_contiguous()):
                 raise ValueError("noise must be a contiguous fp32 CUDA tensor [L][B][K]")
