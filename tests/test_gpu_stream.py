@@ -124,7 +124,7 @@ def test_dims_not_multiple_of_4(mode, monkeypatch):
 
 def test_dims_not_multiple_of_4_dropin_generate():
     """The same odd dims through the drop-in WaveRNN.generate() (upsample, fold, loop, post): the
-    reference output length (T − 1)·hop (fatchord_version.py:242) of finite samples in [−1, 1]."""
+    reference output length (T − 1)·hop (fatchord_version.py:184, :257) of finite samples in [−1, 1]."""
     from wavernn_amd.fatchord_version import WaveRNN
     d = syn.FatchordDims(rnn_dims=30, fc_dims=37, bits=9, compute_dims=16, res_out_dims=20, res_blocks=1,
                          mode="MOL")
