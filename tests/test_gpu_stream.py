@@ -133,3 +133,35 @@ def test_dims_not_multiple_of_4_dropin_generate():
     mel = torch.from_numpy(syn.make_mel(d.feat_dims, 40, 761))[None]
     out = m.generate(mel, None, False, 11000, 550, False, seed=3, verbose=False)
     assert out.shape[0] == (40 - 1) * d.hop_length and np.isfinite(out).all() and np.abs(out).max() <= 1.0
+
+
+@pytest.mark.parametrize("bits,B", [(10, 1), (10, 3), (11, 2)])
+def test_raw_more_than_512_classes(bits, B, monkeypatch):
+    """bits 10 / 11 (1 024 / 2 048 classes): the sampler's generic form (raw_sample_any), labels
+    bit-exact vs the oracle."""
+    from oracle import oracle
+    monkeypatch.delenv("WRNN_PATH", raising=False)
+    d = syn.FatchordDims(bits=bits, mode="RAW")
+    state = syn.make_fatchord_state(d, 770 + bits)
+    mels, aux = syn.make_conditioning(B, 150, d.feat_dims, d.res_out_dims, 771 + B)
+    noise = syn.make_noise("RAW", B, 150, d.n_classes, 772 + B)
+    _, ref_lab = oracle.fatchord_loop(state, "RAW", mels, aux, noise)
+    loop = _loop(d)
+    loop.set_weights(state)
+    _, lab = loop.generate(_cond(mels, aux), noise=torch.from_numpy(noise).to(DEV), want_labels=True)
+    np.testing.assert_array_equal(lab.cpu().numpy(), ref_lab)
+
+
+def test_deepmind_quantisation_512():
+    """deepmind quantisation 512 (the rows kernel's generic sampler): labels bit-exact vs the oracle."""
+    from oracle import oracle
+    from wavernn_amd.loop import DeepmindLoop
+    d = syn.DeepmindDims(hidden_size=128, quantisation=512)
+    B, L = 3, 150
+    state = syn.make_deepmind_state(d, 780)
+    noise = syn.make_dm_noise(B, L, d.quantisation, 781)
+    _, _, ref = oracle.deepmind_loop(state, B, L, noise)
+    loop = DeepmindLoop(d.hidden_size, d.quantisation)
+    loop.set_weights(state)
+    _, comb = loop.generate(B, L, noise=torch.from_numpy(noise).to(DEV))
+    np.testing.assert_array_equal(comb.cpu().numpy().astype(np.int64), ref)

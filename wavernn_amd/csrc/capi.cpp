@@ -1898,8 +1898,6 @@ int wrnn_create(const wrnn_config *cfg, int device, wrnn_t **out) {
     if (c.mode != WRNN_MODE_DM && (c.rnn_dims % 4 || c.fc_dims % 4 || c.aux_dims % 4))
         return fail(h, WRNN_EUNSUPPORTED, "rnn_dims, fc_dims and aux_dims must be multiples of 4");
     if (mol && c.n_classes != 30) return fail(h, WRNN_EINVAL, "MOL mode has n_classes = 30 (10 logistics)");
-    if (!mol && c.n_classes > 64 * kClsPerLaneMax)
-        return fail(h, WRNN_EUNSUPPORTED, "RAW n_classes > 512 (bits > 9) not supported");
     HIP_TRY(h, hipSetDevice(device));
     hipDeviceProp_t prop;
     HIP_TRY(h, hipGetDeviceProperties(&prop, device));
@@ -1909,7 +1907,6 @@ int wrnn_create(const wrnn_config *cfg, int device, wrnn_t **out) {
     if (c.mode == WRNN_MODE_DM) {   // deepmind_version: the multi-row dual-softmax kernel only
         const int H = c.rnn_dims, S = H / 2, Q = c.n_classes;
         if (S % 4) return fail(h, WRNN_EUNSUPPORTED, "DM hidden_size must be a multiple of 8");
-        if (Q > 256) return fail(h, WRNN_EUNSUPPORTED, "DM quantisation > 256 not supported");
         const int gt = c.grid > 0 ? c.grid : h->num_cus;
         h->dm = true;
         h->dmU = (S + gt - 1) / gt;

@@ -281,7 +281,8 @@ __global__ __launch_bounds__(kDmThreads) void deepmind_rows_kernel(DmArgs a, DmG
                 const int b = w + sr * G;
                 if (b >= B) break;
                 const float *q = nzs + (t & 1) * NS * ll.nkp + sr * ll.nkp + (fine ? Q : 0);
-                const int label = raw_sample<4>(tile + sr * ll.KT, q, Q, lane);
+                const int label = Q <= 256 ? raw_sample<4>(tile + sr * ll.KT, q, Q, lane)
+                                           : raw_sample_any(tile + sr * ll.KT, q, Q, lane);
                 if (lane < kXReps) publish(xgp(which) + (size_t)lane * kXRepStride + b, (uint32_t)t + 1u, (float)label);
                 if (!fine) {
                     if (lane == 0) ccur[sr] = (float)label;

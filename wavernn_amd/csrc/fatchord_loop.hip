@@ -458,7 +458,8 @@ __global__ __launch_bounds__(kThreads) void fatchord_loop_kernel(LoopArgs a) {
                 if (MOL) {
                     x = mol_sample(l, u, lane);
                 } else {
-                    label = raw_sample<kClsPerLaneMax>(l, u, NC, lane);
+                    label = NC <= 64 * kClsPerLaneMax ? raw_sample<kClsPerLaneMax>(l, u, NC, lane)
+                                                      : raw_sample_any(l, u, NC, lane);
                     x = label_to_x(label, NC);
                 }
                 if (lane == 0) { xprev[b] = x; lbl[b] = label; }

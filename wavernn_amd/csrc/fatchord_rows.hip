@@ -501,7 +501,8 @@ __global__ __launch_bounds__(kRowsThreads) void fatchord_rows_kernel(RowsArgs a,
                     if (MOL) {
                         x = mol_sample(lgs + sr * ll.ncp, u, lane);
                     } else {
-                        label = raw_sample<kClsPerLaneMax>(tile + sr * ll.KT, u, NC, lane);
+                        label = NC <= 64 * kClsPerLaneMax ? raw_sample<kClsPerLaneMax>(tile + sr * ll.KT, u, NC, lane)
+                                                          : raw_sample_any(tile + sr * ll.KT, u, NC, lane);
                         x = label_to_x(label, NC);
                     }
                     if (lane < kXReps) publish(a.xg + (size_t)lane * kXRepStride + b, want, x);

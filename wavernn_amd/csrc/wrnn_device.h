@@ -519,6 +519,25 @@ __device__ __forceinline__ int raw_sample(const float *l, const float *u, int NC
     return wave_argmax(bv, bi);
 }
 
+// The same for any class count (bits > 9, quantisation > 256): the exponentials are recomputed in
+// each pass instead of held in registers — the same fp32 values in the same per-lane order, so
+// the same label as raw_sample for NC <= 64·kClsPerLane.
+__device__ __forceinline__ int raw_sample_any(const float *l, const float *u, int NC, int lane) {
+    float m = -INFINITY;
+    for (int c = lane; c < NC; c += 64) m = fmaxf(m, l[c]);
+    m = wave_max(m);
+    float s1 = 0.0f;
+    for (int c = lane; c < NC; c += 64) s1 += expf(l[c] - m);
+    s1 = wave_sum(s1);
+    float s2 = 0.0f;
+    for (int c = lane; c < NC; c += 64) s2 += expf(l[c] - m) / s1;
+    s2 = wave_sum(s2);
+    float bv = -INFINITY;
+    int bi = 0x7FFFFFFF;
+    for (int c = lane; c < NC; c += 64) am_merge(bv, bi, ((expf(l[c] - m) / s1) / s2) / u[c], c);
+    return wave_argmax(bv, bi);
+}
+
 // RAW label → sample value (fatchord_version.py:235), fp32 like the reference
 __device__ __forceinline__ float label_to_x(int label, int NC) { return (2.0f * (float)label) / ((float)NC - 1.0f) - 1.0f; }
 
