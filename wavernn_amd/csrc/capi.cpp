@@ -51,10 +51,9 @@ hipError_t xcd_occupancy(int *blocks_per_cu);
 hipError_t launch_xcds(const XcdsArgs &a, hipStream_t st);
 hipError_t prepare_xcds_kernel(int max_lds_bytes);
 hipError_t xcds_occupancy(int *blocks_per_cu);
-hipError_t launch_xcdm(const XcdmArgs &a, int nq, bool raw, bool loc, hipStream_t st);
+hipError_t launch_xcdm(const XcdmArgs &a, int nq, bool raw, hipStream_t st);
 hipError_t prepare_xcdm_kernel(int max_lds_bytes);
 hipError_t xcdm_max_quads(int max_lds_bytes, bool raw, int *nq_max);
-hipError_t xcdm_loc_ok(int max_lds_bytes, bool raw, bool *ok);
 hipError_t launch_philox_fill(float *out, unsigned long long seed, long long row0, int nb, int t0, int Lc, int K, int mol,
                               hipStream_t st);
 hipError_t launch_dx(const DxArgs &a, hipStream_t st);
@@ -152,7 +151,6 @@ struct wrnn_ctx {
     // kernel's terms-GEMM weights (d_xWt)
     bool xcdm_ok = false;
     int xcdm_nq = 0;                                // largest co-resident quad count (rows per XCD / 4)
-    bool xcdm_loc = false;                          // its local-GRU1 one-quad form is co-resident
     XcdmSlab xms{};
     float *d_xmslab = nullptr, *d_xmstate = nullptr, *d_xmnoise = nullptr;
     size_t xmnoise_cap = 0;
@@ -1113,7 +1111,6 @@ void make_xcdm_slab(wrnn_ctx &h) {
     x.a3 = take(raw ? kMWaves * kMJ * 64 : 0);
     x.w3 = take(raw ? 0 : 32 * kMW3Stride);
     x.cst = take(kMCst);
-    x.q1a = take(3 * 512);
     x.total = o;
 }
 
@@ -1124,8 +1121,6 @@ void pack_xcdm_slab(const wrnn_ctx &h, std::vector<float> &slab) {
     const int nin = 1 + h.cfg.feat_dims + A;
     const XcdmSlab &x = h.xms;
     slab.assign((size_t)kXcdWgs * x.total, 0.0f);
-    std::vector<float> q1a(3 * R);   // W_ih1 · W_I[:, 0] of every unit (the local-GRU1 form)
-    for (int r = 0; r < 3 * R; ++r) q1a[r] = xcol_dot(W("rnn1.weight_ih_l0") + (size_t)r * R, IW, nin, R);
     // row r (0..15) of set s of workgroup c: (matrix, row index, row stride)
     auto set_row = [&](int s, int c, int r) -> const float * {
         if (s < MS_FC1) return W("rnn2.weight_ih_l0") + (size_t)(s * R + 16 * c + r) * (R + A);
@@ -1167,7 +1162,6 @@ void pack_xcdm_slab(const wrnn_ctx &h, std::vector<float> &slab) {
                 out[x.cst + MC_BHH2 + i] = W("rnn2.bias_hh_l0")[src];
             }
         }
-        std::memcpy(out + x.q1a, q1a.data(), (size_t)3 * R * 4);
         if (h.cfg.mode == WRNN_MODE_RAW)
             for (int r = 0; r < 16; ++r) out[x.cst + MC_B3 + r] = W("fc3.bias")[16 * c + r];
         else
@@ -1740,11 +1734,6 @@ int generate_xcdm(wrnn_t *h, const float *cond, int B, int L, const float *noise
     for (int b0 = 0; b0 < B; b0 += rows_max) {
         const int nb = std::min(rows_max, B - b0);
         const int nq = (((nb + kXcds - 1) / kXcds) + 3) / 4;   // quads on the fullest XCD
-        // at most kMLocRows rows per XCD: GRU1 of every unit in every workgroup, no h1 hop — opt-in
-        // (WRNN_XCDM_LOCAL=1): measured slower than the hop form so far
-        const char *loc_env = std::getenv("WRNN_XCDM_LOCAL");
-        const bool loc = h->xcdm_loc && nq == 1 && (nb + kXcds - 1) / kXcds <= kMLocRows &&
-                         (loc_env && std::string(loc_env) == "1");
         const int Lc_max = (int)std::max(1.0, std::min((double)L, budget / ((double)nb * (N + h->KXc + (noise ? 0 : NK)))));
         if (grow(h, h->d_X, h->X_cap, (size_t)Lc_max * nb * h->KXc) || grow(h, h->d_T, h->T_cap, (size_t)Lc_max * nb * N) ||
             (!noise && grow(h, h->d_xmnoise, h->xmnoise_cap, (size_t)Lc_max * nb * NK)))
@@ -1791,7 +1780,7 @@ int generate_xcdm(wrnn_t *h, const float *cond, int B, int L, const float *noise
             a.nb = nb;
             a.s = h->xms;
             a.dbg = (b0 == 0 && t0 == 0 && Lc >= kMDbgSkip + kMDbgSteps) ? d_dbg : nullptr;
-            HIP_TRY(h, launch_xcdm(a, nq, raw, loc, st));
+            HIP_TRY(h, launch_xcdm(a, nq, raw, st));
         }
     }
     if (d_dbg) {
@@ -2042,7 +2031,6 @@ int wrnn_create(const wrnn_config *cfg, int device, wrnn_t **out) {
             make_xcdm_slab(*h);
             HIP_TRY(h, prepare_xcdm_kernel(h->max_lds));
             HIP_TRY(h, xcdm_max_quads(h->max_lds, false, &h->xcdm_nq));
-            HIP_TRY(h, xcdm_loc_ok(h->max_lds, false, &h->xcdm_loc));
             h->xcdm_ok = h->xcdm_nq >= 1;
         }
     }
@@ -2052,7 +2040,6 @@ int wrnn_create(const wrnn_config *cfg, int device, wrnn_t **out) {
         make_xcdm_slab(*h);
         HIP_TRY(h, prepare_xcdm_kernel(h->max_lds));
         HIP_TRY(h, xcdm_max_quads(h->max_lds, true, &h->xcdm_nq));
-        HIP_TRY(h, xcdm_loc_ok(h->max_lds, true, &h->xcdm_loc));
         h->xcdm_ok = h->xcdm_nq >= 1;
     }
     // MoL rnn 896 / fc 512: the XCD-resident block-sparse kernel, if the weights turn out

@@ -60,7 +60,6 @@ struct XcdmSlab {
     int a3;      // RAW: [kMWaves][kMJ / 4][64][4] fc3 A operands (own classes), copied to LDS
     int w3;      // [32][kMW3Stride]             W3[j][16c + r] at j·20 + r (j >= 30: 0)
     int cst;     // [kMCst]
-    int q1a;     // [3][512] W_ih1 · W_I[:, 0] of every unit, gate-major (local GRU1, kLoc)
     int total;
 };
 
@@ -70,16 +69,8 @@ constexpr int kMRing = 144;
 constexpr int kMNoise = 12;                // 11 MoL sampler terms per row and step, padded
 
 // Per-workgroup state carried between time chunks: h1 / h2 of the own units [16][16 rows],
-// W_hh1·h1 / W_hh2·h2 [3][16][16], x [16]; then (kLoc) h1 of every unit [4 rows][512]
-constexpr int kMStateBase = 256 + 256 + 768 + 768 + 16;
-constexpr int kMStateW = kMStateBase + 4 * 512;
-
-// Local GRU1 (kLoc: one quad, at most kMLocRows rows per XCD — fold-batched 5 s and small
-// utterance batches): every workgroup evaluates GRU1 for all 512 units itself (its only step
-// input besides x is rank-1 in x), so h1 needs no hop.  Each workgroup publishes the GRU1 terms
-// S = {S_r, S_z, Gi_n, Gh_n} of its own units for the next step (granules (n·512 + j)·4 + k, in
-// the H1 hop region) and waves 2, 3 gather all of them while the rows are sampled.
-constexpr int kMLocRows = 2;
+// W_hh1·h1 / W_hh2·h2 [3][16][16], x [16]
+constexpr int kMStateW = 256 + 256 + 768 + 768 + 16;
 
 struct XcdmArgs {
     const float *slab;            // [kXcdWgs][slab.total]
@@ -104,7 +95,7 @@ struct XcdmArgs {
 constexpr int kMStamps = 24, kMDbgSteps = 48, kMDbgSkip = 16;
 
 struct XcdmLds {
-    int stg_h1, stg, pbig, phh1, pfc1, pfc2, gh1, gh2, f2, ring, nz, cst, w3, a3, sg, q1a, xs, misc, dbg, total;
+    int stg_h1, stg, pbig, phh1, pfc1, pfc2, gh1, gh2, f2, ring, nz, cst, w3, a3, xs, misc, dbg, total;
 };
 
 // staging of a polled vector slice, per wave: [quad][4 rows][64], value k of row j4 at
@@ -135,7 +126,7 @@ __host__ __device__ constexpr int xcdm_pset(int nq) {
     return xcdm_big(nq) ? 16 * 4 * nq * kMWaves : kMWaves * 16 * xcdm_pstride_row(nq);
 }
 
-__host__ __device__ inline XcdmLds xcdm_lds_layout(int nq, bool dbg = false, bool raw = false, bool loc = false) {
+__host__ __device__ inline XcdmLds xcdm_lds_layout(int nq, bool dbg = false, bool raw = false) {
     const int nr = 4 * nq, nq_stg = xcdm_big(nq) ? kMQuadMax : nq;
     XcdmLds l;
     int o = 0;
@@ -153,8 +144,6 @@ __host__ __device__ inline XcdmLds xcdm_lds_layout(int nq, bool dbg = false, boo
     l.cst = o;    o += kMCst;
     l.w3 = o;     o += raw ? 0 : 32 * kMW3Stride;
     l.a3 = o;     o += raw ? kMWaves * kMJ * 64 : 0;   // RAW: fc3 A operands (LDS-resident)
-    l.sg = o;     o += loc ? kMLocRows * 512 * 4 : 0;  // kLoc: the GRU1 terms of every unit [n][512][4]
-    l.q1a = o;    o += loc ? 3 * 512 : 0;              // kLoc: q1 of every unit [3][512]
     l.xs = o;     o += 16;
     l.misc = o;   o += 8;                              // [0] abort flag, [1] member index
     l.dbg = o;    o += dbg ? kMDbgSteps * kMWaves * kMStamps : 0;

@@ -477,25 +477,19 @@ __device__ __forceinline__ int rsample(const unsigned long long *lg, int n, uint
 // kRaw: the RAW (9-bit softmax) head — f2 published as a hop vector, fc3 (own 16 classes, A
 // operands in LDS) on the gathered f2 slice, the logits a sixth hop, rsample instead of msample;
 // the Exp(1) draws always come from `noise` (Philox pre-filled by the host).
-// kLoc (NQ = 1, at most kMLocRows rows per XCD): GRU1 of every unit in every workgroup, no h1 hop
-// (fatchord_xcdm.h, kMLocRows): step A is GRU1-all straight into the h1 staging images, step B
-// starts the W_ih2 layer at once; wave 1 publishes the own units' GRU1 terms of step t + 1 in F,
-// waves 2 and 3 gather every unit's during J.
-template <int NQ, bool kDbg, bool kRaw, bool kLoc>
+template <int NQ, bool kDbg, bool kRaw>
 __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm_kernel(XcdmArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    static_assert(!kLoc || NQ == 1, "local GRU1 is the one-quad form");
     constexpr int NR = 4 * NQ;
     constexpr bool kTwoLevel = NQ >= 2;
     constexpr int N = kXcdWgs * kXTerms;
-    const XcdmLds ll = xcdm_lds_layout(NQ, kDbg, kRaw, kLoc);
+    const XcdmLds ll = xcdm_lds_layout(NQ, kDbg, kRaw);
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     constexpr int kStgQ = xcdm_big(NQ) ? kMQuadMax : NQ;   // staged quads per wave
     float *stg_h1 = smem + ll.stg_h1 + wave * kStgQ * kMStg, *stg = smem + ll.stg + wave * kStgQ * kMStg;
     float *pbig = smem + ll.pbig, *phh1 = smem + ll.phh1, *pfc1 = smem + ll.pfc1, *pfc2 = smem + ll.pfc2;
     float *gh1 = smem + ll.gh1, *gh2 = smem + ll.gh2, *f2s = smem + ll.f2, *ring = smem + ll.ring, *nzr = smem + ll.nz;
     float *cst = smem + ll.cst, *w3s = smem + ll.w3, *xs = smem + ll.xs, *a3s = smem + ll.a3;
-    float *sgl = smem + ll.sg, *q1s = smem + ll.q1a;
     int *misc = reinterpret_cast<int *>(smem + ll.misc);
     int *abort_flag = misc;
     unsigned *dbgs = reinterpret_cast<unsigned *>(smem + ll.dbg);
@@ -564,24 +558,10 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
     for (int i = tid; i < 2 * NR * kMRing; i += kMThreads) ring[i] = 0.0f;
     for (int i = tid; i < 3 * 16 * NR; i += kMThreads) gh1[i] = gh2[i] = 0.0f;
     if (tid < 16) xs[tid] = 0.0f;
-    if constexpr (kLoc) {
-        for (int i = tid; i < 3 * 512; i += kMThreads) q1s[i] = S[a.s.q1a + i];
-        // rows >= RX of the h1 images stay zero (GRU1-all writes rows < RX only)
-        for (int i = tid; i < kMWaves * kMStg; i += kMThreads) smem[ll.stg_h1 + i] = 0.0f;
-    }
     __syncthreads();
     const bool resume = a.t0 > 0;
     float *st = a.state + ((size_t)k * kXcdWgs + c) * kMStateW;
     float h1v = 0.0f, h2v = 0.0f;   // h1 / h2 of (unit gu, row gn): this thread's recurrent state
-    // kLoc: h1 of the units j = (tid + 256i) & 511, rows n = (tid + 256i) >> 9 (< RX), i < 4
-    float h1l[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-    if (kLoc && resume) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int p = tid + 256 * i;
-            if ((p >> 9) < RX) h1l[i] = st[kMStateBase + p];
-        }
-    }
     if (resume) {
         if (gru) {
             h1v = st[gu * 16 + gn];
@@ -605,48 +585,6 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         }
     __syncthreads();
 
-    // kLoc: the GRU1 terms of the own units for step ts (GH = Σ W_hh1·h1 of step ts − 1, in gh1),
-    // published by wave 1, lanes (u, n) = (l & 15, l >> 4), n < RX — the association of step A's
-    // non-local form: S_r = (GH_r + b_hh,r) + (P1_r + b_ih,r), S_z likewise, Gi_n = P1_n + b_ih,n,
-    // Gh_n = GH_n + b_hh,n
-    auto publish_s = [&](int ts, const float (&p1)[3]) {
-        const int u = lane & 15, n = lane >> 4;
-        unsigned long long *g = xg + kMHopOff[MH_H1] + ((size_t)n * 512 + 16 * c + u) * 4;
-        const uint32_t tg = (uint32_t)ts + 1u;
-        const float ghr = gh1[u * NR + n], ghz = gh1[(16 + u) * NR + n], ghn = gh1[(32 + u) * NR + n];
-        xpub(g + 0, tg, (ghr + cst[MC_BHH1 + u]) + (p1[0] + cst[MC_BIH1 + u]));
-        xpub(g + 1, tg, (ghz + cst[MC_BHH1 + 16 + u]) + (p1[1] + cst[MC_BIH1 + 16 + u]));
-        xpub(g + 2, tg, p1[2] + cst[MC_BIH1 + 32 + u]);
-        xpub(g + 3, tg, ghn + cst[MC_BHH1 + 32 + u]);
-    };
-    // waves 2 and 3: every unit's terms of step ts → sgl [n][512][4] (2 048 granules per row), all
-    // of a wave's loads in flight at once: two rows — wave 2 row 0, wave 3 row 1; one row — half each
-    auto gather_s = [&](int ts) {
-        const uint32_t tg = (uint32_t)ts + 1u;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        auto put = [&](int base) {
-            return [=](int i, float v0, float v1) { *reinterpret_cast<f2v *>(sgl + base + i) = f2v{v0, v1}; };
-        };
-        if (RX == 2) {
-            const int base = (wave - 2) * 2048;
-            xgather16<16>(xg + kMHopOff[MH_H1] + base, tg, a.ctl, a.timeout_ticks, ts, MH_H1, abort_flag, lane, put(base));
-        } else {
-            const int base = (wave - 2) * 1024;
-            xgather16<8>(xg + kMHopOff[MH_H1] + base, tg, a.ctl, a.timeout_ticks, ts, MH_H1, abort_flag, lane, put(base));
-        }
-    };
-    if constexpr (kLoc) {
-        if (wave == 1 && (lane >> 4) < RX) {
-            float p1[3];
-#pragma unroll
-            for (int q = 0; q < 3; ++q) p1[q] = TERMS(a.t0, lane >> 4)[XT_P1 + (lane & 15) * 3 + q];
-            publish_s(a.t0, p1);
-        }
-        if (wave >= 2) gather_s(a.t0);
-        __syncthreads();
-        if (*abort_flag) return;
-    }
-
     for (int t = a.t0; t < t_end; ++t) {
         // per-thread indices re-derived every step from an opaque copy of threadIdx.x: otherwise
         // hipcc hoists every per-thread address out of the loop and keeps them all live in VGPRs,
@@ -662,28 +600,7 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         if (kDbg && lane == 0 && (unsigned)(t - a.t0 - kMDbgSkip) < (unsigned)kMDbgSteps)
             dbgs[((t - a.t0 - kMDbgSkip) * kMWaves + wave) * kMStamps + kMStamps - 1] = (unsigned)__builtin_amdgcn_s_memrealtime();
         // ---- A: GRU1 (:208-210) of unit gu, row gn: W_ih1·x_I is rank-1 in x given the terms
-        float p1n[3] = {0.0f, 0.0f, 0.0f};   // kLoc, wave 1: P1 of step t + 1 for the S publish in F
-        if constexpr (kLoc) {
-            if (wave == 1 && more && (lane >> 4) < RX) {
-#pragma unroll
-                for (int q = 0; q < 3; ++q) p1n[q] = TERMS(t + 1, lane >> 4)[XT_P1 + (lane & 15) * 3 + q];
-            }
-            if (gru) x = xs[gn];
-            // GRU1 of every unit j, row n < RX, straight into the h1 staging image of wave j / 128
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int pp = tid + 256 * i, n = pp >> 9, j = pp & 511;
-                if (n < RX) {
-                    const f4v s4 = lds4(sgl + pp * 4);
-                    const float xn = xs[n];
-                    const float r = sigmoid_(fmaf(xn, q1s[j], s4.x));
-                    const float z = sigmoid_(fmaf(xn, q1s[512 + j], s4.y));
-                    const float nn = tanh_(fmaf(xn, q1s[1024 + j], s4.z) + s4.w * r);
-                    h1l[i] = (h1l[i] - nn) * z + nn;
-                    smem[ll.stg_h1 + (j >> 7) * kMStg + mstg_at(n, j & 127)] = h1l[i];
-                }
-            }
-        } else if (gru) {
+        if (gru) {
             x = xs[gn];
             const float *tr = rg + gn * kMRing;
             float sr, sz, gin, ghn;
@@ -703,12 +620,8 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         MST(1);
         // ---- B: the h1 slice → W_ih2[:, :R]·h1 (the GRU2 input gates, :213-214)
         {
-            if constexpr (kLoc) {
-                bar();
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                mgather<NQ>(xg + kMHopOff[MH_H1], stg_h1, wave, tag, a.ctl, a.timeout_ticks, t, MH_H1, abort_flag, lane);
-            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            mgather<NQ>(xg + kMHopOff[MH_H1], stg_h1, wave, tag, a.ctl, a.timeout_ticks, t, MH_H1, abort_flag, lane);
             MST(2);
             mlayer_any<NQ, MS_IH2, 3>(A, stg_h1, pbig, lane, wave);
             MST(3);
@@ -726,7 +639,6 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
                 gh[q] = gh2[i * NR + gn] + cst[MC_BHH2 + i];
             }
             h2v = gru_gate_math(gi[0], gi[1], gi[2], gh[0], gh[1], gh[2], h2v);
-            if constexpr (kLoc) h1v = smem[ll.stg_h1 + ((16 * c + gu) >> 7) * kMStg + mstg_at(gn, (16 * c + gu) & 127)];
             const float xi = fmaf(cst[MC_WI0 + gu], x, tr[XT_CI + gu]);
             const float y = (xi + h1v) + h2v;
             xpub(xg + kMHopOff[MH_Y] + gn * 512 + 16 * c + gu, tag, y);
@@ -759,14 +671,6 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
                     const int i = q * 16 + gu;
                     gh1[i * NR + gn] = mpart<NQ>(phh1, i, gn);
                 }
-            }
-        }
-        if constexpr (kLoc) {   // wave 1: Σ W_hh1·h1 of the own units → gh1, the terms of step t + 1 out
-            if (wave == 1 && (lane >> 4) < RX) {
-                const int u = lane & 15, n = lane >> 4;
-#pragma unroll
-                for (int q = 0; q < 3; ++q) gh1[(q * 16 + u) * NR + n] = mpart<NQ>(phh1, q * 16 + u, n);
-                if (more) publish_s(t + 1, p1n);
             }
         }
         MST(10);
@@ -888,12 +792,10 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
             const int na = (kMWaves - aux_w0) * 64;
             for (int e = tid - aux_w0 * 64; e < 3 * 16 * NR; e += na) {
                 const int i = e / NR, n = e - i * NR;
-                if (!kLoc) gh1[e] = mpart<NQ>(phh1, i, n);   // (kLoc: wave 1 took them in F)
+                gh1[e] = mpart<NQ>(phh1, i, n);
                 gh2[e] = mpart<NQ>(pbig, i, n);
             }
         }
-        // kLoc: every unit's GRU1 terms of step t + 1 (published in F) while the rows are sampled
-        if (kLoc && more && wave >= 2) gather_s(t + 1);
         MST(19);
         // ---- J: sample (:225-229; RAW :231-237) row n of this XCD, wave-uniform x
         const float *nz = nz_at(t);
@@ -971,13 +873,6 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         }
     }
     if (tid < RX) st[2048 + tid] = xs[tid];
-    if constexpr (kLoc) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int pp = tid + 256 * i;
-            if ((pp >> 9) < RX) st[kMStateBase + pp] = h1l[i];
-        }
-    }
 }
 
 // The in-kernel Philox draws of launch rows [0, nb) for steps [t0, t0 + Lc) into the injected-noise
@@ -1000,42 +895,34 @@ hipError_t launch_philox_fill(float *out, unsigned long long seed, long long row
     return hipGetLastError();
 }
 
-// RAW kernels have no stamp variant (the stamp buffer does not fit LDS beside the fc3 operands);
-// the local-GRU1 form (loc) exists for one quad only
-static const void *xcdm_kernel(int nq, bool dbg, bool raw, bool loc = false) {
+// RAW kernels have no stamp variant (the stamp buffer does not fit LDS beside the fc3 operands)
+static const void *xcdm_kernel(int nq, bool dbg, bool raw) {
     static const void *k[3][kMQuadMax] = {
-        {(const void *)fatchord_xcdm_kernel<1, false, false, false>, (const void *)fatchord_xcdm_kernel<2, false, false, false>,
-         (const void *)fatchord_xcdm_kernel<3, false, false, false>, (const void *)fatchord_xcdm_kernel<4, false, false, false>},
-        {(const void *)fatchord_xcdm_kernel<1, true, false, false>, (const void *)fatchord_xcdm_kernel<2, true, false, false>,
-         (const void *)fatchord_xcdm_kernel<3, true, false, false>, (const void *)fatchord_xcdm_kernel<4, true, false, false>},
-        {(const void *)fatchord_xcdm_kernel<1, false, true, false>, (const void *)fatchord_xcdm_kernel<2, false, true, false>,
-         (const void *)fatchord_xcdm_kernel<3, false, true, false>, (const void *)fatchord_xcdm_kernel<4, false, true, false>}};
-    static const void *kl[3] = {(const void *)fatchord_xcdm_kernel<1, false, false, true>,
-                                (const void *)fatchord_xcdm_kernel<1, true, false, true>,
-                                (const void *)fatchord_xcdm_kernel<1, false, true, true>};
-    const int v = raw ? 2 : dbg ? 1 : 0;
-    if (loc && nq == 1) return kl[v];
-    return k[v][nq < 1 ? 0 : nq > kMQuadMax ? kMQuadMax - 1 : nq - 1];
+        {(const void *)fatchord_xcdm_kernel<1, false, false>, (const void *)fatchord_xcdm_kernel<2, false, false>,
+         (const void *)fatchord_xcdm_kernel<3, false, false>, (const void *)fatchord_xcdm_kernel<4, false, false>},
+        {(const void *)fatchord_xcdm_kernel<1, true, false>, (const void *)fatchord_xcdm_kernel<2, true, false>,
+         (const void *)fatchord_xcdm_kernel<3, true, false>, (const void *)fatchord_xcdm_kernel<4, true, false>},
+        {(const void *)fatchord_xcdm_kernel<1, false, true>, (const void *)fatchord_xcdm_kernel<2, false, true>,
+         (const void *)fatchord_xcdm_kernel<3, false, true>, (const void *)fatchord_xcdm_kernel<4, false, true>}};
+    return k[raw ? 2 : dbg ? 1 : 0][nq < 1 ? 0 : nq > kMQuadMax ? kMQuadMax - 1 : nq - 1];
 }
 
-hipError_t launch_xcdm(const XcdmArgs &a, int nq, bool raw, bool loc, hipStream_t st) {
+hipError_t launch_xcdm(const XcdmArgs &a, int nq, bool raw, hipStream_t st) {
     XcdmArgs args = a;
     void *params[] = {&args};
     const bool dbg = !raw && a.dbg != nullptr;
-    loc = loc && nq == 1;
-    const void *kf = xcdm_kernel(nq, dbg, raw, loc);
+    const void *kf = xcdm_kernel(nq, dbg, raw);
     return hipLaunchKernel(kf, dim3(kXcds * kXcdWgs), dim3(kMThreads), params,
-                           xcdm_lds_layout(nq, dbg, raw, loc).total * sizeof(float), st);
+                           xcdm_lds_layout(nq, dbg, raw).total * sizeof(float), st);
 }
 
 hipError_t prepare_xcdm_kernel(int max_lds_bytes) {
     for (int v = 0; v < 3; ++v)
-        for (int nq = 1; nq <= kMQuadMax; ++nq)
-            for (int loc = 0; loc < (nq == 1 ? 2 : 1); ++loc) {
-                hipError_t e = hipFuncSetAttribute(xcdm_kernel(nq, v == 1, v == 2, loc == 1),
-                                                   hipFuncAttributeMaxDynamicSharedMemorySize, max_lds_bytes);
-                if (e != hipSuccess) return e;
-            }
+        for (int nq = 1; nq <= kMQuadMax; ++nq) {
+            hipError_t e = hipFuncSetAttribute(xcdm_kernel(nq, v == 1, v == 2), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               max_lds_bytes);
+            if (e != hipSuccess) return e;
+        }
     return hipSuccess;
 }
 
@@ -1053,21 +940,6 @@ hipError_t xcdm_max_quads(int max_lds_bytes, bool raw, int *nq_max) {
         }
         *nq_max = nq;
     }
-    return hipSuccess;
-}
-
-// whether the local-GRU1 one-quad form is co-resident (its LDS adds the terms of every unit)
-hipError_t xcdm_loc_ok(int max_lds_bytes, bool raw, bool *ok) {
-    *ok = false;
-    for (int dbg = 0; dbg < (raw ? 1 : 2); ++dbg) {
-        const size_t lds = xcdm_lds_layout(1, dbg, raw, true).total * sizeof(float);
-        if (lds > (size_t)max_lds_bytes) return hipSuccess;
-        int n = 0;
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, xcdm_kernel(1, dbg, raw, true), kMThreads, lds);
-        if (e != hipSuccess) return e;
-        if (n < 1) return hipSuccess;
-    }
-    *ok = true;
     return hipSuccess;
 }
 
