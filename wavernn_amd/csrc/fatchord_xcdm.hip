@@ -312,7 +312,8 @@ template <int NQ, int S0, int NS, typename Hook = MPollNone>
 __device__ __forceinline__ void mlayer_any(const float (&A)[kMSets][kMJ], const float *stg, float *P, int lane, int wave,
                                            Hook &&hook = Hook{}) {
     // (16x16x4: ≥ 3 sets interleaved already cover its ≈ 40-cycle dependent latency)
-    if constexpr (xcdm_big(NQ)) mlayer16<NQ, S0, NS, 2>(A, stg, P, lane, wave, hook);
+    // (one set: four chains, so the ≈ 40-cycle dependent latency never stalls the 32-cycle issue)
+    if constexpr (xcdm_big(NQ)) mlayer16<NQ, S0, NS, NS == 1 ? 4 : 2>(A, stg, P, lane, wave, hook);
     else mlayer<NQ, S0, NS, MChains<NQ, NS>::v>(A, stg, P, lane, wave, hook);
 }
 // one set whose A operands are in LDS (RAW fc3); partials in the set-0 slot of P
