@@ -1,0 +1,69 @@
+"""§8(f)4: the training-side teacher-forced forward (models/fatchord_version.py:131-167;
+deepmind_version.py:36-72) runs on the MI355X with the GRUs on MIOpen (torch.nn.GRU on ROCm) —
+forward and backward against the same module on the CPU (ATen), fp32 tolerances for the
+different GRU kernels' summation orders."""
+import numpy as np
+import pytest
+import torch
+
+from wavernn_amd import synthetic as syn
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _pair(d, seed):
+    from wavernn_amd.fatchord_version import WaveRNN
+    state = {k: torch.from_numpy(np.array(v)) for k, v in syn.make_fatchord_state(d, seed).items()}
+    cpu = WaveRNN(**d.ctor_kwargs())
+    cpu.load_state_dict(state)
+    gpu = WaveRNN(**d.ctor_kwargs()).to(DEV)
+    gpu.load_state_dict(state)
+    return cpu, gpu
+
+
+@pytest.mark.parametrize("mode", ["MOL", "RAW"])
+def test_fatchord_training_forward_backward_on_miopen(mode):
+    d = syn.DEFAULT_MOL if mode == "MOL" else syn.DEFAULT_RAW
+    cpu, gpu = _pair(d, 5)
+    cpu.eval()
+    gpu.eval()
+    g = np.random.default_rng(3)
+    B, T = 2, 4
+    mel = torch.from_numpy(g.uniform(0, 1, (B, d.feat_dims, T + 2 * d.pad)).astype(np.float32))
+    x = torch.from_numpy(g.uniform(-1, 1, (B, T * d.hop_length)).astype(np.float32))
+    yc = cpu(x, mel)
+    yg = gpu(x.to(DEV), mel.to(DEV))
+    assert yg.shape == yc.shape
+    assert (yg.detach().cpu() - yc.detach()).abs().max().item() <= 1e-4
+    # backward through MIOpen's GRU (training mode: BatchNorm on batch statistics in both)
+    cpu.train()
+    gpu.train()
+    yc = cpu(x, mel)
+    yg = gpu(x.to(DEV), mel.to(DEV))
+    assert (yg.detach().cpu() - yc.detach()).abs().max().item() <= 1e-4
+    yc.square().mean().backward()
+    yg.square().mean().backward()
+    for (n, pc), (_, pg) in zip(cpu.named_parameters(), gpu.named_parameters()):
+        if pc.grad is None:
+            continue
+        err = (pg.grad.cpu() - pc.grad).abs().max().item()
+        assert err <= 1e-4 * max(1.0, pc.grad.abs().max().item()), (n, err)
+
+
+def test_deepmind_training_forward_on_gpu():
+    from wavernn_amd.deepmind_version import WaveRNN
+    d = syn.DEFAULT_DM
+    state = {k: torch.from_numpy(np.array(v)) for k, v in syn.make_deepmind_state(d, 6).items()}
+    cpu = WaveRNN(**d.ctor_kwargs())
+    cpu.load_state_dict(state)
+    gpu = WaveRNN(**d.ctor_kwargs()).to(DEV)
+    gpu.load_state_dict(state)
+    g = np.random.default_rng(4)
+    prev_y = torch.from_numpy(g.uniform(-1, 1, (3, 2)).astype(np.float32))
+    prev_hidden = torch.from_numpy(g.uniform(-1, 1, (3, d.hidden_size)).astype(np.float32))
+    current_coarse = torch.from_numpy(g.uniform(-1, 1, (3, 1)).astype(np.float32))
+    outc = cpu(prev_y, prev_hidden, current_coarse)
+    outg = gpu(prev_y.to(DEV), prev_hidden.to(DEV), current_coarse.to(DEV))
+    for a, b in zip(outc, outg):
+        assert (b.detach().cpu() - a.detach()).abs().max().item() <= 1e-5
