@@ -15,6 +15,7 @@ of the conditioning terms, the slab prologue), so `bytes` = 2 x FETCH + WRITE; b
 `bytes` as `roofline.traffic`.  The rows kernels add 4-byte flag and 8-byte granule polls
 (uncalibrated widths) beside their 16-B tile LDS-DMA: their per-step figures are approximate."""
 import csv
+import re
 import json
 import sys
 
@@ -46,8 +47,13 @@ def loop_dispatch(path):
 def other_sums(path):
     out = {}
     for r in rows(path):
+        name = r["Kernel_Name"]
+        # the many-row kernel's RAW instantiations (<NQ, dbg, true>: bench.py's config-1 lines)
+        # are not config 3's
+        if "fatchord_xcdm_kernel" in name and re.search(r"fatchord_xcdm_kernel<\d+, \w+, true>", name):
+            continue
         for k in OTHER:
-            if k in r["Kernel_Name"]:
+            if k in name:
                 out[k] = out.get(k, 0.0) + float(r["Counter_Value"])
     return out
 
