@@ -1,4 +1,4 @@
-"""Static check of the inline-asm MFMAs in fatchord_xcdm.hip and deepmind_xcd.hip (hipcc does not
+"""Static check of the inline-asm MFMAs in fatchord_xcdm.hip (MoL and RAW heads) and deepmind_xcd.hip (hipcc does not
 pad hazards around inline asm): no VALU write to an MFMA source within 2 wait states before it,
 no non-MFMA read of an MFMA result within 8 (4x4x1) / 19 (16x16x4) wait states after it.
 Compiles the device asm of both files itself (hipcc, gfx950) into /tmp.
@@ -10,7 +10,8 @@ import subprocess
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = [("fatchord_xcdm.hip", ["_ZN4wrnn20fatchord_xcdm_kernelILi%sELb0EEEvNS_8XcdmArgsE" % q for q in "1234"]),
+KERNELS = [("fatchord_xcdm.hip", ["_ZN4wrnn20fatchord_xcdm_kernelILi%sELb0ELb%dEEEvNS_8XcdmArgsE" % (q, raw)
+                                   for q in "1234" for raw in (0, 1)]),
            ("deepmind_xcd.hip", ["_ZN4wrnn19deepmind_xcd_kernelILb0EEEvNS_6DxArgsE"])]
 def regs(tok):
     # expand v5 / v[4:7] / a3 / a[0:3]
