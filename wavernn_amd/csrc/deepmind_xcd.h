@@ -104,7 +104,7 @@ constexpr int kDxAL = kDxA - DA_RQ;   // 42
 __host__ __device__ inline DxLds dx_lds_layout(bool dbg = false) {
     DxLds l;
     int o = 0;
-    l.stg = o;  o += 2 * kDxWaves * 4 * kDxST;     // staged slices: [h_c then h_f | o1 then o3][wave][n][kDxST]
+    l.stg = o;  o += 3 * kDxWaves * 4 * kDxST;     // staged slices: [h_f | o1 then o3 | h_c][wave][n][kDxST]
     l.ao = o;   o += kDxWaves * kDxAL * 64;
     l.pr = o;   o += kDxPR;
     l.prq = o;  o += kDxPRQ;

@@ -92,6 +92,11 @@ __device__ __forceinline__ void dx_stage(float *stg, int lane, const u4v (&v)[4]
     }
 }
 
+// no poll riding along
+struct MPollNoneDx {
+    __device__ __forceinline__ void step(int) {}
+};
+
 // A poll that rides along an MFMA layer: loads issued at chunk kAt, checked after the layer
 // (fallback: the bounded blocking poll), as MPoll in fatchord_xcdm.hip
 template <int kAt>
@@ -175,9 +180,11 @@ __device__ __forceinline__ void dx_o24(const float *Al, const float *stg, float 
 }
 
 // One half (kHalf 0: coarse columns from h_c, 1: fine columns from h_f) of R·h over the wave's
-// 112 columns: 5 sets (sets 0..3 AGPR, set 4 VGPR) × 28 MFMAs + the quarter set's 7 (A from
-// LDS), one chain per set continued across the halves; hook.step(c) at each of the 7 chunks
-template <int kHalf, typename Hook>
+// 112 columns for the sets [S0, S1) (sets 0..3 AGPR, set 4 VGPR; 28 MFMAs each) and, with kQ,
+// the quarter set's 7 (A from LDS); one chain per set continued across the halves; hook.step(c)
+// at each of the 7 chunks.  Two row groups run in different windows of the step (below): sets
+// 0..2 (WG-local rows 0..47: every coarse gate row) and sets 3, 4 + the quarter (rows 48..83).
+template <int kHalf, int S0, int S1, bool kQ, typename Hook>
 __device__ __forceinline__ void dx_rhalf(const float (&AR)[5][56], const float *ARQl, const float *stg,
                                          f4v (&accR)[5], f4v &accQ, int lane, Hook &hook) {
     const int j = lane & 3, sp = lane >> 4, b = lane >> 2;
@@ -189,12 +196,16 @@ __device__ __forceinline__ void dx_rhalf(const float (&AR)[5][56], const float *
     for (int c = 0; c < 7; ++c) {
         hook.step(c);
         if (c + 1 < 7) bb[(c + 1) & 1] = lds4(bp + 4 * (c + 1));
-        const float qv = bq[c], qa = ARQl[(7 * kHalf + c) * 64 + lane];
+        float qv = 0.0f, qa = 0.0f;
+        if constexpr (kQ) {
+            qv = bq[c];
+            qa = ARQl[(7 * kHalf + c) * 64 + lane];
+        }
 #pragma unroll
         for (int mm = 0; mm < 4; ++mm) {
             const int m = 4 * c + mm;
 #pragma unroll
-            for (int s = 0; s < 5; ++s) {
+            for (int s = S0; s < S1; ++s) {
                 const float a = AR[s][28 * kHalf + m], x = bb[c & 1][mm];
                 if (kHalf == 0 && m == 0) {
                     if (s < 4) mfma_first<true>(accR[s], a, x);
@@ -205,31 +216,37 @@ __device__ __forceinline__ void dx_rhalf(const float (&AR)[5][56], const float *
                 }
             }
         }
-        if (kHalf == 0 && c == 0) mfma_first<false>(accQ, qa, qv);
-        else mfma_acc<false>(accQ, qa, qv);
+        if constexpr (kQ) {
+            if (kHalf == 0 && c == 0) mfma_first<false>(accQ, qa, qv);
+            else mfma_acc<false>(accQ, qa, qv);
+        }
     }
 }
 
-// R·h partials → LDS: sets [set][wave][row 16][n (+1)][k-slice 4], quarter [wave][row 4][n][16]
+// R·h partials of the sets [S0, S1) (+ the quarter set) → LDS: sets [set][wave][row 16][n (+1)][k-slice 4],
+// quarter [wave][row 4][n][16]
+template <int S0, int S1, bool kQ>
 __device__ __forceinline__ void dx_rput(f4v (&accR)[5], f4v &accQ, float *PR, float *PRQ, int lane, int wave) {
     mfma_drain_begin();
 #pragma unroll
-    for (int s = 0; s < 5; ++s) mfma_tie(accR[s]);
-    mfma_tie(accQ);
+    for (int s = S0; s < S1; ++s) mfma_tie(accR[s]);
+    if constexpr (kQ) mfma_tie(accQ);
     const int j = lane & 3, g = (lane >> 2) & 3, sp = lane >> 4, b = lane >> 2;
 #pragma unroll
-    for (int s = 0; s < 5; ++s) {
+    for (int s = S0; s < S1; ++s) {
         float *p = PR + ((s * kDxWaves + wave) * 16 + 4 * g) * 20 + 4 * j + sp;
         p[0] = accR[s].x;
         p[20] = accR[s].y;
         p[40] = accR[s].z;
         p[60] = accR[s].w;
     }
-    float *q = PRQ + (wave * 16 + j) * 16 + b;   // [wave][row i][n j][slice b]: row stride 64
-    q[0] = accQ.x;
-    q[64] = accQ.y;
-    q[128] = accQ.z;
-    q[192] = accQ.w;
+    if constexpr (kQ) {
+        float *q = PRQ + (wave * 16 + j) * 16 + b;   // [wave][row i][n j][slice b]: row stride 64
+        q[0] = accQ.x;
+        q[64] = accQ.y;
+        q[128] = accQ.z;
+        q[192] = accQ.w;
+    }
 }
 
 // Σ over waves and k-slices of WG-local R row rr (0..83), batch row n — fixed order
@@ -349,8 +366,8 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
     for (int i = tid; i < kDxPRQ; i += kDxThreads) prq[i] = resume ? st[8 * kDxU + kDxPR + i] : 0.0f;
     if (tid < 16) lab[tid] = (resume && tid < 8) ? st[8 * kDxU + kDxPR + kDxPRQ + tid] : 0.0f;   // out_coarse = out_fine = 0 (:89-90)
     // Σ R·h of every own gate row (WG-local row rr, batch row n) → rs[rr·4 + n], from the partials
-    auto r_sums = [&](int e0, int de) {
-        for (int e = e0; e < 84 * 4; e += de) rs[e] = dx_rsum(pr, prq, e >> 2, e & 3);
+    auto r_sums = [&](int e0, int de, int r0, int r1) {
+        for (int e = r0 * 4 + e0; e < r1 * 4; e += de) rs[e] = dx_rsum(pr, prq, e >> 2, e & 3);
     };
     float hc = 0.0f, hf = 0.0f;   // h of (unit gu, row gn): this thread's recurrent state
     if (gate && resume) {
@@ -363,8 +380,17 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             log4(*reinterpret_cast<const f4v *>(noise_src(a.t0, n) + 4 * f));
     }
     __syncthreads();
-    r_sums(tid, kDxThreads);
+    r_sums(tid, kDxThreads, 0, 84);
     __syncthreads();
+
+    // R[rows 48..83, :]·h of the staged h_c (stg_of(2)) and h_f (stg_of(0)) slices → partials
+    auto r_group_b = [&]() {
+        f4v bR[5], bQ;
+        MPollNoneDx none;
+        dx_rhalf<0, 3, 5, true>(AR, arq, stg_of(2), bR, bQ, lane, none);
+        dx_rhalf<1, 3, 5, true>(AR, arq, stg_of(0), bR, bQ, lane, none);
+        dx_rput<3, 5, true>(bR, bQ, pr, prq, lane, wave);
+    };
 
     constexpr int kNzF4 = 2 * kDxQ / 4;                         // float4s of one row's draws
     // draws loaded by waves 1..3 (wave 0 publishes the O1 epilogue meanwhile)
@@ -397,13 +423,17 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             hc = uu * hc + (1.0f - uu) * ee;
             xpub(xg + kDxHopOff[DX_HC] + gn * kDxS + kDxU * c + gu, tag, hc);
         }
+        // row group B (WG-local rows 48..83: fine gate rows only) of R·h_{t-1}, both halves from the
+        // still-staged h_c(t-1) / h_f(t-1) slices: waves 1..3 while wave 0 runs the coarse gates,
+        // wave 0 in its h_c hop wait; partials → LDS (summed in this step's O2 epilogue window)
+        if (t > a.t0) r_group_b();
         DST(1);
         // ---- h_c slice → O1 → relu → o1
         {
             u4v v[4];
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             dx_poll(hop_rsrc(xg + kDxHopOff[DX_HC]), wave, tag, a.ctl, a.timeout_ticks, t, DX_HC, abort_flag, lane, v);
-            dx_stage(stg_of(0), lane, v);
+            dx_stage(stg_of(2), lane, v);
         }
         // the draws of step t + 1 → registers of waves 1..3; their logs go into the ring while
         // wave 0 publishes o1 (below)
@@ -420,7 +450,7 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             }
         }
         DST(2);
-        dx_o13<true>(AO1, stg_of(0), po1, lane, wave);
+        dx_o13<true>(AO1, stg_of(2), po1, lane, wave);
         bar();
         DST(3);
         if (tid < 4 * kDxU) {
@@ -439,11 +469,12 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             }
         }
         DST(4);
-        // ---- R[:, :S]·h_c (next step's R·h, coarse half) with the o1 poll riding along
+        // ---- R[rows 0..47, :S]·h_c (next step's R·h, coarse half of row group A) with the o1 poll
+        // riding along; group B (rows 48..83) runs at the start of the next step
         f4v accR[5], accQ;
         {
             DxRide<4> po(xg + kDxHopOff[DX_O1], wave, tag, lane);
-            dx_rhalf<0>(AR, arq, stg_of(0), accR, accQ, lane, po);
+            dx_rhalf<0, 0, 3, false>(AR, arq, stg_of(2), accR, accQ, lane, po);
             DST(5);
             po.finish(a.ctl, a.timeout_ticks, t, DX_O1, abort_flag);
             dx_stage(stg_of(1), lane, po.v);
@@ -456,6 +487,8 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         if (tid < 4 * kDxUO2) {
             const int r = tid % kDxUO2, n = tid / kDxUO2;
             xpub(xg + kDxHopOff[DX_LC] + n * kDxQ + kDxUO2 * c + r, tag, dx_o24sum(po2, r, n) + cst[DC_B2 + r]);
+        } else if (tid >= 64 && t > a.t0) {
+            r_sums(tid - 64, kDxThreads - 64, 48, 84);   // group B of R·h_{t-1} (partials from this step's start)
         }
         DST(8);
         // ---- sample c_t (:129-131): wave n samples row n
@@ -533,11 +566,12 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             xpub(xg + kDxHopOff[DX_O3] + n * kDxS + kDxU * c + r, tag, o > 0.0f ? o : 0.0f);
         }
         DST(13);
-        // ---- R[:, S:]·h_f finishes R·h_t (the gates above have read R·h_{t-1}) → LDS partials
+        // ---- R[rows 0..47, S:]·h_f finishes group A of R·h_t (the gates above have read R·h_{t-1})
+        // → LDS partials
         {
             DxRide<4> po(xg + kDxHopOff[DX_O3], wave, tag, lane);
-            dx_rhalf<1>(AR, arq, stg_of(0), accR, accQ, lane, po);
-            dx_rput(accR, accQ, pr, prq, lane, wave);
+            dx_rhalf<1, 0, 3, false>(AR, arq, stg_of(0), accR, accQ, lane, po);
+            dx_rput<0, 3, false>(accR, accQ, pr, prq, lane, wave);
             DST(14);
             po.finish(a.ctl, a.timeout_ticks, t, DX_O3, abort_flag);
             dx_stage(stg_of(1), lane, po.v);
@@ -551,7 +585,7 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             const int r = tid % kDxUO2, n = tid / kDxUO2;
             xpub(xg + kDxHopOff[DX_LF] + n * kDxQ + kDxUO2 * c + r, tag, dx_o24sum(po4, r, n) + cst[DC_B4 + r]);
         } else if (tid >= 64) {
-            r_sums(tid - 64, kDxThreads - 64);   // R·h_t (complete since the barrier) for step t + 1's gates
+            r_sums(tid - 64, kDxThreads - 64, 0, 48);   // group A of R·h_t (complete since the barrier)
         }
         DST(17);
         // ---- sample f_t (:149-151); combine_signal (utils/dsp.py:33); previous labels ← (c_t, f_t)
@@ -573,6 +607,9 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         bar();
         if (*abort_flag) return;
     }
+    // row group B of the last step's R·h (the next chunk starts from complete partials)
+    if (a.Lc > 0) r_group_b();
+    __syncthreads();
     if (kDbg && a.dbg) {
         __syncthreads();
         for (int i = tid; i < kDxDbgSteps * kDxWaves * kDxStamps; i += kDxThreads) {
