@@ -2279,11 +2279,11 @@ int wrnn_check(wrnn_t *h, void *stream) {
                                         "coarse label", "fine label"};
         static const char *split_hops[] = {"y", "f1", "f2", "h2", "h2", "gru1-terms", "gru1-terms"};
         static const char *xcd_hops[] = {"y", "f1", "f2", "h2", "gru1-terms", "gru1-terms"};
-        static const char *xcdm_hops[] = {"h1", "y", "h2", "f1", "f2 (partial logits)", "x"};
+        static const char *xcdm_hops[] = {"h1", "y", "h2", "f1", "f2 (partial logits)", "x", "logits"};
         const int lp = h->last_path;
         const char *name = lp == 8 || lp == 3 || lp == 10 ? (hop >= 0 && hop < 8 ? dm_hops[hop] : "?")
                            : lp == 2 || lp == 9         ? (hop >= 0 && hop < 6 ? row_hops[hop] : "?")
-                           : lp == 7                    ? (hop >= 0 && hop < 6 ? xcdm_hops[hop] : "?")
+                           : lp == 7                    ? (hop >= 0 && hop < 7 ? xcdm_hops[hop] : "?")
                            : lp >= 5                    ? (hop >= 0 && hop < 6 ? xcd_hops[hop] : "?")
                            : lp == 4                    ? (hop >= 0 && hop < 7 ? split_hops[hop] : "?")
                                                         : (hop >= 0 && hop < 7 ? lat_hops[hop] : "?");
