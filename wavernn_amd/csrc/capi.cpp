@@ -1738,7 +1738,8 @@ int generate_xcdm(wrnn_t *h, const float *cond, int B, int L, const float *noise
         if (grow(h, h->d_X, h->X_cap, (size_t)Lc_max * nb * h->KXc) || grow(h, h->d_T, h->T_cap, (size_t)Lc_max * nb * N) ||
             (!noise && grow(h, h->d_xmnoise, h->xmnoise_cap, (size_t)Lc_max * nb * NK)))
             return WRNN_EHIP;
-        HIP_TRY(h, hipMemsetAsync(h->d_xmxg, 0, xg_words * 8, st));   // tags restart at 1
+        // tags restart at 1, every packed hop element empty (fatchord_xcdm.h: all bits set)
+        HIP_TRY(h, hipMemsetAsync(h->d_xmxg, 0xFF, xg_words * 8, st));
         for (int t0 = 0; t0 < L; t0 += Lc_max) {
             const int Lc = std::min(Lc_max, L - t0);
             if ((size_t)Lc * nb * h->KXc > h->X_cap || (size_t)Lc * nb * N > h->T_cap)

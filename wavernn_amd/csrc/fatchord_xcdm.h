@@ -24,7 +24,7 @@ constexpr int kMRowsXcd = 4 * kMQuadMax;   // rows per XCD
 constexpr int kMRowsMax = kXcds * kMRowsXcd;   // rows per launch (128 ≥ config 3's 115 folds)
 constexpr int kMK = 512 / kMWaves;         // K window of a wave: wave w multiplies columns [kMK·w, kMK·(w + 1))
 constexpr int kMJ = kMK / 4;               // MFMAs per set and quad (4 k-slices of kMJ columns)
-constexpr int kMPL = kMK / 32;             // 16-byte poll loads per lane and quad (4 rows × kMK granules)
+constexpr int kMPP = kMK / 64;             // 16-byte poll loads per lane and quad (4 rows × kMK packed floats)
 
 // The eleven 16-row weight sets a workgroup c multiplies (rows of its units 16c..16c+15 / fc rows
 // 16c..16c+15), register-resident as MFMA A operands (16 per set and wave: kMK / 4 k-slices)
@@ -34,16 +34,26 @@ enum MSet { MS_IH2 = 0, MS_FC1 = 3, MS_FC2 = 4, MS_HH2 = 5, MS_HH1 = 8, kMSets =
 // A operand of set s, MFMA j (0..kMJ-1), lane l = 4b + j4 (block b = 4s' + g: row group g = b & 3,
 // k-slice s' = b >> 2): W_s[row 4g + j4][kMK·w + kMJ·s' + j]  (slab [kMWaves][11][kMJ][64 lanes])
 
-// Hand-off vectors of one XCD.  Row n (0..15) of the XCD = launch row k + 8n.  Granules
-// {tag = step + 1, value}: H1 / Y / H2 / F1 at n·512 + j (unit or fc row j); F2 (partial logits
-// of producer c) at (n·32 + c)·32 + j, j < 32 (30, 31 zero); X (two-level sampler) at n.
-// RAW: F2 holds the f2 vectors (n·512 + j) and LG the logits (n·512 + class).
+// Hand-off vectors of one XCD.  Row n (0..15) of the XCD = launch row k + 8n.
+// Tagged granules {tag = step + 1, value}: F2 (MoL partial logits of producer c) at
+// (n·32 + c)·32 + j, j < 32 (30, 31 zero); X (two-level sampler) at n; RAW: LG the logits
+// (n·512 + class).
+// Packed vectors (untagged fp32, two slots by step parity, kMPackOff granules in): H1 / Y / H2 /
+// F1 (RAW: and the f2 vector, MH_F2) at slot·kMVec + n·512 + j (unit or fc row j).  An empty
+// element holds kMEmpty (a NaN bit pattern no fp32 operation produces); the producer of an
+// element empties the other slot once its B poll of step t has seen every workgroup's h1_t —
+// by then every consumer has read all of step t - 1 — and a later publish of its own orders the
+// clear before step t + 1's polls.  Twice the values per 16-byte poll of the tagged form.
 enum MHop { MH_H1 = 0, MH_Y = 1, MH_H2 = 2, MH_F1 = 3, MH_F2 = 4, MH_X = 5, MH_LG = 6, kMHops = 7 };
+constexpr int kMPacked = 5;                // packed vectors: MH_H1 .. MH_F2
+constexpr uint32_t kMEmpty = 0xFFFFFFFFu;
 constexpr long long kMVec = (long long)kMRowsXcd * 512;
 constexpr long long kMF2 = (long long)kMRowsXcd * kXcdWgs * 32;   // >= kMVec
 constexpr long long kMHopOff[kMHops] = {0, kMVec, 2 * kMVec, 3 * kMVec, 4 * kMVec, 4 * kMVec + kMF2,
                                         4 * kMVec + kMF2 + 64};
-constexpr long long kMXcdStride = 5 * kMVec + kMF2 + 64;   // granules per XCD
+constexpr long long kMPackOff = 5 * kMVec + kMF2 + 64;           // granules: the packed area
+constexpr long long kMXcdStride = kMPackOff + kMPacked * kMVec;  // granules per XCD (packed: 2 floats each)
+// (every word of the area starts as 0xFFFFFFFF: an empty packed element, a tag no step carries)
 constexpr int kMRawNC = 512;        // RAW classes (bits = 9)
 // MoL fc3 partials: the 16 fc3 columns of a logit and the 16 own f2 rows of a batch row are each
 // read as four ds_read_b128; rows padded to 20 floats so the 16 lanes of a b128 phase hit distinct banks
@@ -101,11 +111,11 @@ struct XcdmLds {
 // staging of a polled vector slice, per wave: [quad][4 rows][64], value k of row j4 at
 // j4·64 + (k ^ 4·j4) (the XOR keeps the B-operand reads of the four rows on distinct banks)
 constexpr int kMStg = 4 * kMK;
-// lane l's pair i (of kMPL·NQ): quad i / kMPL; pairs p = l + 64·(i % kMPL) cover the 4 rows of the
-// quad row-major (kMK / 2 pairs per row)
-__host__ __device__ constexpr int mpoll_row(int i) { return 4 * (i / kMPL) + (((i % kMPL) * 64) / (kMK / 2)); }
-__host__ __device__ inline int mpoll_col(int lane) { return 2 * (lane % (kMK / 2)); }
-__host__ __device__ inline int mpoll_lane_off(int lane) { return ((lane / (kMK / 2)) * 512 + mpoll_col(lane)) * 8; }
+// lane l's float4 i (of kMPP·NQ) of a packed vector slice: quad i / kMPP; float4s
+// p = l + 64·(i % kMPP) cover the 4 rows of the quad row-major (kMK / 4 per row)
+__host__ __device__ constexpr int mpoll_row(int i) { return 4 * (i / kMPP) + (((i % kMPP) * 64) / (kMK / 4)); }
+__host__ __device__ inline int mpoll_col(int lane) { return 4 * (lane % (kMK / 4)); }
+__host__ __device__ inline int mpoll_lane_off(int lane) { return ((lane / (kMK / 4)) * 512 + mpoll_col(lane)) * 4; }
 // staging position of (row j4, column kk): 4-float groups XOR-swizzled so that the B reads of the
 // 16 (row, k-slice) combinations of a wave instruction fall on distinct bank groups
 __host__ __device__ inline int mstg_at(int j4, int kk) {

@@ -59,21 +59,40 @@ __device__ __forceinline__ float sum8(const float *p) {
     return ((u.x + u.y) + (u.z + u.w)) + ((v.x + v.y) + (v.z + v.w));
 }
 
-// Poll wave w's slice [64w, 64w + 64) of a hop vector for every quad: lane l reads the granule
-// pairs (row 4q + 2h + (l >> 5), columns 64w + 2(l & 31) + {0, 1}), h = 0, 1.  Bounded.
+// A packed hop vector (fatchord_xcdm.h): the slot of step t, and its publish (a plain 4-byte
+// store that stays in the XCD's L2, as xpub)
+// (slot index made wave-uniform explicitly: otherwise the step-parity select is taken as
+// divergent and every poll's buffer descriptor sits in a waterfall loop)
+__device__ __forceinline__ float *pvec(unsigned long long *xg, int hop, int t) {
+    const int slot = __builtin_amdgcn_readfirstlane(2 * (hop - MH_H1) + (t & 1));
+    return reinterpret_cast<float *>(xg + kMPackOff) + (size_t)slot * kMVec;
+}
+__device__ __forceinline__ void ppub(float *p, float v) {
+    __hip_atomic_store(reinterpret_cast<unsigned *>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void pclear(float *p) {
+    __hip_atomic_store(reinterpret_cast<unsigned *>(p), kMEmpty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// all four floats of a polled float4 published (none still empty)
+__device__ __forceinline__ bool pfull(u4v v) {
+    return (v.x != kMEmpty) & (v.y != kMEmpty) & (v.z != kMEmpty) & (v.w != kMEmpty);
+}
+
+// Poll wave w's slice [kMK·w, kMK·w + kMK) of a packed hop vector for every quad: lane l reads
+// the float4s (row 4q + 2h + (l >> 5), columns kMK·w + 4(l & 31) + {0..3}), h = 0, 1.  Bounded.
 template <int NQ>
-__device__ __forceinline__ void mpoll(const unsigned long long *vec, int w, uint32_t tag, int *ctl, long long timeout,
-                                      int step, int hop, int *lds_abort, int lane, u4v (&v)[kMPL * NQ]) {
-    const __amdgpu_buffer_rsrc_t r = hop_rsrc(vec);
-    const int off = kMK * w * 8 + mpoll_lane_off(lane);
+__device__ __forceinline__ void mpoll(const float *vec, int w, int *ctl, long long timeout, int step, int hop,
+                                      int *lds_abort, int lane, u4v (&v)[kMPP * NQ]) {
+    const __amdgpu_buffer_rsrc_t r = hop_rsrc(reinterpret_cast<const unsigned long long *>(vec));
+    const int off = kMK * w * 4 + mpoll_lane_off(lane);
     const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
     unsigned spins = 0;
     for (;;) {
 #pragma unroll
-        for (int i = 0; i < kMPL * NQ; ++i) v[i] = ld16_sc1(r, off + mpoll_row(i) * 512 * 8);
+        for (int i = 0; i < kMPP * NQ; ++i) v[i] = ld16_sc1(r, off + mpoll_row(i) * 512 * 4);
         bool ok = true;
 #pragma unroll
-        for (int i = 0; i < kMPL * NQ; ++i) ok &= (v[i].y == tag) & (v[i].w == tag);
+        for (int i = 0; i < kMPP * NQ; ++i) ok &= pfull(v[i]);
         if (ok) return;
         if ((++spins & 63u) == 0) {
             const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - c0) > timeout;
@@ -87,29 +106,29 @@ __device__ __forceinline__ void mpoll(const unsigned long long *vec, int w, uint
     }
 }
 
-// polled pairs → the wave's staging area ([quad][row j4][64], XOR-swizzled by 4·j4)
+// polled float4s → the wave's staging area ([quad][row j4][64], XOR-swizzled by 4·j4)
 // (quads q0 .. q0 + NQ - 1 of the wave's staging image; the 16x16x4 form's swizzle depends on
-// the absolute row)
+// the absolute row; a float4 of 4 columns stays contiguous under both swizzles)
 template <int NQ, bool kBig>
-__device__ __forceinline__ void mstage(float *stg, int q0, int lane, const u4v (&v)[kMPL * NQ]) {
+__device__ __forceinline__ void mstage(float *stg, int q0, int lane, const u4v (&v)[kMPP * NQ]) {
 #pragma unroll
-    for (int i = 0; i < kMPL * NQ; ++i) {
-        const int q = q0 + i / kMPL, j4 = mpoll_row(i) - 4 * (i / kMPL) + lane / (kMK / 2), kk = mpoll_col(lane);
+    for (int i = 0; i < kMPP * NQ; ++i) {
+        const int q = q0 + i / kMPP, j4 = mpoll_row(i) - 4 * (i / kMPP) + lane / (kMK / 4), kk = mpoll_col(lane);
         const int at = kBig ? mstg16_at(4 * q + j4, kk) : q * kMStg + mstg_at(j4, kk);
-        *reinterpret_cast<f2v *>(stg + at) = f2v{__uint_as_float(v[i].x), __uint_as_float(v[i].z)};
+        *reinterpret_cast<u4v *>(stg + at) = v[i];
     }
 }
 
-// Poll + stage a wave's slice of all NQ quads, at most two quads per poll round (register budget)
+// Poll + stage a wave's slice of all NQ quads, at most four quads (8 float4s) per poll round
 template <int NQ, int Q0 = 0>
-__device__ __forceinline__ void mgather(const unsigned long long *vec, float *stg, int w, uint32_t tag, int *ctl,
-                                        long long timeout, int step, int hop, int *lds_abort, int lane) {
+__device__ __forceinline__ void mgather(const float *vec, float *stg, int w, int *ctl, long long timeout, int step,
+                                        int hop, int *lds_abort, int lane) {
     if constexpr (Q0 < NQ) {
-        constexpr int G = NQ - Q0 < 2 ? NQ - Q0 : 2;
-        u4v v[kMPL * G];
-        mpoll<G>(vec + (size_t)Q0 * 4 * 512, w, tag, ctl, timeout, step, hop, lds_abort, lane, v);
+        constexpr int G = NQ - Q0 < 4 ? NQ - Q0 : 4;
+        u4v v[kMPP * G];
+        mpoll<G>(vec + (size_t)Q0 * 4 * 512, w, ctl, timeout, step, hop, lds_abort, lane, v);
         mstage<G, xcdm_big(NQ)>(stg, Q0, lane, v);
-        mgather<NQ, Q0 + G>(vec, stg, w, tag, ctl, timeout, step, hop, lds_abort, lane);
+        mgather<NQ, Q0 + G>(vec, stg, w, ctl, timeout, step, hop, lds_abort, lane);
     }
 }
 
@@ -117,38 +136,37 @@ __device__ __forceinline__ void mgather(const unsigned long long *vec, float *st
 // layer calls step(jc) at the start of each of its 8 k-chunks, and the poll's loads are issued
 // once, at chunk kAt, so that the rest of the layer's MFMAs cover their round trip; finish()
 // checks them after the layer (a wait only if they have not landed) and falls back to the
-// bounded blocking poll (mpoll) if some granule still carried an old tag.  (Checking inside the
+// bounded blocking poll (mpoll) if some element was still empty.  (Checking inside the
 // layer would stall it: reading the loaded registers waits for the loads, landed or not.)
 struct MPollNone {
     __device__ __forceinline__ void step(int) {}
 };
 template <int G, int kAt>
 struct MPoll {
-    u4v v[G > 0 ? kMPL * G : 1];
+    u4v v[G > 0 ? kMPP * G : 1];
     __amdgpu_buffer_rsrc_t r;
     int off;
-    uint32_t tag;
-    __device__ __forceinline__ MPoll(const unsigned long long *vec, int w, uint32_t tag_, int lane) : off(0), tag(tag_) {
+    __device__ __forceinline__ MPoll(const float *vec, int w, int lane) : off(0) {
         if constexpr (G > 0) {
-            r = hop_rsrc(vec);
-            off = kMK * w * 8 + mpoll_lane_off(lane);
+            r = hop_rsrc(reinterpret_cast<const unsigned long long *>(vec));
+            off = kMK * w * 4 + mpoll_lane_off(lane);
         }
     }
     __device__ __forceinline__ void step(int jc) {
         if constexpr (G > 0) {
             if (jc == kAt) {
 #pragma unroll
-                for (int i = 0; i < kMPL * G; ++i) v[i] = ld16_sc1(r, off + mpoll_row(i) * 512 * 8);
+                for (int i = 0; i < kMPP * G; ++i) v[i] = ld16_sc1(r, off + mpoll_row(i) * 512 * 4);
             }
         }
     }
-    __device__ __forceinline__ void finish(const unsigned long long *vec, int w, int *ctl, long long timeout, int step_,
-                                           int hop, int *lds_abort, int lane) {
+    __device__ __forceinline__ void finish(const float *vec, int w, int *ctl, long long timeout, int step_, int hop,
+                                           int *lds_abort, int lane) {
         if constexpr (G > 0) {
             bool ok = true;
 #pragma unroll
-            for (int i = 0; i < kMPL * G; ++i) ok &= (v[i].y == tag) & (v[i].w == tag);
-            if (__ballot(!ok) != 0) mpoll<G>(vec, w, tag, ctl, timeout, step_, hop, lds_abort, lane, v);
+            for (int i = 0; i < kMPP * G; ++i) ok &= pfull(v[i]);
+            if (__ballot(!ok) != 0) mpoll<G>(vec, w, ctl, timeout, step_, hop, lds_abort, lane, v);
         }
     }
 };
@@ -324,17 +342,17 @@ __device__ __forceinline__ void mlayer_lds(const float (&A)[kMSets][kMJ], const 
     else mlayer<NQ, 0, 1, MChains<NQ, 1>::v, MPollNone, true>(A, stg, P, lane, wave, MPollNone{}, AL);
 }
 
-// quads polled beside an off-critical layer (none above one quad: the registers are not there),
-// and the k-chunk at which its loads are issued
+// quads polled beside an off-critical layer (all of them: ≤ 8 float4s per lane, the registers
+// the tagged form's two quads took), and the k-chunk at which its loads are issued
 template <int NQ>
 struct MRide {
-    static constexpr int G = NQ == 1 ? 1 : 2;
+    static constexpr int G = NQ;
     static constexpr int at = 3;
 };
 
 // Poll + stage the hop vector `vec` (all quads) with its first MRide group already polled by `pr`
 template <int NQ>
-__device__ __forceinline__ void mgather_rest(MPoll<MRide<NQ>::G, MRide<NQ>::at> &pr, const unsigned long long *vec,
+__device__ __forceinline__ void mgather_rest(MPoll<MRide<NQ>::G, MRide<NQ>::at> &pr, const float *vec,
                                              float *stg, int w, int *ctl, long long timeout, int step, int hop,
                                              int *lds_abort, int lane) {
     constexpr int G = MRide<NQ>::G;
@@ -344,7 +362,7 @@ __device__ __forceinline__ void mgather_rest(MPoll<MRide<NQ>::G, MRide<NQ>::at> 
     } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    mgather<NQ, G>(vec, stg, w, pr.tag, ctl, timeout, step, hop, lds_abort, lane);
+    mgather<NQ, G>(vec, stg, w, ctl, timeout, step, hop, lds_abort, lane);
 }
 
 // MoL sample of XCD row n by one wave: Σ of the 32 producers' partial logits + b3, then
@@ -616,14 +634,21 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
             const float z = sigmoid_(fmaf(x, cst[MC_Q1 + 16 + gu], sz));
             const float nn = tanh_(fmaf(x, cst[MC_Q1 + 32 + gu], gin) + ghn * r);
             h1v = (h1v - nn) * z + nn;
-            xpub(xg + kMHopOff[MH_H1] + gn * 512 + 16 * c + gu, tag, h1v);
+            ppub(pvec(xg, MH_H1, t) + gn * 512 + 16 * c + gu, h1v);
         }
         MST(1);
         // ---- B: the h1 slice → W_ih2[:, :R]·h1 (the GRU2 input gates, :213-214)
         {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            mgather<NQ>(xg + kMHopOff[MH_H1], stg_h1, wave, tag, a.ctl, a.timeout_ticks, t, MH_H1, abort_flag, lane);
+            mgather<NQ>(pvec(xg, MH_H1, t), stg_h1, wave, a.ctl, a.timeout_ticks, t, MH_H1, abort_flag, lane);
             MST(2);
+            // every workgroup's h1_t is here, so every consumer has read all of step t - 1: empty
+            // this thread's elements of the other slot (step t + 1's), ordered before the y publish
+            if (gru) {
+                const int e = gn * 512 + 16 * c + gu;
+#pragma unroll
+                for (int hv = MH_H1; hv < (kRaw ? MH_F2 + 1 : MH_F2); ++hv) pclear(pvec(xg, hv, t + 1) + e);
+            }
             mlayer_any<NQ, MS_IH2, 3>(A, stg_h1, pbig, lane, wave);
             MST(3);
         }
@@ -642,22 +667,23 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
             h2v = gru_gate_math(gi[0], gi[1], gi[2], gh[0], gh[1], gh[2], h2v);
             const float xi = fmaf(cst[MC_WI0 + gu], x, tr[XT_CI + gu]);
             const float y = (xi + h1v) + h2v;
-            xpub(xg + kMHopOff[MH_Y] + gn * 512 + 16 * c + gu, tag, y);
-            xpub(xg + kMHopOff[MH_H2] + gn * 512 + 16 * c + gu, tag, h2v);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the slot clears of B first
+            ppub(pvec(xg, MH_Y, t) + gn * 512 + 16 * c + gu, y);
+            ppub(pvec(xg, MH_H2, t) + gn * 512 + 16 * c + gu, h2v);
         }
         MST(5);
         // ---- D: W_hh1·h1 (the GRU1 terms of step t + 1; carried to the next chunk after the
         // last one) from the staged h1 slice, with the y poll of E riding along (hop Y's window)
-        MPoll<MRide<NQ>::G, MRide<NQ>::at> py(xg + kMHopOff[MH_Y], wave, tag, lane);
+        MPoll<MRide<NQ>::G, MRide<NQ>::at> py(pvec(xg, MH_Y, t), wave, lane);
         mlayer_any<NQ, MS_HH1, 3>(A, stg_h1, phh1, lane, wave, py);
         MST(6);
         // ---- E: the y slice → fc1 (:217-218)
         {
-            mgather_rest<NQ>(py, xg + kMHopOff[MH_Y], stg, wave, a.ctl, a.timeout_ticks, t, MH_Y, abort_flag, lane);
+            mgather_rest<NQ>(py, pvec(xg, MH_Y, t), stg, wave, a.ctl, a.timeout_ticks, t, MH_Y, abort_flag, lane);
             MST(7);
         }
         // h2 was published with y: its poll rides along fc1 and is checked in G, after F
-        MPoll<MRide<NQ>::G, MRide<NQ>::at> ph(xg + kMHopOff[MH_H2], wave, tag, lane);
+        MPoll<MRide<NQ>::G, MRide<NQ>::at> ph(pvec(xg, MH_H2, t), wave, lane);
         mlayer_any<NQ, MS_FC1, 1>(A, stg, pfc1, lane, wave, ph);
         MST(8);
         bar();
@@ -665,7 +691,7 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         // ---- F: fc1 epilogue → f1; Σ W_hh1·h1 for the next GRU1
         if (gru) {
             const float f = mpart<NQ>(pfc1, gu, gn) + rg[gn * kMRing + XT_V1 + gu];
-            xpub(xg + kMHopOff[MH_F1] + gn * 512 + 16 * c + gu, tag, f > 0.0f ? f : 0.0f);
+            ppub(pvec(xg, MH_F1, t) + gn * 512 + 16 * c + gu, f > 0.0f ? f : 0.0f);
             if (aux_w0 >= kMWaves) {
 #pragma unroll
                 for (int q = 0; q < 3; ++q) {
@@ -678,13 +704,13 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         // ---- G: the h2 slice → W_hh2·h2 (the next step's GRU2), with the f1 poll of H riding
         // along (hop F1's window); f1 is staged once the layer's B reads of the h2 slice are done
         {
-            mgather_rest<NQ>(ph, xg + kMHopOff[MH_H2], stg, wave, a.ctl, a.timeout_ticks, t, MH_H2, abort_flag, lane);
+            mgather_rest<NQ>(ph, pvec(xg, MH_H2, t), stg, wave, a.ctl, a.timeout_ticks, t, MH_H2, abort_flag, lane);
             MST(11);
-            MPoll<MRide<NQ>::G, MRide<NQ>::at> pf(xg + kMHopOff[MH_F1], wave, tag, lane);
+            MPoll<MRide<NQ>::G, MRide<NQ>::at> pf(pvec(xg, MH_F1, t), wave, lane);
             mlayer_any<NQ, MS_HH2, 3>(A, stg, pbig, lane, wave, pf);
             MST(12);
             // ---- H: the f1 slice → fc2 (:220-221)
-            mgather_rest<NQ>(pf, xg + kMHopOff[MH_F1], stg, wave, a.ctl, a.timeout_ticks, t, MH_F1, abort_flag, lane);
+            mgather_rest<NQ>(pf, pvec(xg, MH_F1, t), stg, wave, a.ctl, a.timeout_ticks, t, MH_F1, abort_flag, lane);
             MST(13);
             mlayer_any<NQ, MS_FC2, 1>(A, stg, pfc2, lane, wave);
             MST(14);
@@ -744,7 +770,7 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         // ---- I: fc2 epilogue → f2 (LDS); Σ W_hh2·h2 for the next GRU2
         if (gru) {
             const float f = mpart<NQ>(pfc2, gu, gn) + rg[gn * kMRing + XT_V2 + gu];
-            if constexpr (kRaw) xpub(xg + kMHopOff[MH_F2] + gn * 512 + 16 * c + gu, tag, f > 0.0f ? f : 0.0f);
+            if constexpr (kRaw) ppub(pvec(xg, MH_F2, t) + gn * 512 + 16 * c + gu, f > 0.0f ? f : 0.0f);
             else f2s[gn * kMW3Stride + gu] = f > 0.0f ? f : 0.0f;
             if (aux_w0 >= kMWaves) {
 #pragma unroll
@@ -758,7 +784,7 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         if constexpr (kRaw) {
             // fc3 (:223) rows of the own 16 classes on the gathered f2 slice → logits [hop LG]
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            mgather<NQ>(xg + kMHopOff[MH_F2], stg, wave, tag, a.ctl, a.timeout_ticks, t, MH_F2, abort_flag, lane);
+            mgather<NQ>(pvec(xg, MH_F2, t), stg, wave, a.ctl, a.timeout_ticks, t, MH_F2, abort_flag, lane);
             MST(17);
             mlayer_lds<NQ>(A, a3s + wave * kMJ * 64, stg, pfc1, lane, wave);
             bar();
