@@ -114,6 +114,10 @@ struct DxRide {
         }
     }
     __device__ __forceinline__ void finish(int *ctl, long long timeout, int step_, int hop, int *lds_abort) {
+        // pinned after the layer (empty volatile asm, ordered with the MFMA asm): hipcc otherwise
+        // hoists the tag test and its s_waitcnt into the layer's MFMA stream
+#pragma unroll
+        for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(v[i]));
         bool ok = true;
 #pragma unroll
         for (int i = 0; i < 4; ++i) ok &= (v[i].y == tag) & (v[i].w == tag);

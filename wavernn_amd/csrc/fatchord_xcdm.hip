@@ -163,6 +163,11 @@ struct MPoll {
     __device__ __forceinline__ void finish(const float *vec, int w, int *ctl, long long timeout, int step_, int hop,
                                            int *lds_abort, int lane) {
         if constexpr (G > 0) {
+            // the loaded registers pass through an empty volatile asm here, so the check (and its
+            // s_waitcnt) cannot be hoisted into the layer's MFMA stream (volatile asm, kept in
+            // order): hipcc otherwise tests each float4 right after its load and stalls the layer
+#pragma unroll
+            for (int i = 0; i < kMPP * G; ++i) asm volatile("" : "+v"(v[i]));
             bool ok = true;
 #pragma unroll
             for (int i = 0; i < kMPP * G; ++i) ok &= pfull(v[i]);
@@ -344,10 +349,13 @@ __device__ __forceinline__ void mlayer_lds(const float (&A)[kMSets][kMJ], const 
 
 // quads polled beside an off-critical layer (all of them: ≤ 8 float4s per lane, the registers
 // the tagged form's two quads took), and the k-chunk at which its loads are issued
+#ifndef WRNN_XCDM_RIDE_AT
+#define WRNN_XCDM_RIDE_AT 3
+#endif
 template <int NQ>
 struct MRide {
     static constexpr int G = NQ;
-    static constexpr int at = 3;
+    static constexpr int at = WRNN_XCDM_RIDE_AT;
 };
 
 // Poll + stage the hop vector `vec` (all quads) with its first MRide group already polled by `pr`
