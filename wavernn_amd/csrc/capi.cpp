@@ -153,6 +153,7 @@ struct wrnn_ctx {
     int xcdm_nq = 0;                                // largest co-resident quad count (rows per XCD / 4)
     XcdmSlab xms{};
     float *d_xmslab = nullptr, *d_xmstate = nullptr, *d_xmnoise = nullptr;
+    float *d_xmWt = nullptr;   // many-row kernel's terms-GEMM weights: the first kMRing rows of each workgroup's record
     size_t xmnoise_cap = 0;
     // XCD-resident deepmind kernel (hidden 896, quantisation 256, MFMA): deepmind_xcd.hip
     bool dx_ok = false;
@@ -1707,7 +1708,7 @@ int generate_xcds(wrnn_t *h, const float *cond, int B, int L, const float *noise
 // WRNN_TERMS_MB (default 8192 MiB); the recurrent state is carried per workgroup in d_xmstate.
 int generate_xcdm(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed, int64_t row_offset,
                   float *out, int32_t *labels, hipStream_t st) {
-    const int N = kXcdWgs * kXTerms;
+    const int N = kXcdWgs * kMRing;   // compact terms record (d_xmWt)
     const bool raw = h->cfg.mode == WRNN_MODE_RAW;
     const int NK = raw ? kMRawNC : 11;              // draws per row-step: Exp(1) per class / MoL uniforms
     if (!h->blas && rocblas_create_handle(&h->blas) != rocblas_status_success)
@@ -1746,7 +1747,7 @@ int generate_xcdm(wrnn_t *h, const float *cond, int B, int L, const float *noise
                 return fail(h, WRNN_EINVAL, "xcdm: terms workspace too small");
             HIP_TRY(h, launch_pack_cond_input(cond, h->CD, B, b0, nb, t0, Lc, h->KXc, h->d_X, st));
             if (rocblas_sgemm(h->blas, rocblas_operation_transpose, rocblas_operation_none, N, Lc * nb, h->KXc, &one,
-                              h->d_xWt, h->KXc, h->d_X, h->KXc, &zero, h->d_T, N) != rocblas_status_success)
+                              h->d_xmWt, h->KXc, h->d_X, h->KXc, &zero, h->d_T, N) != rocblas_status_success)
                 return fail(h, WRNN_EHIP, "rocblas_sgemm (conditioning terms) failed");
             HIP_TRY(h, hipMemsetAsync(h->d_members, 0, kXcds * sizeof(int), st));
             XcdmArgs a{};
@@ -2188,7 +2189,15 @@ int wrnn_set_weights(wrnn_t *h, const wrnn_tensor *tensors, int n) {
         }
     }
     if (h->xcdm_ok) {
-        std::vector<float> slab;
+        std::vector<float> slab, Wt, Wm;
+        pack_xcd_terms_weights(*h, Wt);
+        Wm.reserve((size_t)kXcdWgs * kMRing * h->KXc);
+        for (int c = 0; c < kXcdWgs; ++c)   // rows c·kXTerms + j, j < kMRing → c·kMRing + j
+            Wm.insert(Wm.end(), Wt.begin() + (size_t)c * kXTerms * h->KXc, Wt.begin() + ((size_t)c * kXTerms + kMRing) * h->KXc);
+        if (h->d_xmWt) HIP_TRY(h, hipFree(h->d_xmWt));
+        h->d_xmWt = nullptr;
+        HIP_TRY(h, hipMalloc(&h->d_xmWt, Wm.size() * 4));
+        HIP_TRY(h, hipMemcpy(h->d_xmWt, Wm.data(), Wm.size() * 4, hipMemcpyHostToDevice));
         pack_xcdm_slab(*h, slab);
         if (h->d_xmslab) HIP_TRY(h, hipFree(h->d_xmslab));
         h->d_xmslab = nullptr;
@@ -2354,6 +2363,7 @@ void wrnn_destroy(wrnn_t *h) {
                     (void *)h->d_sWt, (void *)h->g2.d_slab, (void *)h->g2.d_Wt, (void *)h->dm2.d_slab,
                     (void *)h->d_gact, (void *)h->d_xslab, (void *)h->d_xWt, (void *)h->d_xstate, (void *)h->d_xgx,
                     (void *)h->d_members, (void *)h->d_xmslab, (void *)h->d_xmstate, (void *)h->d_xmxg, (void *)h->d_xmnoise,
+                    (void *)h->d_xmWt,
                     (void *)h->d_dxslab, (void *)h->d_dxstate, (void *)h->d_dxnoise, (void *)h->d_dxxg})
         if (p) (void)hipFree(p);
     if (h->blas) (void)rocblas_destroy_handle(h->blas);

@@ -509,7 +509,7 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int NR = 4 * NQ;
     constexpr bool kTwoLevel = NQ >= 2;
-    constexpr int N = kXcdWgs * kXTerms;
+    constexpr int N = kXcdWgs * kMRing;   // the compact terms record (capi.cpp: d_xmWt)
     const XcdmLds ll = xcdm_lds_layout(NQ, kDbg, kRaw);
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     constexpr int kStgQ = xcdm_big(NQ) ? kMQuadMax : NQ;   // staged quads per wave
@@ -538,7 +538,7 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
     unsigned long long *xg = a.xg + (size_t)k * kMXcdStride;
     const float *S = a.slab + (size_t)c * a.s.total;
     auto TERMS = [&](int t, int n) {
-        return a.terms + ((size_t)(t - a.t0) * a.nb + (k + kXcds * n)) * N + (size_t)c * kXTerms;
+        return a.terms + ((size_t)(t - a.t0) * a.nb + (k + kXcds * n)) * N + (size_t)c * kMRing;
     };
 
     // ---- register-resident MFMA A operands: the wave's K window of all eleven sets
