@@ -33,7 +33,7 @@ from wavernn_amd import synthetic as syn  # noqa: E402
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak (dense)
 MOL_MACS_PER_ROW_STEP = 3825152   # loop MACs per row-step, MoL rnn 512
-PMC_PROFILE = os.environ.get("WRNN_PMC_PROFILE", os.path.join(REPO, "profiles", "r03_v4_pmc_traffic.json"))
+PMC_PROFILE = os.environ.get("WRNN_PMC_PROFILE", os.path.join(REPO, "profiles", "r03_v7_pmc_traffic.json"))
 SPARSE896_BYTES_PER_STEP = 5536598   # config 4 sparse values + int16 block indices, fp32
 DM_BYTES_PER_STEP = 12200196         # config 5 deepmind weights, fp32
 
