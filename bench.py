@@ -5,20 +5,30 @@ T = 401 frames → 110 275 loop steps, 110 000 output samples), unbatched (batch
 sampling, random weights of the 800k-step MoL architecture (hparams.py).  A "step" of this
 benchmark is one full `WaveRNN.generate()` of that utterance (upsample → persistent HIP
 loop → float64 post-processing).  N GPUs = N ranks, one utterance each (weak scaling; the
-utterances are independent, there is no collective in the data path).
+utterances are independent, there is no collective in the data path; the finished audio is
+gathered to rank 0 over RCCL).
+
+`python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment starts its N rank
+processes itself (before the parent touches a GPU); under torchrun it is one of them.
 
 Prints ONE JSON line on rank 0.  `roofline` is computed for the persistent loop kernel from
-HIP events around its launch; `cpu_baseline` times the reference's own op sequence as a
-PyTorch-CPU eager restatement (oracle/torch_cpu.py: upsample, the per-step loop, float64 post) on
-this host's cores over a bounded slice of the same workload; `cpu_baseline_c_oracle` the
-single-threaded C oracle (oracle/wavernn_oracle.c) on the same slice.
+HIP events around its launch; `roofline.traffic` from two rocprofv3 --pmc passes (FETCH_SIZE,
+WRITE_SIZE) of this same script run as child processes before the measured run (N = 1; the
+committed profile is the labelled fallback); `cpu_baseline` times the reference's own op
+sequence as a PyTorch-CPU eager restatement (oracle/torch_cpu.py) on this host's cores over a
+bounded slice of the same workload.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import shutil
+import signal
+import socket
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -36,24 +46,7 @@ MOL_MACS_PER_ROW_STEP = 3825152   # loop MACs per row-step, Mo
 PMC_PROFILE = os.environ.get("WRNN_PMC_PROFILE", os.path.join(REPO, "profiles", "r03_v7_pmc_traffic.json"))
 SPARSE896_BYTES_PER_STEP = 5536598   # config 4 sparse values + int16 block indices, fp32
 DM_BYTES_PER_STEP = 12200196         # config 5 deepmind weights, fp32
-
-
-def pmc_traffic_bytes(mode: str, batched: bool, seconds: float):
-    """HBM-side bytes per launch from the committed rocprofv3 PMC passes (FETCH_SIZE +
-    WRITE_SIZE, separate passes) for this exact workload, or None.  gfx950 correction
-    (MI355X_MICROARCH.md): FETCH_SIZE counts half the bytes of 16-B-per-lane reads."""
-    if mode != "MOL" or batched or abs(seconds - 5.0) > 1e-9 or not os.path.exists(PMC_PROFILE):
-        return None
-    c = json.load(open(PMC_PROFILE))["counters"]
-    return 1024.0 * (2.0 * c["FETCH_SIZE"]["value_kib"] + c["WRITE_SIZE"]["value_kib"])
-
-
-def pmc_config_traffic(key: str):
-    """HBM bytes per loop step of another config's loop kernel from the same PMC passes, or None."""
-    if not os.path.exists(PMC_PROFILE):
-        return None
-    c = json.load(open(PMC_PROFILE)).get("other_configs", {}).get(key)
-    return c["bytes_per_step"] if c else None
+DM_MACS_PER_ROW_STEP = 3045952
 COND_BYTES_PER_ROW_STEP = 836  # 208 fp32 conditioning + 1 fp32 output (SURVEY.md §8(d))
 KERNELS = {7: "fatchord_xcdm_kernel (many rows per XCD, MFMA)", 5: "fatchord_xcd_kernel (one XCD, 32 CUs)",
            4: "fatchord_split_kernel", 2: "fatchord_rows_kernel", 1: "fatchord_loop_kernel"}
@@ -73,69 +66,154 @@ def hbm_roofline(bytes_per_step: float, us_per_step: float, note: str) -> dict:
             "frac": achieved / HBM_PEAK_GBS, "note": note}
 
 
-def other_configs(dev) -> dict:
-    """BASELINE configs 3-5 on one GPU (synthetic inputs, random weights of each architecture):
-      3: MoL fold-batched generate() of one 60 s utterance (115 folds x 12 100 steps);
-      4: rnn 896 with 95 % 4x4 block-sparse GRU weights, 8 utterances of 5 s (8 rows) per GPU;
-      5: deepmind dual softmax, 32 utterances of 1 s at 16 kHz (32 rows) per GPU;
-    plus the headline architecture serving 8 independent batch-1 streams at once (one per XCD)."""
+# ------------------------------------------------------------------------ rank launcher
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """One process per GPU, started from this (GPU-untouched) parent: RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* as torchrun sets them, 127.0.0.1 rendezvous.  Returns the first
+    non-zero exit code (the other ranks are then stopped), else 0."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in procs:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+# ---------------------------------------------------------------------- HBM traffic (PMC)
+def _under_profiler() -> bool:
+    return any(k.startswith("ROCPROF") for k in os.environ) or "rocprof" in os.environ.get("LD_PRELOAD", "")
+
+
+def pmc_live(timeout_s: float = 240.0):
+    """FETCH_SIZE and WRITE_SIZE passes (one counter each, MI355X_MICROARCH.md's recipe) over
+    `bench.py --pmc-child` (the headline and configs 2×8 / 3 / 4 / 5 generated once each), run
+    as child processes before this process touches the GPU.  Returns the summary record
+    (tools/pmc_summary.py) or None when rocprofv3 is absent or a pass fails."""
+    exe = shutil.which("rocprofv3")
+    if exe is None or _under_profiler():
+        return None
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import pmc_summary
+    tmp = tempfile.mkdtemp(prefix="wrnn_pmc_")
+    try:
+        for c in ("FETCH_SIZE", "WRITE_SIZE"):
+            cmd = [exe, "--pmc", c, "-d", os.path.join(tmp, "pmc_" + c), "-o", "pmc", "--output-format", "csv", "--",
+                   sys.executable, os.path.abspath(__file__), "--pmc-child"]
+            p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, start_new_session=True,
+                                 env=dict(os.environ, WRNN_BENCH_PMC_CHILD="1"))
+            try:
+                if p.wait(timeout=timeout_s) != 0:
+                    return None
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+                return None
+        return pmc_summary.summarise(tmp)
+    except Exception:          # an unreadable summary falls back to the committed profile
+        return None
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def committed_pmc():
+    if not os.path.exists(PMC_PROFILE):
+        return None
+    with open(PMC_PROFILE) as f:
+        return json.load(f)
+
+
+# ------------------------------------------------------------------------ other configs
+def _mol_model(d, dev, state):
     from wavernn_amd.fatchord_version import WaveRNN
-    from wavernn_amd.loop import DeepmindLoop, FatchordLoop
+    model = WaveRNN(**d.ctor_kwargs()).to(dev)
+    model.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in state.items()})
+    return model
+
+
+def _timed(fn):
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    out = fn()
+    torch.cuda.synchronize()
+    return out, time.perf_counter() - t
+
+
+def other_configs(dev, warm: bool = True, cpu_steps: int = 0, threads: int = 1) -> dict:
+    """BASELINE configs 1 and 3-5 on one GPU, every one through the drop-in API (upsample and
+    post-processing included), synthetic inputs, random weights of each architecture:
+      1: RAW 9-bit generate(), 1 s unbatched and 5 s fold-batched;
+      3: MoL fold-batched generate() of one 60 s utterance (115 folds x 12 100 steps);
+      4: rnn 896 with 95 % 4x4 block-sparse GRU weights, 8 utterances of 5 s in one
+         generate_many() launch (the per-GPU share of 64 over 8 GPUs);
+      5: deepmind dual softmax, 32 utterances of 1 s at 16 kHz in one generate(batch=32);
+    plus the headline architecture serving 8 utterances at once (generate_many, one per XCD).
+    `warm` = an untimed first call per config (the PMC child runs each config once)."""
+    from wavernn_amd.deepmind_version import WaveRNN as DeepmindWaveRNN
     from wavernn_amd.pruning import prune_state
     res = {}
+    sr = 22050
     # config 2 architecture, 8 concurrent unbatched utterances (per-stream latency unchanged)
     d = syn.DEFAULT_MOL
-    L2, B2 = syn.frames_for_seconds(5.0, d.sample_rate, d.hop_length) * d.hop_length, 8
-    loop = FatchordLoop(d.mode, d.rnn_dims, d.fc_dims, d.aux_dims, d.feat_dims, d.n_classes)
-    loop.set_weights(syn.make_fatchord_state(d, 0))
-    mels, aux = syn.make_conditioning(B2, L2, d.feat_dims, d.res_out_dims, 4)
-    cond = torch.from_numpy(np.concatenate([mels, aux], 2).transpose(1, 0, 2).copy()).to(dev)
-    loop.generate(cond[:100].contiguous(), seed=1)
-    loop.generate(cond, seed=2)
-    ms = loop.elapsed_ms()
-    res["config2_8_streams"] = {"samples_per_s": B2 * L2 / ms * 1e3, "rtf_per_stream": L2 / ms * 1e3 / d.sample_rate,
-                                "rows": B2, "loop_steps": L2, "device_ms": ms, "us_per_loop_step": ms * 1e3 / L2,
-                                "kernel_path": loop.info["last_path"],
-                                "roofline": hbm_roofline(loop_weight_bytes(d) + B2 * COND_BYTES_PER_ROW_STEP, ms * 1e3 / L2,
+    model = _mol_model(d, dev, syn.make_fatchord_state(d, 0))
+    T5 = syn.frames_for_seconds(5.0, d.sample_rate, d.hop_length)
+    mels = [torch.from_numpy(syn.make_mel(d.feat_dims, T5, 40 + i))[None] for i in range(8)]
+    if warm:
+        model.generate_many(mels, None, False, 11000, 550, True, seed=1)
+    outs, dt = _timed(lambda: model.generate_many(mels, None, False, 11000, 550, True, seed=2))
+    ms, L2 = model.loop_handle().elapsed_ms(), T5 * d.hop_length
+    n = sum(o.shape[0] for o in outs)
+    res["config2_8_streams"] = {"samples_per_s": n / dt, "rtf_per_stream": n / 8 / dt / sr, "rows": 8,
+                                "loop_steps": L2, "device_ms": ms, "wall_s": dt, "us_per_loop_step": ms * 1e3 / L2,
+                                "kernel_path": model.loop_handle().info["last_path"],
+                                "roofline": hbm_roofline(loop_weight_bytes(d) + 8 * COND_BYTES_PER_ROW_STEP, ms * 1e3 / L2,
                                                          "algorithmic bytes per step (all loop weights once + 836 B "
                                                          "per row) / step time; weights resident, latency-bound"),
-                                "note": "8 independent 5 s utterances, unbatched, one per XCD in one launch of "
-                                        "fatchord_xcd_kernel (path 5), from upsampled conditioning (upsample "
-                                        "excluded), incl. the conditioning-terms GEMM"}
-    del cond
-    loop.close()
+                                "note": "8 independent 5 s utterances, unbatched, WaveRNN.generate_many (ONE launch of "
+                                        "fatchord_xcd_kernel, one utterance per XCD); rate over the whole call "
+                                        "(upsample, loop, float64 post)"}
+    del model
     # config 1's model (RAW 9-bit, rnn 512) on the GPU through the drop-in generate(): 1 s unbatched
     # (the reference runs it on the CPU) and a 5 s utterance fold-batched
     dr = syn.DEFAULT_RAW
-    model = WaveRNN(**dr.ctor_kwargs()).to(dev)
-    model.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in syn.make_fatchord_state(dr, 0).items()})
+    model = _mol_model(dr, dev, syn.make_fatchord_state(dr, 0))
     for key, sec, batched in (("config1_raw_1s_unbatched", 1.0, False), ("config1_raw_5s_fold_batched", 5.0, True)):
         mel = torch.from_numpy(syn.make_mel(dr.feat_dims, syn.frames_for_seconds(sec, dr.sample_rate, dr.hop_length),
                                             5))[None]
-        model.generate(mel, None, batched, 11000, 550, True, seed=1, verbose=False)
-        torch.cuda.synchronize()
-        t = time.perf_counter()
-        out = model.generate(mel, None, batched, 11000, 550, True, seed=2, verbose=False)
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t
+        if warm:
+            model.generate(mel, None, batched, 11000, 550, True, seed=1, verbose=False)
+        out, dt = _timed(lambda: model.generate(mel, None, batched, 11000, 550, True, seed=2, verbose=False))
         h = model.loop_handle()
-        ms = h.elapsed_ms()
         res[key] = {"samples_per_s": out.shape[0] / dt, "rtf": out.shape[0] / dt / dr.sample_rate, "wall_s": dt,
-                    "device_ms": ms, "kernel_path": h.info["last_path"],
+                    "device_ms": h.elapsed_ms(), "kernel_path": h.info["last_path"],
                     "note": "RAW 9-bit (bits mode, mu-law) generate() of a synthetic mel on the drop-in; path 7 = "
                             "fatchord_xcdm_kernel's softmax head; rate over the whole generate() wall time"}
     del model
     # config 3
-    d = syn.DEFAULT_MOL
-    model = WaveRNN(**d.ctor_kwargs()).to(dev)
-    model.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in syn.make_fatchord_state(d, 0).items()})
+    state3 = syn.make_fatchord_state(d, 0)
+    model = _mol_model(d, dev, state3)
     mel = torch.from_numpy(syn.make_mel(d.feat_dims, syn.frames_for_seconds(60.0, d.sample_rate, d.hop_length), 3))[None]
-    model.generate(mel, None, True, 11000, 550, True, seed=1, verbose=False)     # warm (MIOpen tunes per shape)
-    torch.cuda.synchronize()
-    t = time.perf_counter()
-    out = model.generate(mel, None, True, 11000, 550, True, seed=2, verbose=False)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t
+    if warm:
+        model.generate(mel, None, True, 11000, 550, True, seed=1, verbose=False)     # MIOpen tunes per shape
+    out, dt = _timed(lambda: model.generate(mel, None, True, 11000, 550, True, seed=2, verbose=False))
     ms = model.loop_handle().elapsed_ms()
     flops = 2.0 * MOL_MACS_PER_ROW_STEP * 115 * 12100
     res["config3_mol_fold_60s"] = {"samples_per_s": out.shape[0] / dt, "rtf": out.shape[0] / dt / d.sample_rate,
@@ -148,52 +226,81 @@ def other_configs(dev) -> dict:
                                                 "note": "algorithmic FLOP = 2 x 3 825 152 MAC x 115 rows per step "
                                                         "(SURVEY.md 8(d): AI 57 F/B > ridge); device time of the loop "
                                                         "launches incl. the terms GEMMs between time chunks"}}
+    if cpu_steps > 0:
+        from oracle import torch_cpu
+        n = min(cpu_steps, 12100)
+        noise = syn.make_noise("MOL", 115, 12100, d.n_classes, 7)
+        r = torch_cpu.timed_generate(state3, d, mel[0].numpy(), True, 11000, 550, True, noise, loop_steps=n,
+                                     threads=threads)
+        t_cpu = r["loop_s"] + n / 12100 * (r["pre_s"] + r["post_s"])
+        res["config3_mol_fold_60s"]["cpu_baseline"] = {
+            "value": n * 115 / t_cpu, "unit": "samples/s", "cores": r["threads"], "kind": "port",
+            "rtf": n * 115 / t_cpu / sr, "loop_s": r["loop_s"], "pre_s": r["pre_s"], "post_s": r["post_s"],
+            "sample": f"PyTorch-CPU eager fold-batched generate() (oracle/torch_cpu.py, {r['threads']} threads): "
+                      f"upsample + fold of the whole 60 s mel, {n} of 12100 loop steps x 115 folds, float64 post of "
+                      f"the whole utterance; value = loop-step samples / (loop time + {n / 12100:.3f} x pre/post)"}
     del model
-    # config 4
+    # config 4: 8 utterances of 5 s per GPU through generate_many (upsample included)
     d4 = syn.SPARSE896_MOL
-    L4, B4 = syn.frames_for_seconds(5.0, d4.sample_rate, d4.hop_length) * d4.hop_length, 8
-    loop = FatchordLoop(d4.mode, d4.rnn_dims, d4.fc_dims, d4.aux_dims, d4.feat_dims, d4.n_classes)
-    loop.set_weights(prune_state(syn.make_fatchord_state(d4, 0), 0.95))
-    mels, aux = syn.make_conditioning(B4, L4, d4.feat_dims, d4.res_out_dims, 4)
-    cond = torch.from_numpy(np.concatenate([mels, aux], 2).transpose(1, 0, 2).copy()).to(dev)
-    loop.generate(cond[:100].contiguous(), seed=1)
-    ms = 0.0
-    loop.generate(cond, seed=2)
-    ms = loop.elapsed_ms()
-    res["config4_sparse896_8utt"] = {"samples_per_s": B4 * L4 / ms * 1e3, "rtf": B4 * L4 / ms * 1e3 / d4.sample_rate,
-                                     "rows": B4, "loop_steps": L4, "device_ms": ms, "us_per_loop_step": ms * 1e3 / L4,
-                                     "sparse_blocks_per_gate_row": loop.info["sparse_blocks"],
-                                     "kernel_path": loop.info["last_path"],
-                                     "roofline": hbm_roofline(SPARSE896_BYTES_PER_STEP + B4 * COND_BYTES_PER_ROW_STEP,
+    model = _mol_model(d4, dev, prune_state(syn.make_fatchord_state(d4, 0), 0.95))
+    mels = [torch.from_numpy(syn.make_mel(d4.feat_dims, T5, 60 + i))[None] for i in range(8)]
+    if warm:
+        model.generate_many(mels, None, False, 11000, 550, True, seed=1)
+    outs, dt = _timed(lambda: model.generate_many(mels, None, False, 11000, 550, True, seed=2))
+    h = model.loop_handle()
+    ms, L4 = h.elapsed_ms(), T5 * d4.hop_length
+    n = sum(o.shape[0] for o in outs)
+    res["config4_sparse896_8utt"] = {"samples_per_s": n / dt, "rtf": n / dt / sr, "rows": 8, "loop_steps": L4,
+                                     "device_ms": ms, "wall_s": dt, "us_per_loop_step": ms * 1e3 / L4,
+                                     "loop_samples_per_s": 8 * L4 / ms * 1e3,
+                                     "sparse_blocks_per_gate_row": h.info["sparse_blocks"],
+                                     "kernel_path": h.info["last_path"],
+                                     "roofline": hbm_roofline(SPARSE896_BYTES_PER_STEP + 8 * COND_BYTES_PER_ROW_STEP,
                                                               ms * 1e3 / L4,
                                                               "SURVEY.md 8(d) bytes per step (sparse weights + int16 "
                                                               "block indices once + 836 B per row) / step time; "
                                                               "blocks resident, latency-bound"),
-                                     "note": "loop launch from upsampled conditioning (upsample excluded); path 6 = "
-                                             "fatchord_xcds_kernel (one utterance per XCD, block-sparse GRU blocks), "
-                                             "incl. the conditioning-terms GEMM"}
-    loop.close()
-    # config 5
+                                     "note": "WaveRNN(rnn_dims=896).generate_many of 8 synthetic 5 s mels (the per-GPU "
+                                             "share of 64 utterances over 8 GPUs) in ONE launch of fatchord_xcds_kernel "
+                                             "(path 6, one utterance per XCD); samples_per_s over the whole call "
+                                             "(MelResNet + upsample, loop incl. the conditioning-terms GEMM, post)"}
+    del model
+    # config 5: 32 utterances of 1 s at 16 kHz per GPU through the deepmind drop-in
     dm = syn.DEFAULT_DM
     B5, L5 = 32, 16000
-    loop5 = DeepmindLoop(dm.hidden_size, dm.quantisation)
-    loop5.set_weights(syn.make_deepmind_state(dm, 0))
-    loop5.generate(B5, 100, seed=1)
-    loop5.generate(B5, L5, seed=2)
-    ms = loop5.elapsed_ms()
-    res["config5_deepmind_32utt"] = {"samples_per_s": B5 * L5 / ms * 1e3, "rtf": B5 * L5 / ms * 1e3 / 16000.0,
-                                     "rows": B5, "loop_steps": L5, "device_ms": ms, "us_per_loop_step": ms * 1e3 / L5,
-                                     "kernel_path": loop5.info["last_path"],
+    state5 = syn.make_deepmind_state(dm, 0)
+    model = DeepmindWaveRNN(**dm.ctor_kwargs()).to(dev)
+    model.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in state5.items()})
+    if warm:
+        model.generate(100, batch=B5, seed=1)
+    (out5, _, _), dt = _timed(lambda: model.generate(L5, batch=B5, seed=2))
+    h = model.loop_handle()
+    ms = h.elapsed_ms()
+    res["config5_deepmind_32utt"] = {"samples_per_s": out5.size / dt, "rtf": out5.size / dt / 16000.0, "rows": B5,
+                                     "loop_steps": L5, "device_ms": ms, "wall_s": dt, "us_per_loop_step": ms * 1e3 / L5,
+                                     "loop_samples_per_s": B5 * L5 / ms * 1e3,
+                                     "kernel_path": h.info["last_path"],
                                      "roofline": hbm_roofline(DM_BYTES_PER_STEP + 4 * B5, ms * 1e3 / L5,
                                                               "SURVEY.md 8(d) bytes per step (weights once + 4 B per "
                                                               "row) / step time; weights resident in each XCD's "
                                                               "registers + LDS (path 8 = deepmind_xcd_kernel, 4 rows "
-                                                              "per XCD), hand-off-latency-bound")}
-    loop5.close()
+                                                              "per XCD), hand-off-latency-bound"),
+                                     "note": "deepmind WaveRNN.generate(16000, batch=32) (the per-GPU share of 256 "
+                                             "utterances over 8 GPUs), rate over the whole call incl. the label D2H"}
+    if cpu_steps > 0:
+        from oracle import torch_cpu
+        n = min(cpu_steps, L5)
+        r = torch_cpu.timed_deepmind(state5, B5, syn.make_dm_noise(B5, n, dm.quantisation, 7), n, threads=threads)
+        res["config5_deepmind_32utt"]["cpu_baseline"] = {
+            "value": n * B5 / r["loop_s"], "unit": "samples/s", "cores": r["threads"], "kind": "port",
+            "rtf": n * B5 / r["loop_s"] / 16000.0, "loop_s": r["loop_s"],
+            "sample": f"PyTorch-CPU eager deepmind loop (oracle/torch_cpu.deepmind_loop: the reference's per-step ops "
+                      f"for 32 rows at once, {r['threads']} threads), {n} of {L5} steps x 32 rows"}
     return res
 
 
-def main():
+# ------------------------------------------------------------------------------- main
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -202,61 +309,121 @@ def main():
     ap.add_argument("--mode", default="MOL", choices=["MOL", "RAW"])
     ap.add_argument("--batched", action="store_true", help="fold-batched generate (target 11000, overlap 550)")
     ap.add_argument("--cpu-steps", type=int, default=25000, help="loop steps timed for cpu_baseline (0: skip)")
-    ap.add_argument("--other-configs", type=int, default=1, help="also time BASELINE configs 3/4/5 on this GPU (N=1)")
+    ap.add_argument("--other-configs", type=int, default=1, help="also time BASELINE configs 1/3/4/5 on this GPU (N=1)")
     ap.add_argument("--fold-batched", type=int, default=1, help="also time the same utterance through generate(batched=True)")
-    args = ap.parse_args()
+    ap.add_argument("--pmc", type=int, default=1, help="live rocprofv3 FETCH_SIZE/WRITE_SIZE passes for roofline.traffic")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--stub", action="store_true",
+                    help="no GPU: gloo ranks time a stand-in generation (tests of the launcher / timing contract)")
+    return ap.parse_args(argv)
 
+
+def timed_steps(step, steps: int, warmup: int, world: int, dev):
+    """W untimed warm-up steps, then K steps between barrier + synchronize pairs; returns the
+    elapsed time MAX over ranks and the samples SUMMED over ranks."""
+    sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
+    for i in range(warmup):
+        step(-1 - i)
+    sync()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    n_samples = 0
+    for i in range(steps):
+        n_samples += step(i)
+    sync()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    stats = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    tot = torch.tensor([float(n_samples)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    return float(stats[0]), float(tot[0])
+
+
+def stub_main(args, world, rank):
+    """The launcher + timing contract without a GPU: every rank 'generates' 22 050 samples per
+    step (a 10 ms sleep) and rank 0 gathers them, as the real step does."""
+    dev = torch.device("cpu")
+    if world > 1:
+        dist.init_process_group("gloo")
+    from wavernn_amd import sharding
+
+    def step(i):
+        time.sleep(0.01)
+        out = np.zeros(22050)
+        if world > 1:
+            sharding.gather_audio({rank: out}, world, dev)
+        return out.shape[0]
+
+    elapsed, total = timed_steps(step, args.steps, args.warmup, world, dev)
+    if rank == 0:
+        print(json.dumps({"metric": "stub", "value": total / elapsed, "unit": "samples/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+                          "higher_is_better": True, "scaling": "weak", "data": "stub"}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main():
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.stub:
+        return stub_main(args, world, rank)
+    if args.pmc_child:
+        args.steps, args.warmup, args.cpu_steps, args.fold_batched, args.pmc = 1, 0, 0, 0, 0
+    # HBM traffic passes first, while this process has not touched the GPU (child processes)
+    traffic, traffic_from = None, None
+    if args.pmc and world == 1 and not args.batched and args.mode == "MOL" and abs(args.seconds - 5.0) < 1e-9:
+        live = pmc_live()
+        if live is not None:
+            traffic, traffic_from = live, "live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this run"
+    if traffic is None and not args.batched and args.mode == "MOL" and abs(args.seconds - 5.0) < 1e-9:
+        traffic = committed_pmc()
+        traffic_from = os.path.relpath(PMC_PROFILE, REPO) + " (committed profile; live passes unavailable)" \
+            if traffic else None
+
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    from wavernn_amd.fatchord_version import WaveRNN
     d = syn.DEFAULT_MOL if args.mode == "MOL" else syn.DEFAULT_RAW
     state = syn.make_fatchord_state(d, 0)
-    model = WaveRNN(**d.ctor_kwargs()).to(dev)
-    model.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in state.items()}, strict=True)
+    model = _mol_model(d, dev, state)
     T = syn.frames_for_seconds(args.seconds, d.sample_rate, d.hop_length)
     mel = torch.from_numpy(syn.make_mel(d.feat_dims, T, seed=1 + rank))[None]
     target, overlap = 11000, 550
+    loop_ms = []
 
     from wavernn_amd import sharding
 
     def step(i):
-        # every rank vocodes its own utterance (global index = i·world + rank, Philox keyed by
-        # it); the finished audio is gathered to rank 0 — the path's only collective
+        # every rank vocodes its own utterance (Philox keyed by global row = i·world + rank);
+        # the finished audio is gathered to rank 0 — the path's only collective
         g = i * world + rank
-        out = model.generate(mel, None, args.batched, target, overlap, True, seed=1000 + g, verbose=False)
+        out = model.generate(mel, None, args.batched, target, overlap, True, seed=1000, row_offset=g, verbose=False)
         if world > 1:
             sharding.gather_audio({rank: out}, world, dev)
-        return out
+        if i >= 0:
+            loop_ms.append(model.loop_handle().elapsed_ms())
+        return out.shape[0]
 
-    for i in range(args.warmup):
-        step(-1 - i)
-    torch.cuda.synchronize()
+    elapsed, total_samples = timed_steps(step, args.steps, args.warmup, world, dev)
+    lm = torch.tensor([float(np.mean(loop_ms))], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.barrier()
-    loop_ms = []
-    t0 = time.perf_counter()
-    n_samples = 0
-    for i in range(args.steps):
-        out = step(i)
-        n_samples += out.shape[0]
-        loop_ms.append(model.loop_handle().elapsed_ms())
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    stats = torch.tensor([elapsed, float(np.mean(loop_ms))], dtype=torch.float64, device=dev)
-    tot = torch.tensor([float(n_samples)], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-    elapsed, loop_ms_max = float(stats[0]), float(stats[1])
-    total_samples = float(tot[0])
+        dist.all_reduce(lm, op=dist.ReduceOp.MAX)
+    loop_ms_max = float(lm[0])
+
+    if args.pmc_child:
+        other_configs(dev, warm=False)
+        return
 
     if rank == 0:
         cond, _ = model.conditioning(mel, args.batched, target, overlap)
@@ -284,7 +451,7 @@ def main():
                 "workload": f"fatchord WaveRNN {args.mode} generate(), {args.seconds:g} s utterance per GPU, "
                             f"{'fold-batched target 11000/overlap 550' if args.batched else 'unbatched (batch=1)'}",
                 "mode": args.mode, "rnn_dims": d.rnn_dims, "fc_dims": d.fc_dims, "utterance_s": args.seconds,
-                "loop_steps": L, "rows": B, "samples_per_utterance": int(n_samples / args.steps),
+                "loop_steps": L, "rows": B, "samples_per_utterance": int(total_samples / args.steps / world),
                 "parallelism": f"utterance-sharded x{world}",
                 "kernel": KERNELS.get(info["last_path"], str(info["last_path"])),
             },
@@ -294,27 +461,21 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": pmc_traffic_bytes(args.mode, args.batched, args.seconds),
-                "traffic_from": os.path.relpath(PMC_PROFILE, REPO) if pmc_traffic_bytes(args.mode, args.batched,
-                                                                                       args.seconds) else None,
+                "traffic": traffic["bytes"] if traffic else None,
+                "traffic_from": traffic_from,
                 "note": "achieved = algorithmic bytes (all loop weights fp32 per step + 836 B/row-step) per launch "
                         "/ launch time (HIP events); the weights are LDS/VGPR-resident on one XCD's 32 CUs "
-                        "(fatchord_xcd_kernel), the kernel is hand-off-latency bound. "
-                        f"traffic = 2 x FETCH_SIZE + WRITE_SIZE bytes per launch (gfx950 read correction), NOT measured "
-                        f"in this run: read from the committed rocprofv3 --pmc passes of the same command in "
-                        f"{os.path.relpath(PMC_PROFILE, REPO)} (traffic_from): conditioning-terms reads; the hand-offs "
-                        f"stay in the XCD's L2",
+                        "(fatchord_xcd_kernel), the kernel is hand-off-latency bound. traffic = 2 x FETCH_SIZE + "
+                        "WRITE_SIZE bytes of the headline launch (gfx950 read correction; traffic_from says whether "
+                        "the passes ran in this bench or came from the committed profile): conditioning-terms "
+                        "reads; the hand-offs stay in the XCD's L2",
             },
         }
         if args.fold_batched and not args.batched and args.mode == "MOL":
             # the same utterance through the reference's default generate() mode
             # (hparams voc_gen_batched = True: 11000/550 folds, one multi-row launch)
             model.generate(mel, None, True, target, overlap, True, seed=7, verbose=False)
-            torch.cuda.synchronize()
-            tb = time.perf_counter()
-            outb = model.generate(mel, None, True, target, overlap, True, seed=8, verbose=False)
-            torch.cuda.synchronize()
-            dtb = time.perf_counter() - tb
+            outb, dtb = _timed(lambda: model.generate(mel, None, True, target, overlap, True, seed=8, verbose=False))
             kb = model.loop_handle().elapsed_ms()
             condb, _ = model.conditioning(mel, True, target, overlap)
             rec["fold_batched"] = {
@@ -327,17 +488,18 @@ def main():
                         "hparams (10 folds in one launch) + conditioning-terms GEMM; rate over the whole "
                         "generate() wall time (upsample, loop, float64 post)",
             }
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
         if args.other_configs and world == 1 and args.mode == "MOL":
-            rec["other_configs"] = other_configs(dev)
+            rec["other_configs"] = other_configs(dev, cpu_steps=min(args.cpu_steps, 2000), threads=threads)
             for key, v in rec["other_configs"].items():
-                tr = pmc_config_traffic(key)
+                tr = (traffic or {}).get("other_configs", {}).get(key)
                 if tr is not None and "roofline" in v:
-                    v["roofline"]["traffic_per_step"] = tr   # HBM bytes per loop step (PMC, corrected)
+                    v["roofline"]["traffic_per_step"] = tr["bytes_per_step"]   # HBM bytes per loop step (PMC)
+                    v["roofline"]["traffic_from"] = traffic_from
         if args.cpu_steps > 0 and world == 1:
             # the reference's op sequence on this host's cores: PyTorch-CPU eager (oracle/torch_cpu.py),
             # whole pre/post + a bounded slice of the loop; and the C oracle on the same slice
             from oracle import oracle, torch_cpu
-            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
             n = min(args.cpu_steps, L)
             noise = syn.make_noise(d.mode, B, L, d.n_classes, 7)
             r = torch_cpu.timed_generate(state, d, mel[0].numpy(), args.batched, target, overlap, True, noise,

@@ -92,8 +92,11 @@ typedef struct {
                                 block-sparse rnn 896, 7 XCD-resident many-row, 8 XCD-resident
                                 deepmind, 9 multi-row with the weights streamed from HBM (dense
                                 weights beyond LDS), 10 deepmind streamed (0: none yet) */
-    int32_t xcd_rows;        /* XCD-resident kernel (dense rnn 512, or rnn 896 with block-sparse
-                                GRU weights once they are set): rows per launch (0: unavailable) */
+    int32_t xcd_rows;        /* XCD-resident kernel, rows per launch (0: unavailable).  RAW/MOL
+                                handles: the one-row-per-XCD kernel (dense rnn 512, or rnn 896
+                                with block-sparse GRU weights once they are set), 8.  DM handles
+                                (ABI 5): the XCD-resident deepmind kernel (hidden 896 / Q 256,
+                                4 rows per XCD), 32. */
     int32_t xcdm_rows;       /* XCD-resident many-row kernel (MoL rnn/fc 512): rows per launch
                                 (0: unavailable)                                           (ABI 5) */
 } wrnn_info;

@@ -14,6 +14,8 @@ behaviour with the same eager torch ops on the CPU:
                           residual, cat + fc1 + relu, cat + fc2 + relu, fc3, then the MoL sampler
                           (utils/distribution.py:87-123) or softmax + Categorical (:231-237)
   post                    :243-258 (float64 numpy, oracle.postprocess)
+  deepmind loop           models/deepmind_version.py:98-156 (config 5's cpu_baseline): R, the
+                          coarse gates, O1/O2 + softmax + Categorical, the fine half likewise
 
 The sampler draws are injected ([L][B][K], the reference draw order of SURVEY.md §8(b)), so
 the result can be checked against the C oracle (tests/test_torch_cpu_baseline.py)."""
@@ -136,3 +138,55 @@ def timed_generate(state, dims, mel: np.ndarray, batched: bool, target: int, ove
     t3 = time.perf_counter()
     return {"pre_s": t1 - t0, "loop_s": t2 - t1, "post_s": t3 - t2, "loop_steps": n, "L": L, "rows": B,
             "out": out, "wave": wave, "threads": torch.get_num_threads()}
+
+
+def deepmind_loop(state: Dict[str, np.ndarray], B: int, noise: np.ndarray, steps: int) -> np.ndarray:
+    """deepmind_version.py:98-156 for B independent rows (the reference runs one), `steps` steps;
+    noise [L][B][2Q] Exp(1) (coarse q, then fine q; Categorical.sample ≡ argmax(probs / q)).
+    Returns output [B][steps] int64 = coarse·256 + fine − 2^15 (utils/dsp.py:33-34)."""
+    R = _t(state, "R.weight")
+    O1w, O1b, O2w, O2b = (_t(state, k) for k in ("O1.weight", "O1.bias", "O2.weight", "O2.bias"))
+    O3w, O3b, O4w, O4b = (_t(state, k) for k in ("O3.weight", "O3.bias", "O4.weight", "O4.bias"))
+    Ic, If = _t(state, "I_coarse.weight"), _t(state, "I_fine.weight")
+    H = R.shape[1]
+    S, Q = H // 2, O2w.shape[0]
+    bu, br, be = (_t(state, k) for k in ("bias_u", "bias_r", "bias_e"))
+    (bcu, bfu), (bcr, bfr), (bce, bfe) = (torch.split(b, S) for b in (bu, br, be))   # (:80-83)
+    nz = torch.as_tensor(np.ascontiguousarray(noise[:steps]), dtype=torch.float32)
+    out_c = torch.zeros(B, dtype=torch.long)                                         # (:89-90)
+    out_f = torch.zeros(B, dtype=torch.long)
+    hidden = torch.zeros(B, H)
+    res = torch.empty(B, steps, dtype=torch.int64)
+    with torch.no_grad():
+        for i in range(steps):
+            hc, hf = torch.split(hidden, S, dim=1)                                   # (:102-103)
+            prev = torch.stack([out_c.float() / 127.5 - 1.0, out_f.float() / 127.5 - 1.0], dim=1)
+            Icu, Icr, Ice = torch.split(F.linear(prev, Ic), S, dim=1)                # (:111-113)
+            Rcu, Rfu, Rcr, Rfr, Rce, Rfe = torch.split(F.linear(hidden, R), S, dim=1)   # (:116-119)
+            u = torch.sigmoid(Rcu + Icu + bcu)                                       # (:122-125)
+            r = torch.sigmoid(Rcr + Icr + bcr)
+            e = torch.tanh(r * Rce + Ice + bce)
+            hc = u * hc + (1.0 - u) * e
+            p = F.softmax(F.linear(F.relu(F.linear(hc, O1w, O1b)), O2w, O2b), dim=1)   # (:128-129)
+            out_c = (p / nz[i, :, :Q]).argmax(dim=1)                                 # Categorical (:130-131)
+            fin = torch.cat([prev, (out_c.float() / 127.5 - 1.0).unsqueeze(1)], dim=1)  # (:135-136)
+            Ifu, Ifr, Ife = torch.split(F.linear(fin, If), S, dim=1)
+            u = torch.sigmoid(Rfu + Ifu + bfu)                                       # (:142-145)
+            r = torch.sigmoid(Rfr + Ifr + bfr)
+            e = torch.tanh(r * Rfe + Ife + bfe)
+            hf = u * hf + (1.0 - u) * e
+            p = F.softmax(F.linear(F.relu(F.linear(hf, O3w, O3b)), O4w, O4b), dim=1)   # (:148-149)
+            out_f = (p / nz[i, :, Q:]).argmax(dim=1)
+            hidden = torch.cat([hc, hf], dim=1)                                      # (:154)
+            res[:, i] = out_c * 256 + out_f - 2 ** 15
+    return res.numpy()
+
+
+def timed_deepmind(state, B: int, noise: np.ndarray, steps: int, threads: Optional[int] = None) -> dict:
+    """deepmind_loop over a bounded slice of `steps` steps × B rows, wall-timed."""
+    if threads:
+        torch.set_num_threads(threads)
+    t0 = time.perf_counter()
+    out = deepmind_loop(state, B, noise, steps)
+    return {"loop_s": time.perf_counter() - t0, "steps": steps, "rows": B, "out": out,
+            "threads": torch.get_num_threads()}

@@ -2,6 +2,7 @@
 from the seeds it records, checking the SHA-256 digests made at generation time."""
 from __future__ import annotations
 
+import ast
 import os
 
 import numpy as np
@@ -27,9 +28,15 @@ def load(name: str) -> dict:
 
 
 def dims_of(fx: dict):
+    """The dims record make_golden stored (the repr of a frozen dataclass), parsed — never
+    evaluated: one call of FatchordDims / DeepmindDims whose keyword values are literals."""
     text = str(fx["dims"])
-    assert text.startswith("FatchordDims(") or text.startswith("DeepmindDims(")
-    return eval("syn." + text, {"syn": syn})  # repr of a frozen dataclass written by make_golden
+    tree = ast.parse(text, mode="eval").body
+    if not (isinstance(tree, ast.Call) and isinstance(tree.func, ast.Name) and not tree.args
+            and tree.func.id in ("FatchordDims", "DeepmindDims")):
+        raise ValueError(f"unexpected dims record {text!r}")
+    kwargs = {kw.arg: ast.literal_eval(kw.value) for kw in tree.keywords}
+    return getattr(syn, tree.func.id)(**kwargs)
 
 
 def loop_inputs(fx: dict):

@@ -2,7 +2,9 @@
 
 * config 3 (MoL rnn 512, one 60 s utterance fold-batched = 115 rows of 12 100 steps): all 115
   rows in one generate() call, 300 steps, MoL |Δ| <= MOL_TOL vs the oracle; the RAW 9-bit model
-  at the same row count, labels bit-exact.
+  at the same row count, labels bit-exact; and the whole 12 100 steps of all 115 rows against the
+  C oracle's full-length fixture (tests/golden/long_mol_fold115.npz: rows 0/7/64/114 at every
+  step, every row at every 50th).
 * config 5 (deepmind 896/256, 32 utterances per GPU): 32 rows × 1 000 steps, every coarse/fine
   label and combined sample bit-exact vs the oracle (deepmind_version.py:98-156).
 Injected noise in the reference draw order; tolerances as tests/golden/fixtures.py."""
@@ -57,4 +59,24 @@ def test_config5_32_rows_bit_exact():
     got = comb.cpu().numpy().astype(np.int64)
     eq = got == ref
     assert eq.all(), f"{eq.mean():.6f} equal, first mismatch {np.argwhere(~eq)[0].tolist()}"
+    loop.close()
+
+
+def test_config3_115_rows_full_length_vs_oracle_fixture():
+    """No drift at 115 rows over a whole fold (12 100 steps): the many-row kernel against the C
+    oracle's output (make_long_fixtures.py), same injected noise."""
+    from wavernn_amd.loop import FatchordLoop
+    fx = gf.load("long_mol_fold115")
+    d, state, mels, aux, noise = gf.loop_inputs(fx)
+    assert (int(fx["B"]), int(fx["L"])) == (115, 12100)
+    loop = FatchordLoop(d.mode, d.rnn_dims, d.fc_dims, d.aux_dims, d.feat_dims, d.n_classes, device=0)
+    loop.set_weights(state)
+    out, _ = loop.generate(_cond(mels, aux), noise=torch.from_numpy(noise).to(DEV))
+    assert loop.info["last_path"] == 7
+    got = out.cpu().numpy()
+    sub = int(fx["sub"])
+    for name, a, b in (("full rows", got[fx["full_rows"]], fx["out_full"]), ("every row", got[:, ::sub], fx["out_sub"])):
+        err = np.abs(a - b)
+        print(f"config 3 {name}: max |Δ| {err.max():.3g}, mean {err.mean():.3g}")
+        assert err.max() <= gf.MOL_TOL, f"{name}: max |Δ| {err.max()} at {np.unravel_index(err.argmax(), err.shape)}"
     loop.close()

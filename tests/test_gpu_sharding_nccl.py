@@ -1,6 +1,7 @@
 """generate_sharded under the "nccl" backend (RCCL) on the GPU box: world_size 1, one process,
-127.0.0.1 rendezvous.  The gathered float64 audio equals each utterance's own generate()
-bit-for-bit (the same Philox keying by global utterance index)."""
+127.0.0.1 rendezvous.  The gathered float64 audio (one generate_many launch per rank) equals
+each utterance's own generate() bit-for-bit under the same Philox keying by global row id; the
+deepmind variant likewise."""
 import os
 import socket
 
@@ -34,7 +35,16 @@ def test_generate_sharded_nccl_world1():
         got = sharding.generate_sharded(m, mels, False, 11000, 550, True, base_seed=77, device=dev)
         assert dist.get_backend() == "nccl" and len(got) == 3
         for i, mel in enumerate(mels):
-            ref = m.generate(mel, None, False, 11000, 550, True, seed=77 + i, verbose=False)
+            ref = m.generate(mel, None, False, 11000, 550, True, seed=77, row_offset=i, verbose=False)
             assert got[i].dtype == np.float64 and np.array_equal(got[i], ref)
+        from wavernn_amd.deepmind_version import WaveRNN as DM
+        dd = syn.DEFAULT_DM
+        dm = DM(**dd.ctor_kwargs()).to(dev)
+        dm.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in syn.make_deepmind_state(dd, 2).items()})
+        got = sharding.generate_sharded_deepmind(dm, 5, 300, base_seed=9, device=dev)
+        assert len(got) == 5
+        for i in range(5):
+            ref, _, _ = dm.generate(300, seed=9, row_offset=i)
+            assert got[i].dtype == np.int64 and np.array_equal(got[i], ref), i
     finally:
         dist.destroy_process_group()

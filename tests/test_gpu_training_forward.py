@@ -1,6 +1,6 @@
 """§8(f)4: the training-side teacher-forced forward (models/fatchord_version.py:131-167;
 deepmind_version.py:36-72) runs on the MI355X with the GRUs on MIOpen (torch.nn.GRU on ROCm) —
-forward (1e-4) and backward (1e-2 of each parameter's largest gradient) against the same module
+forward (1e-4) and backward (2e-3 of each parameter's largest gradient) against the same module
 on the CPU (ATen): fp32 tolerances for the different kernels' summation orders."""
 import numpy as np
 import pytest
@@ -44,13 +44,18 @@ def test_fatchord_training_forward_backward_on_miopen(mode):
     assert (yg.detach().cpu() - yc.detach()).abs().max().item() <= 1e-4
     yc.square().mean().backward()
     yg.square().mean().backward()
+    rel = {}
     for (n, pc), (_, pg) in zip(cpu.named_parameters(), gpu.named_parameters()):
         if pc.grad is None:
             continue
-        # (reductions over B·T = 2 200 rows in other orders and MIOpen's GRU backward: observed up
-        # to 2.3e-3 of a parameter's largest gradient; a wrong backward is off by O(1))
+        # reductions over B·T = 2 200 rows in other orders and MIOpen's GRU backward: observed
+        # 4.7e-4 of a parameter's largest gradient (fc2.weight, RAW, profiles/r03_v4_pytest_gpu.log);
+        # a wrong backward is off by O(1)
         err = (pg.grad.cpu() - pc.grad).abs().max().item()
-        assert err <= 1e-2 * pc.grad.abs().max().item() + 1e-6, (n, err)
+        rel[n] = err / (pc.grad.abs().max().item() + 1e-12)
+        assert err <= 2e-3 * pc.grad.abs().max().item() + 1e-7, (n, err)
+    worst = max(rel, key=rel.get)
+    print(f"\n{mode}: largest relative gradient error {rel[worst]:.2e} ({worst})")
 
 
 def test_deepmind_training_forward_on_gpu():

@@ -113,26 +113,20 @@ def test_xcds_one_second_vs_oracle(monkeypatch):
     assert err.max() <= gf.MOL_TOL, f"max |Δ| {err.max()} at {np.unravel_index(err.argmax(), err.shape)}"
 
 
-def test_xcds_five_seconds_vs_rows_kernel(monkeypatch):
-    """Config 4 at its own length: a whole 5 s utterance (110 275 steps) of the sparse rnn-896
-    model through the sparse XCD kernel and through the sparse multi-row kernel — two independent
-    implementations — under the same injected noise (the C oracle would take ~10 min here; it
-    pins both kernels at 1 s above): no drift between them over the utterance."""
-    d = syn.SPARSE896_MOL
-    L = syn.frames_for_seconds(5.0) * 275
-    assert L == 110275
-    state = prune_state(syn.make_fatchord_state(d, 670), 0.95)
-    mels, aux = syn.make_conditioning(1, L, d.feat_dims, d.res_out_dims, 671)
-    noise = torch.from_numpy(syn.make_noise("MOL", 1, L, d.n_classes, 672)).to(DEV)
-    cond = _cond(mels, aux)
-    res = {}
-    for p, path in (("", 6), ("rows", 2)):
-        monkeypatch.setenv("WRNN_PATH", p)
-        loop = _loop(d)
-        loop.set_weights(state)
-        res[p], _ = loop.generate(cond, noise=noise)
-        assert loop.info["last_path"] == path
-        loop.close()
-    err = (res[""] - res["rows"]).abs()
-    print(f"sparse 5 s (110 275 steps) xcds vs rows: max |Δ| {err.max().item():.3g}, mean {err.mean().item():.3g}")
-    assert err.max().item() <= 2 * gf.MOL_TOL
+def test_xcds_five_seconds_vs_oracle_fixture(monkeypatch):
+    """Config 4 at its own length: a whole 5 s utterance (110 275 steps) of the 95 %-pruned
+    rnn-896 model through the sparse XCD kernel against the C oracle's full-length output
+    (tests/golden/long_sparse896_5s.npz, make_long_fixtures.py; the oracle is pinned to the
+    reference by the reference fixtures), under the same injected noise: no drift."""
+    monkeypatch.delenv("WRNN_PATH", raising=False)
+    fx = gf.load("long_sparse896_5s")
+    d, state, mels, aux, noise = gf.loop_inputs(fx)
+    assert int(fx["L"]) == 110275
+    loop = _loop(d)
+    loop.set_weights(state)
+    out, _ = loop.generate(_cond(mels, aux), noise=torch.from_numpy(noise).to(DEV))
+    assert loop.info["last_path"] == 6
+    err = np.abs(out.cpu().numpy()[fx["full_rows"]] - fx["out_full"])
+    print(f"sparse 5 s (110 275 steps) vs oracle: max |Δ| {err.max():.3g}, mean {err.mean():.3g}")
+    assert err.max() <= gf.MOL_TOL, f"max |Δ| {err.max()} at {np.unravel_index(err.argmax(), err.shape)}"
+    loop.close()

@@ -1,10 +1,14 @@
 """INTEGRATION.md section B — the ctypes binding a reference maintainer would add to
 models/fatchord_version.py — executed as written (only the library path is made absolute), on a
-module with the reference constructor and state_dict keys (the drop-in WaveRNN, on the CPU; not
-the reference itself).  Without a GPU the loop call must fail through wrnn_create's status."""
+module with the reference constructor and state_dict keys (the drop-in WaveRNN; not the
+reference itself).  Without a GPU the loop call must fail through wrnn_create's status; on the
+MI355X it runs the persistent kernel and matches the C oracle (injected noise) and the package's
+own FatchordLoop (Philox)."""
 import ctypes
 import os
 import re
+
+import numpy as np
 
 import pytest
 import torch
@@ -69,3 +73,31 @@ def test_snippet_fails_cleanly_without_gpu():
     rc = lib.wrnn_create(ctypes.byref(ns["_wrnn_cfg"](m)), 0, ctypes.byref(h))
     assert rc < 0
     lib.wrnn_destroy(h)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d", [syn.DEFAULT_MOL, syn.TINY_MOL])
+def test_snippet_hip_loop_on_gpu(d):
+    from oracle import oracle
+    from tests.golden import fixtures as gf
+    from wavernn_amd.loop import FatchordLoop
+    ns = _snippet_ns()
+    m = _model(d)
+    state = syn.make_fatchord_state(d, 21)
+    m.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in state.items()})
+    m = m.to("cuda")
+    B, L = 2, 700
+    mels, aux = syn.make_conditioning(B, L, d.feat_dims, d.res_out_dims, 22)
+    noise = syn.make_noise(d.mode, B, L, d.n_classes, 23)
+    gm, ga = torch.from_numpy(mels).cuda(), torch.from_numpy(aux).cuda()
+    out = ns["_hip_loop"](m, gm, ga, seed=1, noise=torch.from_numpy(noise).cuda())
+    ref, _ = oracle.fatchord_loop(state, d.mode, mels, aux, noise)
+    assert np.abs(out.cpu().numpy() - ref).max() <= gf.MOL_TOL
+    # Philox: the snippet and the package's binding run the same launch
+    out_p = ns["_hip_loop"](m, gm, ga, seed=99)
+    loop = FatchordLoop(d.mode, d.rnn_dims, d.fc_dims, d.aux_dims, d.feat_dims, d.n_classes)
+    loop.set_weights(state)
+    cond = torch.cat([gm, ga], 2).transpose(0, 1).contiguous()
+    y, _ = loop.generate(cond, seed=99)
+    assert torch.equal(out_p, y)
+    loop.close()

@@ -1,8 +1,9 @@
 """Multi-process (gloo, world_size 2, CPU) tests of utterance sharding + the audio gather.
 
-generate() itself needs a GPU, so the per-utterance generator is replaced by a deterministic
-function of the global utterance index; what is under test is the partition and the
-collective that reassembles the audio on rank 0 in input order."""
+generate_many() itself needs a GPU, so the per-block generator is replaced by a deterministic
+function of the global utterance index and the global row id the block starts at; what is
+under test is the partition, the row-id bookkeeping (Philox keys) and the collective that
+reassembles the audio on rank 0 in input order."""
 import os
 import socket
 
@@ -29,28 +30,54 @@ def fake_audio(i: int) -> np.ndarray:
     return a
 
 
-def _worker(rank, world, port, n_items, q):
+class _RowsModel:
+    """Stand-in for WaveRNN.rows_of: a "mel" is its frame count; batched → T // 10 + 1 folds."""
+
+    @staticmethod
+    def rows_of(T, batched, target, overlap):
+        return T // 10 + 1 if batched else 1
+
+
+def _rows_before(mels, i, batched):
+    return sum(_RowsModel.rows_of(m, batched, 0, 0) for m in mels[:i])
+
+
+def _worker(rank, world, port, n_items, batched, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        out = sharding.generate_sharded(None, [None] * n_items, False, 0, 0, False, device=torch.device("cpu"),
-                                        generate_fn=lambda i, m: fake_audio(i))
+        mels = [np.zeros((1, 4, 20 + 7 * i)) for i in range(n_items)]
+        calls = []
+
+        def gen(ii, ms, r0):
+            calls.append(len(ii))
+            # one launch per rank: the block's first row id is the global one
+            assert r0 == _rows_before([m.shape[-1] for m in mels], ii[0], batched)
+            return [fake_audio(i) for i in ii]
+
+        out = sharding.generate_sharded(_RowsModel(), mels, batched, 0, 0, False, device=torch.device("cpu"),
+                                        generate_fn=gen)
+        assert len(calls) <= 1
+        dm = sharding.generate_sharded_deepmind(None, n_items, 5, device=torch.device("cpu"),
+                                                generate_fn=lambda ii, r0: [np.arange(5) * 1000 - 32768 + i
+                                                                            for i in ii])
         if rank == 0:
-            q.put([None if o is None else o.tolist() for o in out])
+            q.put(([None if o is None else o.tolist() for o in out], [d.tolist() for d in dm],
+                   [str(d.dtype) for d in dm]))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n_items", [5, 2, 1])
-def test_sharded_gather_reassembles_in_order(n_items):
+@pytest.mark.parametrize("n_items,batched", [(5, False), (2, True), (1, False), (9, True)])
+def test_sharded_gather_reassembles_in_order(n_items, batched):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_items, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_items, batched, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = q.get(timeout=120)
+    got, dm, dm_dtypes = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -59,11 +86,15 @@ def test_sharded_gather_reassembles_in_order(n_items):
         a = np.asarray(a)
         assert a.dtype == np.float64
         np.testing.assert_array_equal(a, fake_audio(i))     # bit-exact float64
+    assert dm_dtypes == ["int64"] * n_items
+    for i, d in enumerate(dm):
+        np.testing.assert_array_equal(d, np.arange(5) * 1000 - 32768 + i)
 
 
 def test_shard_indices_partition():
     for n in (0, 1, 7, 64):
         for world in (1, 2, 3, 8):
             parts = [sharding.shard_indices(n, r, world) for r in range(world)]
-            flat = sorted(i for p in parts for i in p)
-            assert flat == list(range(n))
+            flat = [i for p in parts for i in p]
+            assert flat == list(range(n))                    # contiguous blocks, in order
+            assert max(map(len, parts)) - min(map(len, parts)) <= 1

@@ -47,3 +47,14 @@ def test_timed_generate_matches_oracle_generate():
     r = torch_cpu.timed_generate(state, d, mel, True, target, overlap, False, noise)
     assert r["loop_steps"] == folds[1] and r["rows"] == folds[0]
     assert np.abs(r["wave"] - ref).max() <= 2 * gf.MOL_TOL
+
+
+def test_deepmind_loop_matches_c_oracle():
+    """config 5's cpu_baseline restatement: every coarse/fine label equals the pinned C oracle's"""
+    d = syn.TINY_DM
+    B, L = 3, 300
+    state = syn.make_deepmind_state(d, 4)
+    noise = syn.make_dm_noise(B, L, d.quantisation, 5)
+    _, _, ref = oracle.deepmind_loop(state, B, L, noise)
+    got = torch_cpu.deepmind_loop(state, B, noise, L)
+    assert got.dtype == np.int64 and np.array_equal(got, ref)

@@ -21,11 +21,14 @@ import sys
 
 HEADLINE = ("fatchord_xcd_kernel", "fatchord_split_kernel", "fatchord_loop_kernel")
 # loop kernel -> (config key in bench.py's other_configs, loop steps of its dispatches in one
-# bench.py --steps 1 --other-configs 1 run: warm-up + timed generate of that config)
-OTHER = {"fatchord_xcdm_kernel": ("config3_mol_fold_60s", 2 * 12100),
-         "fatchord_xcds_kernel": ("config4_sparse896_8utt", 100 + 110275),
-         "deepmind_rows_kernel": ("config5_deepmind_32utt", 100 + 16000),
-         "deepmind_xcd_kernel": ("config5_deepmind_32utt", 100 + 16000)}
+# bench.py --pmc-child run: every config generated ONCE, no warm-up calls, no fold-batched line).
+# The headline is the FIRST headline-kernel dispatch; later fatchord_xcd_kernel dispatches are the
+# 8-utterance line (config2_8_streams).
+OTHER = {"fatchord_xcdm_kernel": ("config3_mol_fold_60s", 12100),
+         "fatchord_xcds_kernel": ("config4_sparse896_8utt", 110275),
+         "deepmind_rows_kernel": ("config5_deepmind_32utt", 16000),
+         "deepmind_xcd_kernel": ("config5_deepmind_32utt", 16000),
+         "fatchord_xcd_kernel": ("config2_8_streams", 110275)}
 
 
 def rows(path):
@@ -33,18 +36,20 @@ def rows(path):
         yield from csv.DictReader(f)
 
 
+def _order(r):
+    return int(r.get("Dispatch_Id") or r.get("Correlation_Id") or 0)
+
+
 def loop_dispatch(path):
-    best = None
-    for r in rows(path):
-        if not any(k in r["Kernel_Name"] for k in HEADLINE):
-            continue
-        dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-        if best is None or dur > best[2]:
-            best = (r["Kernel_Name"], float(r["Counter_Value"]), dur)
-    return best
+    """(name, KiB, duration) of the headline launch: the first headline-kernel dispatch."""
+    hits = [r for r in rows(path) if any(k in r["Kernel_Name"] for k in HEADLINE)]
+    if not hits:
+        return None
+    r = min(hits, key=_order)
+    return r["Kernel_Name"], float(r["Counter_Value"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), _order(r)
 
 
-def other_sums(path):
+def other_sums(path, headline_id):
     out = {}
     for r in rows(path):
         name = r["Kernel_Name"]
@@ -52,19 +57,22 @@ def other_sums(path):
         # are not config 3's
         if "fatchord_xcdm_kernel" in name and re.search(r"fatchord_xcdm_kernel<\d+, \w+, true>", name):
             continue
+        if _order(r) == headline_id:
+            continue
         for k in OTHER:
             if k in name:
                 out[k] = out.get(k, 0.0) + float(r["Counter_Value"])
     return out
 
 
-def main(src, dst):
+def summarise(src):
+    """The two passes under <src>/pmc_FETCH_SIZE, <src>/pmc_WRITE_SIZE → the traffic record."""
     counters, others = {}, {}
     for c in ("FETCH_SIZE", "WRITE_SIZE"):
         path = f"{src}/pmc_{c}/pmc_counter_collection.csv"
-        name, kib, dur = loop_dispatch(path)
+        name, kib, dur, hid = loop_dispatch(path)
         counters[c] = {"kernel": name, "value_kib": kib, "duration_ns": dur}
-        for k, v in other_sums(path).items():
+        for k, v in other_sums(path, hid).items():
             others.setdefault(k, {})[c] = v
     headline_bytes = 1024.0 * (2.0 * counters["FETCH_SIZE"]["value_kib"] + counters["WRITE_SIZE"]["value_kib"])
     cfg = {}
@@ -74,19 +82,21 @@ def main(src, dst):
             b = 1024.0 * (2.0 * v["FETCH_SIZE"] + v["WRITE_SIZE"])
             cfg[key] = {"kernel": k, "fetch_kib": v["FETCH_SIZE"], "write_kib": v["WRITE_SIZE"], "loop_steps": steps,
                         "bytes_per_step": b / steps}
-    out = {
+    return {
         "workload": "MOL rnn512 B=1 5 s (110275 steps), one persistent launch",
         "counters": counters,
         "bytes": headline_bytes,
         "other_configs": cfg,
-        "note": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (bench.py --steps 1). Counter "
-                "values in KiB per dispatch; bytes = 1024 x (2 x FETCH_SIZE + WRITE_SIZE), the gfx950 correction for "
-                "16-B-per-lane reads (MI355X_MICROARCH.md). The XCD kernel's hand-offs are plain 8-byte stores and "
-                "16-byte sc1 polls served by the XCD's L2; its HBM traffic is the float4 reads of the 640 B/step/"
-                "workgroup conditioning terms (32 x 640 = 20 480 B per step). The rows kernels (configs 3, 5) also "
-                "poll 4-byte flags and 8-byte granules, widths the guide leaves uncalibrated, so their bytes_per_step "
-                "are approximate; their HBM traffic is dominated by the sc1 activation-tile LDS-DMA (16 B per lane).",
+        "note": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes of bench.py --pmc-child (every "
+                "config once, no warm-up). Counter values in KiB per dispatch; bytes = 1024 x (2 x FETCH_SIZE + "
+                "WRITE_SIZE), the gfx950 correction for 16-B-per-lane reads (MI355X_MICROARCH.md). The XCD kernels' "
+                "hand-offs are plain stores and 16-byte sc1 polls served by the XCD's L2; their HBM traffic is the "
+                "float4 reads of the conditioning terms (one row: 32 x 640 = 20 480 B per step) and the draws.",
     }
+
+
+def main(src, dst):
+    out = summarise(src)
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))

@@ -24,11 +24,33 @@ def hipcc() -> str:
     return "hipcc"
 
 
+OBJDIR = os.path.join(os.path.dirname(OUT), "obj")
+
+
+def _compile_cmd(src: str) -> list:
+    common = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-I" + os.path.join(REPO, "include")]
+    return common + EXTRA_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", _obj(src)]
+
+
+def _obj(src: str) -> str:
+    return os.path.join(OBJDIR, os.path.basename(src) + ".o")
+
+
+def _stamp_ok(src: str) -> bool:
+    """The object was compiled by exactly today's command (arch and flags included): each object
+    keeps its command line in <obj>.cmd, so a changed WRNN_OFFLOAD_ARCH or flag rebuilds it."""
+    try:
+        with open(_obj(src) + ".cmd") as f:
+            return f.read() == " ".join(_compile_cmd(src))
+    except OSError:
+        return False
+
+
 def up_to_date() -> bool:
     if not os.path.exists(OUT):
         return False
     t = os.path.getmtime(OUT)
-    return all(os.path.getmtime(s) <= t for s in SOURCES + HEADERS)
+    return all(os.path.getmtime(s) <= t for s in SOURCES + HEADERS) and all(_stamp_ok(s) for s in SOURCES)
 
 
 # per-source extra flags: the multi-row kernel's register-blocked dots are plain fp32 FMAs; the
@@ -44,23 +66,26 @@ def build(force: bool = False, verbose: bool = True) -> str:
     if not force and up_to_date():
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    objdir = os.path.join(os.path.dirname(OUT), "obj")
-    os.makedirs(objdir, exist_ok=True)
-    common = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-I" + os.path.join(REPO, "include")]
+    os.makedirs(OBJDIR, exist_ok=True)
     newest_header = max(os.path.getmtime(h) for h in HEADERS)
-    objs, cmds = [], []
+    objs, todo = [], []
     for src in SOURCES:
-        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        obj = _obj(src)
         objs.append(obj)
-        if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), newest_header):
-            cmds.append(common + EXTRA_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj])
-    jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1)), 8))
+        if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), newest_header) \
+                or not _stamp_ok(src):
+            todo.append(src)
+    jobs = max(1, min(len(todo), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1)), 8))
     with ThreadPoolExecutor(max_workers=jobs) as ex:
-        for cmd in cmds:
+        for src in todo:
+            if os.path.exists(_obj(src) + ".cmd"):
+                os.remove(_obj(src) + ".cmd")
             if verbose:
-                print(" ".join(cmd), flush=True)
-        for f in [ex.submit(subprocess.run, cmd, check=True) for cmd in cmds]:
+                print(" ".join(_compile_cmd(src)), flush=True)
+        for src, f in [(src, ex.submit(subprocess.run, _compile_cmd(src), check=True)) for src in todo]:
             f.result()
+            with open(_obj(src) + ".cmd", "w") as fh:
+                fh.write(" ".join(_compile_cmd(src)))
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-lrocblas", "-o", OUT + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)

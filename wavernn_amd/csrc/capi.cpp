@@ -28,7 +28,7 @@ namespace wrnn {
 hipError_t launch_ci_gemm(const float *cond, int CD, int Bt, int b0, int Bc, int t0, int L, const float *W, int ldw,
                           const float *bias, int N, int K, float *cI, int ldc, hipStream_t st);
 hipError_t launch_pack_cond_input(const float *cond, int CD, int Bt, int b0, int B, int t0, int Lc, int KX, float *X,
-                                  hipStream_t st);
+                                  hipStream_t st, int split = 0);
 hipError_t launch_pack_terms_input(const float *cond, int CD, int Bt, int b0, int B, int t0, int Lc, int feat, int A,
                                    int R, int KX, float *X, hipStream_t st);
 hipError_t launch_rows(const RowsArgs &a, const RowsGroup *g1, size_t lds_bytes, hipStream_t st);
@@ -995,6 +995,39 @@ void pack_xcd_terms_weights(const wrnn_ctx &h, std::vector<float> &Wt) {
     }
 }
 
+// Many-row kernel: its compact terms record (kMRing slots per workgroup) SEGMENTED by type
+// (fatchord_xcdm.h, mterm_off) with the columns in the split input order X'' = [mel | a1 | 1 | a2 |
+// a3 | a4 | 1 | 0 0] (pack_cond_input_kernel, split = M + A): P1 and cI depend on mel‖a1 and their
+// bias only, P2 also on a2, V1 / V2 on a3 / a4 and their biases — generate_xcdm runs one GEMM per
+// segment group over just those columns (xcdm_terms_gemms).
+void pack_xcdm_terms_weights(const wrnn_ctx &h, std::vector<float> &Wm) {
+    std::vector<float> Wt;
+    pack_xcd_terms_weights(h, Wt);
+    const int KX = h.KXc, CD = h.CD, split = h.cfg.feat_dims + h.cfg.aux_dims;
+    Wm.assign((size_t)kXcdWgs * kMRing * KX, 0.0f);
+    for (int c = 0; c < kXcdWgs; ++c)
+        for (int s = 0; s < kMRing; ++s) {
+            const float *src = Wt.data() + ((size_t)c * kXTerms + s) * KX;
+            float *dst = Wm.data() + (size_t)mterm_off(c, s) * KX;
+            for (int j = 0; j < CD; ++j) dst[j < split ? j : j + 1] = src[j];
+            dst[s >= XT_V1 ? CD + 1 : split] = src[CD];          // the bias → its type's ones column
+        }
+}
+
+// (segment rows, first input column, depth): [P1 | cI] on mel‖a1‖1, P2 on mel‖a1‖1‖a2, [V1 | V2]
+// on a3‖a4‖1 — the depths rounded up to a multiple of 4 over columns whose weights are zero
+struct XcdmGemm {
+    int row0, rows, col0, k;
+};
+void xcdm_terms_gemms(const wrnn_ctx &h, XcdmGemm (&g)[3]) {
+    const int M = h.cfg.feat_dims, A = h.cfg.aux_dims, split = M + A;
+    auto up4 = [](int n) { return (n + 3) / 4 * 4; };
+    const int v0 = (split + 1 + A) / 4 * 4;                     // first column of a3, rounded down
+    g[0] = {kMSegP1, kMSegP2 - kMSegP1, 0, std::min(up4(split + 1), h.KXc)};
+    g[1] = {kMSegP2, kMSegV1 - kMSegP2, 0, std::min(up4(split + 1 + A), h.KXc)};
+    g[2] = {kMSegV1, kMSegEnd - kMSegV1, v0, std::min(up4(h.CD + 2 - v0), h.KXc - v0)};
+}
+
 // ---- XCD-resident block-sparse kernel (fatchord_xcds.h): workgroup c of an XCD owns units
 // 28c..28c+27 (block-rows ub = 0..6 of each gate) and fc rows 16c..16c+15
 void make_xcds_slab(wrnn_ctx &h) {
@@ -1189,6 +1222,39 @@ hipError_t ensure(T *&p, size_t &cap, size_t n) {
     return e;
 }
 
+// WRNN_DEBUG_STAMPS buffer: freed on every exit path (an early HIP_TRY / fail() return included);
+// the dump helpers take ownership by resetting p first
+struct DbgBuf {
+    unsigned *p = nullptr;
+    DbgBuf() = default;
+    DbgBuf(const DbgBuf &) = delete;
+    DbgBuf &operator=(const DbgBuf &) = delete;
+    ~DbgBuf() {
+        if (p) (void)hipFree(p);
+    }
+    unsigned *release() {
+        unsigned *q = p;
+        p = nullptr;
+        return q;
+    }
+};
+
+// per-wave stamps of the many-row / deepmind kernels: int32 header {waves, steps, stamps}
+int dump_wave_stamps(wrnn_t *h, DbgBuf &dbg, size_t n, int waves, int steps, int stamps, hipStream_t st) {
+    std::vector<unsigned> host(n);
+    HIP_TRY(h, hipStreamSynchronize(st));
+    HIP_TRY(h, hipMemcpy(host.data(), dbg.p, n * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(h, hipFree(dbg.release()));
+    const char *path = std::getenv("WRNN_DEBUG_FILE");
+    if (FILE *f = std::fopen(path ? path : "wrnn_stamps.bin", "wb")) {
+        int hdr[3] = {waves, steps, stamps};
+        std::fwrite(hdr, sizeof(hdr), 1, f);
+        std::fwrite(host.data(), 4, host.size(), f);
+        std::fclose(f);
+    }
+    return WRNN_OK;
+}
+
 // WRNN_DEBUG_FILE (default wrnn_stamps.bin): int32 header {G, steps, kStamps}, then the stamps
 int dump_stamps(wrnn_t *h, unsigned *d_dbg, int dbg_steps, hipStream_t st, int G) {
     std::vector<unsigned> host((size_t)G * dbg_steps * kStamps);
@@ -1245,10 +1311,10 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
     const float one = 1.0f, zero = 0.0f;
     const char *dbg_env = std::getenv("WRNN_DEBUG_STAMPS");
     const int dbg_steps = dbg_env ? std::min(L, std::atoi(dbg_env)) : 0;
-    unsigned *d_dbg = nullptr;
+    DbgBuf dbg;
     if (dbg_steps > 0) {
-        HIP_TRY(h, hipMalloc(&d_dbg, (size_t)h->rG * dbg_steps * kStamps * 4));
-        HIP_TRY(h, hipMemsetAsync(d_dbg, 0, (size_t)h->rG * dbg_steps * kStamps * 4, st));
+        HIP_TRY(h, hipMalloc(&dbg.p, (size_t)h->rG * dbg_steps * kStamps * 4));
+        HIP_TRY(h, hipMemsetAsync(dbg.p, 0, (size_t)h->rG * dbg_steps * kStamps * 4, st));
     }
     for (int b0 = 0; b0 < B;) {
         int Bl = std::min(B - b0, kRowsMax);
@@ -1341,7 +1407,7 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
             a.TB = TB;
             a.KA = h->KA;
             a.s = h->rs;
-            a.dbg = (b0 == 0 && t0 == 0) ? d_dbg : nullptr;
+            a.dbg = (b0 == 0 && t0 == 0) ? dbg.p : nullptr;
             a.dbg_steps = std::min(dbg_steps, Lc);
             a.head_lds = head_lds ? 1 : 0;
             a.gw = h->rows_gw ? 1 : 0;
@@ -1363,7 +1429,7 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
         }
         b0 += Bl;
     }
-    if (d_dbg) return dump_stamps(h, d_dbg, dbg_steps, st, h->rG);
+    if (dbg.p) return dump_stamps(h, dbg.release(), dbg_steps, st, h->rG);
     return WRNN_OK;
 }
 
@@ -1382,10 +1448,10 @@ int generate_dx(wrnn_t *h, int B, int L, const float *noise, uint64_t seed, int6
     const char *dbg_env = std::getenv("WRNN_DEBUG_STAMPS");
     const int dbg_steps = (dbg_env && std::atoi(dbg_env) > 0 && L >= kDxDbgSkip + kDxDbgSteps) ? kDxDbgSteps : 0;
     const size_t dbg_n = (size_t)kXcds * kXcdWgs * kDxWaves * dbg_steps * kDxStamps;
-    unsigned *d_dbg = nullptr;
+    DbgBuf dbg;
     if (dbg_steps > 0) {
-        HIP_TRY(h, hipMalloc(&d_dbg, dbg_n * 4));
-        HIP_TRY(h, hipMemsetAsync(d_dbg, 0, dbg_n * 4, st));
+        HIP_TRY(h, hipMalloc(&dbg.p, dbg_n * 4));
+        HIP_TRY(h, hipMemsetAsync(dbg.p, 0, dbg_n * 4, st));
     }
     for (int b0 = 0; b0 < B; b0 += kDxRowsMax) {
         const int nb = std::min(kDxRowsMax, B - b0);
@@ -1423,23 +1489,11 @@ int generate_dx(wrnn_t *h, int B, int L, const float *noise, uint64_t seed, int6
             a.b0 = b0;
             a.nb = nb;
             a.s = dx_slab_layout();
-            a.dbg = (b0 == 0 && t0 == 0 && Lc >= kDxDbgSkip + kDxDbgSteps) ? d_dbg : nullptr;
+            a.dbg = (b0 == 0 && t0 == 0 && Lc >= kDxDbgSkip + kDxDbgSteps) ? dbg.p : nullptr;
             HIP_TRY(h, launch_dx(a, st));
         }
     }
-    if (d_dbg) {
-        std::vector<unsigned> host(dbg_n);
-        HIP_TRY(h, hipStreamSynchronize(st));
-        HIP_TRY(h, hipMemcpy(host.data(), d_dbg, dbg_n * 4, hipMemcpyDeviceToHost));
-        HIP_TRY(h, hipFree(d_dbg));
-        const char *path = std::getenv("WRNN_DEBUG_FILE");
-        if (FILE *f = std::fopen(path ? path : "wrnn_stamps.bin", "wb")) {
-            int hdr[3] = {kXcds * kXcdWgs * kDxWaves, dbg_steps, kDxStamps};
-            std::fwrite(hdr, sizeof(hdr), 1, f);
-            std::fwrite(host.data(), 4, host.size(), f);
-            std::fclose(f);
-        }
-    }
+    if (dbg.p) return dump_wave_stamps(h, dbg, dbg_n, kXcds * kXcdWgs * kDxWaves, dbg_steps, kDxStamps, st);
     return WRNN_OK;
 }
 
@@ -1554,10 +1608,10 @@ int generate_split(wrnn_t *h, const float *cond, int B, int L, const float *nois
         return WRNN_EHIP;
     const char *dbg_env = std::getenv("WRNN_DEBUG_STAMPS");
     const int dbg_steps = dbg_env ? std::min(L, std::atoi(dbg_env)) : 0;
-    unsigned *d_dbg = nullptr;
+    DbgBuf dbg;
     if (dbg_steps > 0) {
-        HIP_TRY(h, hipMalloc(&d_dbg, (size_t)G * dbg_steps * kStamps * 4));
-        HIP_TRY(h, hipMemsetAsync(d_dbg, 0, (size_t)G * dbg_steps * kStamps * 4, st));
+        HIP_TRY(h, hipMalloc(&dbg.p, (size_t)G * dbg_steps * kStamps * 4));
+        HIP_TRY(h, hipMemsetAsync(dbg.p, 0, (size_t)G * dbg_steps * kStamps * 4, st));
     }
     const float one = 1.0f, zero = 0.0f;
     for (int b0 = 0; b0 < B; ++b0) {
@@ -1594,12 +1648,12 @@ int generate_split(wrnn_t *h, const float *cond, int B, int L, const float *nois
             a.reps = reps;
             a.gs = h->sgs;
             a.fs = h->sfs;
-            a.dbg = (b0 == 0 && t0 == 0) ? d_dbg : nullptr;
+            a.dbg = (b0 == 0 && t0 == 0) ? dbg.p : nullptr;
             a.dbg_steps = std::min(dbg_steps, Lc);
             HIP_TRY(h, launch_split(a, split_lds_bytes(*h), st));
         }
     }
-    if (d_dbg) return dump_stamps(h, d_dbg, dbg_steps, st, G);
+    if (dbg.p) return dump_stamps(h, dbg.release(), dbg_steps, st, G);
     return WRNN_OK;
 }
 
@@ -1623,19 +1677,12 @@ int generate_xcd_rows(wrnn_t *h, const float *cond, int B, int L, const float *n
     const char *mb_env = std::getenv("WRNN_TERMS_MB");
     const double budget = (mb_env ? std::atof(mb_env) : 8192.0) * (1 << 20) / 4.0;   // floats
     const size_t xg_words = (size_t)kXcds * kXXcdStride;
-    if (!h->d_members) {
-        HIP_TRY(h, hipMalloc(&h->d_members, kXcds * sizeof(int)));
-        HIP_TRY(h, hipMalloc(&h->d_xgx, xg_words * 8));
-    }
+    // each buffer under its own check: generate_xcdm / generate_dx allocate d_members too
+    if (!h->d_members) HIP_TRY(h, hipMalloc(&h->d_members, kXcds * sizeof(int)));
+    if (!h->d_xgx) HIP_TRY(h, hipMalloc(&h->d_xgx, xg_words * 8));
     const char *dbg_env = std::getenv("WRNN_DEBUG_STAMPS");
     const int dbg_steps = dbg_env ? std::min(L, std::atoi(dbg_env)) : 0;
-    // the stamp buffer is freed on every exit (dump_stamps frees it itself on success)
-    struct DbgBuf {
-        unsigned *p = nullptr;
-        ~DbgBuf() {
-            if (p) (void)hipFree(p);
-        }
-    } dbg;
+    DbgBuf dbg;
     int dbg_G = 0;
     const float one = 1.0f, zero = 0.0f;
     for (int b0 = 0; b0 < B; b0 += kXcds) {
@@ -1683,11 +1730,7 @@ int generate_xcd_rows(wrnn_t *h, const float *cond, int B, int L, const float *n
             HIP_TRY(h, launch(a, st));
         }
     }
-    if (dbg.p) {
-        unsigned *p = dbg.p;
-        dbg.p = nullptr;
-        return dump_stamps(h, p, dbg_steps, st, dbg_G);
-    }
+    if (dbg.p) return dump_stamps(h, dbg.release(), dbg_steps, st, dbg_G);
     return WRNN_OK;
 }
 
@@ -1722,15 +1765,17 @@ int generate_xcdm(wrnn_t *h, const float *cond, int B, int L, const float *noise
     if (!h->d_xmstate) HIP_TRY(h, hipMalloc(&h->d_xmstate, (size_t)kXcds * kXcdWgs * kMStateW * sizeof(float)));
     const int rows_max = kXcds * 4 * h->xcdm_nq;
     const float one = 1.0f, zero = 0.0f;
+    XcdmGemm gemms[3];
+    xcdm_terms_gemms(*h, gemms);
     // diagnostics: WRNN_DEBUG_STAMPS=1 WRNN_DEBUG_FILE=<path>: per-wave phase stamps of the first
     // launch ([256 · kMWaves][kMDbgSteps][kMStamps] shader clocks, int32 header)
     const char *dbg_env = std::getenv("WRNN_DEBUG_STAMPS");
     const int dbg_steps = (!raw && dbg_env && std::atoi(dbg_env) > 0 && L >= kMDbgSkip + kMDbgSteps) ? kMDbgSteps : 0;
     const size_t dbg_n = (size_t)kXcds * kXcdWgs * kMWaves * dbg_steps * kMStamps;
-    unsigned *d_dbg = nullptr;
+    DbgBuf dbg;
     if (dbg_steps > 0) {
-        HIP_TRY(h, hipMalloc(&d_dbg, dbg_n * 4));
-        HIP_TRY(h, hipMemsetAsync(d_dbg, 0, dbg_n * 4, st));
+        HIP_TRY(h, hipMalloc(&dbg.p, dbg_n * 4));
+        HIP_TRY(h, hipMemsetAsync(dbg.p, 0, dbg_n * 4, st));
     }
     for (int b0 = 0; b0 < B; b0 += rows_max) {
         const int nb = std::min(rows_max, B - b0);
@@ -1745,10 +1790,13 @@ int generate_xcdm(wrnn_t *h, const float *cond, int B, int L, const float *noise
             const int Lc = std::min(Lc_max, L - t0);
             if ((size_t)Lc * nb * h->KXc > h->X_cap || (size_t)Lc * nb * N > h->T_cap)
                 return fail(h, WRNN_EINVAL, "xcdm: terms workspace too small");
-            HIP_TRY(h, launch_pack_cond_input(cond, h->CD, B, b0, nb, t0, Lc, h->KXc, h->d_X, st));
-            if (rocblas_sgemm(h->blas, rocblas_operation_transpose, rocblas_operation_none, N, Lc * nb, h->KXc, &one,
-                              h->d_xmWt, h->KXc, h->d_X, h->KXc, &zero, h->d_T, N) != rocblas_status_success)
-                return fail(h, WRNN_EHIP, "rocblas_sgemm (conditioning terms) failed");
+            HIP_TRY(h, launch_pack_cond_input(cond, h->CD, B, b0, nb, t0, Lc, h->KXc, h->d_X, st,
+                                              h->cfg.feat_dims + h->cfg.aux_dims));
+            for (const XcdmGemm &g : gemms)
+                if (rocblas_sgemm(h->blas, rocblas_operation_transpose, rocblas_operation_none, g.rows, Lc * nb, g.k, &one,
+                                  h->d_xmWt + (size_t)g.row0 * h->KXc + g.col0, h->KXc, h->d_X + g.col0, h->KXc, &zero,
+                                  h->d_T + g.row0, N) != rocblas_status_success)
+                    return fail(h, WRNN_EHIP, "rocblas_sgemm (conditioning terms) failed");
             HIP_TRY(h, hipMemsetAsync(h->d_members, 0, kXcds * sizeof(int), st));
             XcdmArgs a{};
             a.slab = h->d_xmslab;
@@ -1781,23 +1829,11 @@ int generate_xcdm(wrnn_t *h, const float *cond, int B, int L, const float *noise
             a.b0 = b0;
             a.nb = nb;
             a.s = h->xms;
-            a.dbg = (b0 == 0 && t0 == 0 && Lc >= kMDbgSkip + kMDbgSteps) ? d_dbg : nullptr;
+            a.dbg = (b0 == 0 && t0 == 0 && Lc >= kMDbgSkip + kMDbgSteps) ? dbg.p : nullptr;
             HIP_TRY(h, launch_xcdm(a, nq, raw, st));
         }
     }
-    if (d_dbg) {
-        std::vector<unsigned> host(dbg_n);
-        HIP_TRY(h, hipStreamSynchronize(st));
-        HIP_TRY(h, hipMemcpy(host.data(), d_dbg, dbg_n * 4, hipMemcpyDeviceToHost));
-        HIP_TRY(h, hipFree(d_dbg));
-        const char *path = std::getenv("WRNN_DEBUG_FILE");
-        if (FILE *f = std::fopen(path ? path : "wrnn_stamps.bin", "wb")) {
-            int hdr[3] = {kXcds * kXcdWgs * kMWaves, dbg_steps, kMStamps};
-            std::fwrite(hdr, sizeof(hdr), 1, f);
-            std::fwrite(host.data(), 4, host.size(), f);
-            std::fclose(f);
-        }
-    }
+    if (dbg.p) return dump_wave_stamps(h, dbg, dbg_n, kXcds * kXcdWgs * kMWaves, dbg_steps, kMStamps, st);
     return WRNN_OK;
 }
 
@@ -1823,10 +1859,10 @@ int generate_latency(wrnn_t *h, const float *cond, int B, int L, const float *no
     // diagnostics: WRNN_DEBUG_STAMPS=<steps> WRNN_DEBUG_FILE=<path> dumps per-stage stamps
     const char *dbg_env = std::getenv("WRNN_DEBUG_STAMPS");
     const int dbg_steps = dbg_env ? std::min(L, std::atoi(dbg_env)) : 0;
-    unsigned *d_dbg = nullptr;
+    DbgBuf dbg;
     if (dbg_steps > 0) {
-        HIP_TRY(h, hipMalloc(&d_dbg, (size_t)h->G * dbg_steps * kStamps * 4));
-        HIP_TRY(h, hipMemsetAsync(d_dbg, 0, (size_t)h->G * dbg_steps * kStamps * 4, st));
+        HIP_TRY(h, hipMalloc(&dbg.p, (size_t)h->G * dbg_steps * kStamps * 4));
+        HIP_TRY(h, hipMemsetAsync(dbg.p, 0, (size_t)h->G * dbg_steps * kStamps * 4, st));
     }
     for (int b0 = 0; b0 < B; b0 += h->max_rows) {
         const int Bc = std::min(h->max_rows, B - b0);
@@ -1869,11 +1905,11 @@ int generate_latency(wrnn_t *h, const float *cond, int B, int L, const float *no
         a.G = h->G;
         a.NMAX = h->NMAX;
         a.s = h->s;
-        a.dbg = (b0 == 0) ? d_dbg : nullptr;
+        a.dbg = (b0 == 0) ? dbg.p : nullptr;
         a.dbg_steps = dbg_steps;
         HIP_TRY(h, launch_loop(a, lds_bytes_for(*h, Bc), st));
     }
-    if (d_dbg) return dump_stamps(h, d_dbg, dbg_steps, st, h->G);
+    if (dbg.p) return dump_stamps(h, dbg.release(), dbg_steps, st, h->G);
     return WRNN_OK;
 }
 
@@ -2189,11 +2225,8 @@ int wrnn_set_weights(wrnn_t *h, const wrnn_tensor *tensors, int n) {
         }
     }
     if (h->xcdm_ok) {
-        std::vector<float> slab, Wt, Wm;
-        pack_xcd_terms_weights(*h, Wt);
-        Wm.reserve((size_t)kXcdWgs * kMRing * h->KXc);
-        for (int c = 0; c < kXcdWgs; ++c)   // rows c·kXTerms + j, j < kMRing → c·kMRing + j
-            Wm.insert(Wm.end(), Wt.begin() + (size_t)c * kXTerms * h->KXc, Wt.begin() + ((size_t)c * kXTerms + kMRing) * h->KXc);
+        std::vector<float> slab, Wm;
+        pack_xcdm_terms_weights(*h, Wm);
         if (h->d_xmWt) HIP_TRY(h, hipFree(h->d_xmWt));
         h->d_xmWt = nullptr;
         HIP_TRY(h, hipMalloc(&h->d_xmWt, Wm.size() * 4));

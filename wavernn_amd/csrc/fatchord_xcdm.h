@@ -1,8 +1,8 @@
 // Shared between the host launcher (capi.cpp) and fatchord_xcdm.hip: the XCD-resident MoL kernel
 // for MANY rows — up to 16 rows (utterances or folds) on each XCD, all of them stepping together
 // through one copy of the weights held in the XCD's 32 CUs, the matvecs on the matrix cores
-// (v_mfma_f32_4x4x1_16b_f32: 16 blocks of 4 weight rows × 4 rows of the batch), every hand-off
-// kept in the XCD's L2.
+// (v_mfma_f32_4x4x1_16b_f32 at ≤ 2 quads of 4 batch rows, v_mfma_f32_16x16x4_f32 at 3–4 quads),
+// every hand-off kept in the XCD's L2.
 //
 // Shapes: rnn 512, fc 512, aux 32, MoL (30 classes) — BASELINE configs 2 (fold-batched) and 3 —
 // or RAW 9-bit (512 classes, fatchord_version.py:231-237): fc3 is then a twelfth 16-row set (the
@@ -40,7 +40,8 @@ enum MSet { MS_IH2 = 0, MS_FC1 = 3, MS_FC2 = 4, MS_HH2 = 5, MS_HH1 = 8, kMSets =
 // (n·512 + class).
 // Packed vectors (untagged fp32, two slots by step parity, kMPackOff granules in): H1 / Y / H2 /
 // F1 (RAW: and the f2 vector, MH_F2) at slot·kMVec + n·512 + j (unit or fc row j).  An empty
-// element holds kMEmpty (a NaN bit pattern no fp32 operation produces); the producer of an
+// element holds kMEmpty (0xFFFFFFFF, a NaN pattern: ppub maps a published NaN of exactly these
+// bits to the canonical 0x7FC00000, so no published value reads as empty); the producer of an
 // element empties the other slot once its B poll of step t has seen every workgroup's h1_t —
 // by then every consumer has read all of step t - 1 — and a later publish of its own orders the
 // clear before step t + 1's polls.  Twice the values per 16-byte poll of the tagged form.
@@ -77,6 +78,20 @@ struct XcdmSlab {
 // cI [96,112), V1 [112,128), V2 [128,144) — the first kMRing floats of the 160-float record; this
 // kernel's GEMM produces only those (compact weights d_xmWt: 32 × 144 rows, 10 % fewer FLOPs)
 constexpr int kMRing = 144;
+// The record of one row-step is SEGMENTED by term type across the 32 workgroups — [P1 | cI | P2 |
+// V1 | V2] — so that each type's part of the terms GEMM reads only the input columns it depends
+// on (capi.cpp, generate_xcdm: 53 % of the FLOPs of one full-depth GEMM); compact slot s of
+// workgroup c lives at mterm_off(c, s) (4-float groups never straddle a segment).
+constexpr int kMSegP1 = 0, kMSegCI = kMSegP1 + 32 * 48, kMSegP2 = kMSegCI + 32 * 16, kMSegV1 = kMSegP2 + 32 * 48,
+              kMSegV2 = kMSegV1 + 32 * 16, kMSegEnd = kMSegV2 + 32 * 16;
+static_assert(kMSegEnd == kXcdWgs * kMRing, "segmented terms record");
+__host__ __device__ inline int mterm_off(int c, int s) {
+    return s < XT_P2   ? kMSegP1 + c * 48 + s
+           : s < XT_CI ? kMSegP2 + c * 48 + (s - XT_P2)
+           : s < XT_V1 ? kMSegCI + c * 16 + (s - XT_CI)
+           : s < XT_V2 ? kMSegV1 + c * 16 + (s - XT_V1)
+                       : kMSegV2 + c * 16 + (s - XT_V2);
+}
 constexpr int kMNoise = 12;                // 11 MoL sampler terms per row and step, padded
 
 // Per-workgroup state carried between time chunks: h1 / h2 of the own units [16][16 rows],

@@ -3,17 +3,18 @@
 // folds of fold_with_overlap (:293-340; BASELINE config 2 batched: 10 folds, config 3: 115 folds)
 // or independent utterances.
 //
-// The weights of the loop are held once per XCD, spread over its 32 CUs as MFMA A operands in
-// VGPRs (176 per lane and wave): workgroup c owns GRU units 16c..16c+15 (both GRUs) and fc rows
-// 16c..16c+15; wave w multiplies the K window [64w, 64w + 64) of every one of the eleven 16-row
-// weight sets (fatchord_xcdm.h, MSet) with v_mfma_f32_4x4x1_16b_f32 — 16 blocks of (4 weight rows
-// × 1 k) · (1 k × 4 batch rows) per instruction, so a batch quad of 4 rows costs what one row
-// would: block b = 4s' + g takes row group g and k-slice s' of the window, 16 MFMAs walk the
-// slice's 16 columns.  The activations (B operands) of the window come from the hop vectors: each
-// wave polls only its own 64-wide slice of every vector (granules of 4 producer workgroups),
-// stages it in LDS and reads it back as B.  K-split partial sums are reduced in the wave (the four
-// k-slices: permlane16/32 swaps) and across the 8 waves (LDS, fixed order) by the threads that
-// finish each layer, one (unit or fc row, batch row) each.
+// The weights of the loop are held once per XCD, spread over its 32 CUs as MFMA A operands:
+// workgroup c (4 waves, one per SIMD) owns GRU units 16c..16c+15 (both GRUs) and fc rows
+// 16c..16c+15; wave w multiplies the K window [128w, 128w + 128) of every one of the eleven 16-row
+// weight sets (fatchord_xcdm.h, MSet): 11 × 32 floats per lane, eight sets in the 256 AGPRs (the
+// MFMAs are inline asm with "a" operands, hazards handled by hand) and W_hh1 in VGPRs.  ≤ 2 quads
+// of 4 batch rows: v_mfma_f32_4x4x1_16b_f32 — 16 blocks of (4 weight rows × 1 k) · (1 k × 4 batch
+// rows) per instruction, block b = 4s' + g takes row group g and k-slice s' of the window; 3–4
+// quads: v_mfma_f32_16x16x4_f32 (16 batch rows on N, K reduced inside).  The activations (B
+// operands) of the window come from the packed hop vectors: each wave polls only its own
+// 128-wide slice of every vector, stages it in LDS (XOR-swizzled) and reads it back as B.  The
+// partial sums of the four k-slices and four waves are left unreduced in LDS; the threads that
+// finish each layer (one unit or fc row and batch row each) sum them in a fixed order.
 //
 // Per step t (x = x_{t-1} of every row):
 //   A  GRU1 of the own units (gate math; W_hh1·h1_{t-1} from the previous step)  → publish h1  [hop H1]
@@ -67,8 +68,12 @@ __device__ __forceinline__ float *pvec(unsigned long long *xg, int hop, int t) {
     const int slot = __builtin_amdgcn_readfirstlane(2 * (hop - MH_H1) + (t & 1));
     return reinterpret_cast<float *>(xg + kMPackOff) + (size_t)slot * kMVec;
 }
+// (a NaN whose bits equal kMEmpty — a NaN input can carry that payload through the layers — is
+// published as the canonical quiet NaN, so a real value never reads as "empty")
 __device__ __forceinline__ void ppub(float *p, float v) {
-    __hip_atomic_store(reinterpret_cast<unsigned *>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const unsigned u = __float_as_uint(v);
+    __hip_atomic_store(reinterpret_cast<unsigned *>(p), u == kMEmpty ? 0x7FC00000u : u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ void pclear(float *p) {
     __hip_atomic_store(reinterpret_cast<unsigned *>(p), kMEmpty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -537,9 +542,8 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
     const int t_end = a.t0 + a.Lc;
     unsigned long long *xg = a.xg + (size_t)k * kMXcdStride;
     const float *S = a.slab + (size_t)c * a.s.total;
-    auto TERMS = [&](int t, int n) {
-        return a.terms + ((size_t)(t - a.t0) * a.nb + (k + kXcds * n)) * N + (size_t)c * kMRing;
-    };
+    // the segmented record of (step t, row n): float4 f of this workgroup's terms at + mterm_off(c, 4f)
+    auto TERMS = [&](int t, int n) { return a.terms + ((size_t)(t - a.t0) * a.nb + (k + kXcds * n)) * N; };
 
     // ---- register-resident MFMA A operands: the wave's K window of all eleven sets
     float A[kMSets][kMJ];
@@ -603,7 +607,8 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
     }
     for (int i = tid; i < RX * kRingF4; i += kMThreads) {
         const int n = i / kRingF4, f = i - n * kRingF4;
-        *reinterpret_cast<f4v *>(ring_at(a.t0) + n * kMRing + 4 * f) = *reinterpret_cast<const f4v *>(TERMS(a.t0, n) + 4 * f);
+        *reinterpret_cast<f4v *>(ring_at(a.t0) + n * kMRing + 4 * f) =
+            *reinterpret_cast<const f4v *>(TERMS(a.t0, n) + mterm_off(c, 4 * f));
     }
     if constexpr (!kRaw)
         for (int i = tid; i < 11 * RX; i += kMThreads) {
@@ -738,7 +743,7 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
                 const int idx = lt + kLdThreads * i;
                 if (idx < RX * kRingF4) {
                     const int n = idx / kRingF4, f = idx - n * kRingF4;
-                    rl[i] = *reinterpret_cast<const f4v *>(TERMS(t + 1, n) + 4 * f);
+                    rl[i] = *reinterpret_cast<const f4v *>(TERMS(t + 1, n) + mterm_off(c, 4 * f));
                 }
             }
             if (!kRaw && lt < 11 * RX) {

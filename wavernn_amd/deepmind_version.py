@@ -1,6 +1,7 @@
 """Drop-in for the reference `models.deepmind_version.WaveRNN` (dual coarse/fine 8-bit softmax,
-BASELINE config 5) whose `generate()` runs on the MI355X persistent kernel
-(wavernn_amd/csrc/deepmind_rows.hip) instead of the per-step eager loop (:98-156).
+BASELINE config 5) whose `generate()` runs on the MI355X persistent kernels instead of the
+per-step eager loop (:98-156): wavernn_amd/csrc/deepmind_xcd.hip for hidden 896 / quantisation
+256 (4 rows per XCD, 32 per launch), deepmind_rows.hip for other sizes.
 
 Same constructor (hidden_size, quantisation), parameter names (so `load_state_dict` takes the
 reference's state_dicts), training `forward` (:37-72) and `generate(seq_len)` return contract
@@ -85,16 +86,18 @@ class WaveRNN(nn.Module):
         return self._loop
 
     @torch.no_grad()
-    def generate(self, seq_len, *, batch: int = 1, noise=None, seed: Optional[int] = None):
+    def generate(self, seq_len, *, batch: int = 1, noise=None, seed: Optional[int] = None, row_offset: int = 0):
         """deepmind_version.py:75-165.  Returns (output, coarse, fine) as numpy int64 arrays of
-        shape (seq_len,) for batch = 1 (the reference contract), (batch, seq_len) otherwise."""
+        shape (seq_len,) for batch = 1 (the reference contract), (batch, seq_len) otherwise.
+        Row b's Philox draws are keyed (seed, row_offset + b): a row generated alone with its
+        row_offset equals the same row of a batch (the sharded entry point relies on it)."""
         loop = self.loop_handle()
         device = next(self.parameters()).device
         if noise is not None:
             noise = torch.as_tensor(np.asarray(noise, dtype=np.float32)).to(device).contiguous()
         if seed is None:
             seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-        _, comb = loop.generate(batch, seq_len, noise=noise, seed=seed, device=device)
+        _, comb = loop.generate(batch, seq_len, noise=noise, seed=seed, row_offset=row_offset, device=device)
         output = comb.cpu().numpy().astype(np.int64)
         unsigned = output + 2 ** 15                      # split_signal, utils/dsp.py:25-29
         coarse, fine = unsigned // 256, unsigned % 256

@@ -18,7 +18,7 @@ from __future__ import annotations
 
 import time
 from pathlib import Path
-from typing import Optional, Union
+from typing import List, Optional, Sequence, Union
 
 import numpy as np
 import torch
@@ -210,12 +210,14 @@ class WaveRNN(nn.Module):
         return cond, wave_len
 
     def generate(self, mels, save_path: Union[str, Path, None], batched, target, overlap, mu_law, *,
-                 noise=None, seed: Optional[int] = None, verbose: bool = True):
+                 noise=None, seed: Optional[int] = None, row_offset: int = 0, verbose: bool = True):
         """fatchord_version.py:169-264 with the loop on the GPU.
 
         Keyword-only extensions: `noise` [L][B][K] injects the sampler draws in reference order
         (parity testing); otherwise draws come from in-kernel Philox keyed by `seed` (default:
-        drawn from torch's global RNG, so torch.manual_seed governs reproducibility)."""
+        drawn from torch's global RNG, so torch.manual_seed governs reproducibility) and by the
+        global row id `row_offset + b` of each loop row b (a fold when batched) — the key that
+        makes `generate_many` and the sharded entry points reproduce single calls."""
         self.eval()
         mu_law = mu_law if self.mode == 'RAW' else False
         start = time.time()
@@ -228,7 +230,7 @@ class WaveRNN(nn.Module):
                 nz = torch.as_tensor(noise, dtype=torch.float32).to(cond.device).contiguous()
             if seed is None:
                 seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-            out, _ = loop.generate(cond, noise=nz, seed=seed)
+            out, _ = loop.generate(cond, noise=nz, seed=seed, row_offset=row_offset)
             # mu-law, xfade_and_unfold / row 0, trim, fade-out (:243-258) in float64 on the device
             output = condition.postprocess(out, batched, overlap, mu_law, self.n_classes, wave_len,
                                            20 * self.hop_length).cpu().numpy()
@@ -238,6 +240,76 @@ class WaveRNN(nn.Module):
         dsp.save_wav(output, save_path, self.sample_rate)
         self.train()
         return output
+
+    def rows_of(self, n_frames: int, batched: bool, target: int, overlap: int) -> int:
+        """Loop rows generate() runs for a mel of n_frames frames: 1, or its fold count."""
+        if not batched:
+            return 1
+        return self.fold_count(n_frames * self.hop_length, target, overlap)[0]
+
+    @torch.no_grad()
+    def conditioning_many(self, mels: Sequence, batched: bool, target: int, overlap: int):
+        """Conditioning of several utterances as the rows of ONE loop launch.
+
+        Returns (cond [L][rows][C], per-utterance (first row, rows, steps, wave_len)).  Unbatched:
+        row i is utterance i, its records padded with zeros after its own L_i steps (a row's
+        samples depend only on earlier steps, so trimming to L_i is exact).  Batched: the folds
+        of utterance i are rows [r_i, r_i + nf_i), all folds sharing the window target + 2·overlap.
+        Mels of one length go through MelResNet and the upsample kernel together."""
+        device = next(self.parameters()).device
+        ms = [torch.as_tensor(m, device=device).to(torch.float32) for m in mels]
+        ms = [m if m.dim() == 3 else m[None] for m in ms]
+        if not ms or any(m.dim() != 3 or m.shape[0] != 1 or m.shape[1] != self.feat_dims for m in ms):
+            raise ValueError(f"mels must be a non-empty sequence of (1, {self.feat_dims}, T) arrays")
+        if len({m.shape[2] for m in ms}) == 1:
+            cond, wave_len = self.conditioning(torch.cat(ms, 0), batched, target, overlap)
+            per = cond.shape[1] // len(ms)
+            return cond, [(i * per, per, cond.shape[0], wave_len) for i in range(len(ms))]
+        parts = [self.conditioning(m, batched, target, overlap) for m in ms]
+        L = max(c.shape[0] for c, _ in parts)
+        rows = sum(c.shape[1] for c, _ in parts)
+        cond = torch.zeros(L, rows, parts[0][0].shape[2], dtype=torch.float32, device=device)
+        spans, r = [], 0
+        for c, wave_len in parts:
+            cond[:c.shape[0], r:r + c.shape[1]] = c
+            spans.append((r, c.shape[1], c.shape[0], wave_len))
+            r += c.shape[1]
+        return cond, spans
+
+    def generate_many(self, mels: Sequence, save_paths: Optional[Sequence] = None, batched: bool = False,
+                      target: int = 11000, overlap: int = 550, mu_law: bool = True, *, noise=None,
+                      seed: Optional[int] = None, row_offset: int = 0, verbose: bool = False) -> List[np.ndarray]:
+        """generate() for several utterances in ONE persistent-kernel launch (the utterances —
+        or, batched, all their folds — are the launch's rows).  The reference vocodes a list one
+        generate() at a time (gen_wavernn.py:11-35, gen_tacotron.py:142-168); this returns the
+        same list of float64 waveforms.  Utterance i's rows are keyed row_offset + (rows of the
+        utterances before it) + j, so under Philox `generate_many(mels, seed=s)[i]` equals
+        `generate(mels[i], seed=s, row_offset=<that first row>)` bit for bit.  `noise`, when given,
+        is [L_max][rows][K] in that row order."""
+        self.eval()
+        mu_law = mu_law if self.mode == 'RAW' else False
+        start = time.time()
+        with torch.no_grad():
+            cond, spans = self.conditioning_many(mels, batched, target, overlap)
+            loop = self.loop_handle()
+            nz = None
+            if noise is not None:
+                nz = torch.as_tensor(noise, dtype=torch.float32).to(cond.device).contiguous()
+            if seed is None:
+                seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+            out, _ = loop.generate(cond, noise=nz, seed=seed, row_offset=row_offset)
+            waves = [condition.postprocess(out[r0:r0 + n, :steps], batched, overlap, mu_law, self.n_classes,
+                                           wave_len, 20 * self.hop_length)
+                     for r0, n, steps, wave_len in spans]
+            outputs = [w.cpu().numpy() for w in waves]
+        self.last_gen_seconds = time.time() - start
+        if verbose:
+            self.gen_display(cond.shape[0] - 1, cond.shape[0], cond.shape[1], start)
+        for i, output in enumerate(outputs):
+            if save_paths is not None and save_paths[i] is not None:
+                dsp.save_wav(output, save_paths[i], self.sample_rate)
+        self.train()
+        return outputs
 
     def gen_display(self, i, seq_len, b_size, start):
         gen_rate = (i + 1) / max(time.time() - start, 1e-9) * b_size / 1000

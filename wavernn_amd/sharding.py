@@ -1,11 +1,13 @@
 """Utterance sharding across GPUs (one process per GPU, torch.distributed).
 
 The reference generates one utterance at a time on one device (gen_wavernn.py:11-35 loops
-over the test set).  Utterances are independent, so the MI355X path shards them: utterance i
-runs on rank i % world, with its sampler draws keyed by the global utterance index (Philox
-seed = base_seed + i), so the audio does not depend on how many GPUs ran the job.  The only
-collective is the final gather of finished audio to rank 0 (RCCL over xGMI under the "nccl"
-backend; gloo on CPU for tests) — there is no exchange inside the sample loop.
+over the test set).  Utterances are independent, so the MI355X path shards them: rank r takes a
+contiguous block of the list (block sizes differ by at most one) and vocodes the whole block as
+the rows of ONE persistent-kernel launch (`WaveRNN.generate_many`; deepmind: `generate(batch=)`).
+Each loop row's sampler draws are keyed by its GLOBAL row id (Philox (seed, row)), so the audio
+does not depend on how many GPUs ran the job.  The only collective is the final gather of
+finished audio to rank 0 (RCCL over xGMI under the "nccl" backend; gloo on CPU for tests) —
+there is no exchange inside the sample loop.
 """
 from __future__ import annotations
 
@@ -17,8 +19,8 @@ import torch.distributed as dist
 
 
 def shard_indices(n_items: int, rank: int, world: int) -> List[int]:
-    """Round-robin assignment: item i → rank i % world."""
-    return list(range(rank, n_items, world))
+    """Contiguous block of rank `rank`: items [rank·n // world, (rank + 1)·n // world)."""
+    return list(range(rank * n_items // world, (rank + 1) * n_items // world))
 
 
 def gather_audio(local: Dict[int, np.ndarray], n_items: int, device: torch.device,
@@ -65,12 +67,43 @@ def generate_sharded(model, mels: Sequence, batched: bool, target: int, overlap:
                      base_seed: int = 0, device: Optional[torch.device] = None, group=None,
                      generate_fn: Optional[Callable] = None) -> Optional[List[np.ndarray]]:
     """Generate every mel in `mels` across the process group; rank 0 returns the list of
-    float64 waveforms in input order, other ranks return None."""
+    float64 waveforms in input order, other ranks return None.
+
+    A rank runs its block through ONE `generate_many` launch, seeded `base_seed` with its first
+    loop row at the global row id of its first utterance (every rank knows every mel's row
+    count from its length), so the result equals `model.generate_many(mels, seed=base_seed)` on
+    one GPU.  `generate_fn(indices, mels, row_offset)` replaces the generation (host tests)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     if device is None:
         device = next(model.parameters()).device
-    gen = generate_fn or (lambda i, m: model.generate(m, None, batched, target, overlap, mu_law,
-                                                      seed=base_seed + i, verbose=False))
-    local = {i: gen(i, mels[i]) for i in shard_indices(len(mels), rank, world)}
-    return gather_audio(local, len(mels), device, group)
+    idx = shard_indices(len(mels), rank, world)
+    rows = [model.rows_of(np.shape(m)[-1], batched, target, overlap) for m in mels]
+    row0 = int(sum(rows[:idx[0]])) if idx else 0
+    gen = generate_fn or (lambda ii, ms, r0: model.generate_many(ms, None, batched, target, overlap, mu_law,
+                                                                  seed=base_seed, row_offset=r0))
+    outs = gen(idx, [mels[i] for i in idx], row0) if idx else []
+    return gather_audio(dict(zip(idx, outs)), len(mels), device, group)
+
+
+def generate_sharded_deepmind(model, n_utterances: int, seq_len: int, base_seed: int = 0,
+                              device: Optional[torch.device] = None, group=None,
+                              generate_fn: Optional[Callable] = None) -> Optional[List[np.ndarray]]:
+    """deepmind_version.generate(seq_len) for n_utterances independent utterances across the
+    process group (BASELINE config 5: 256 over 8 GPUs): rank r runs its contiguous block as the
+    rows of one `generate(batch=...)` launch keyed by the global utterance index, rank 0 returns
+    the int64 outputs (coarse·256 + fine − 2^15) in utterance order.  Outputs travel as float64
+    (exact: |v| ≤ 2^15)."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if device is None:
+        device = next(model.parameters()).device
+    idx = shard_indices(n_utterances, rank, world)
+
+    def _gen(ii, r0):
+        out, _, _ = model.generate(seq_len, batch=len(ii), seed=base_seed, row_offset=r0)
+        return list(np.asarray(out).reshape(len(ii), seq_len))
+
+    outs = (generate_fn or _gen)(idx, idx[0]) if idx else []
+    got = gather_audio({i: np.asarray(o, dtype=np.float64) for i, o in zip(idx, outs)}, n_utterances, device, group)
+    return None if got is None else [g.astype(np.int64) for g in got]
