@@ -35,7 +35,7 @@ CASES = {
     "long_mol_fold115": dict(dims=syn.DEFAULT_MOL, B=115, L=12100, wseed=0, cseed=31, nseed=32, prune=0.0,
                              full_rows=(0, 7, 64, 114), sub=50),
     "long_sparse896_5s": dict(dims=syn.SPARSE896_MOL, B=1, L=110275, wseed=0, cseed=41, nseed=42, prune=0.95,
-                              full_rows=(0,), sub=1),
+                              full_rows=(0,), sub=50),
 }
 
 
