@@ -2,7 +2,11 @@
 
 * `WaveRNN.generate_many(mels)` runs several utterances (or all their folds) as the rows of ONE
   loop launch; under Philox each utterance equals its own `generate(mel, row_offset=<first row>)`
-  bit for bit when both run the same kernel (row-keyed draws, identical per-row arithmetic).
+  (row-keyed draws, the same kernel) within the MoL tolerance used between launches of different
+  shapes (2·MOL_TOL): the library GEMMs around the loop (MelResNet on MIOpen for equal-length
+  mels batched together, the rocBLAS terms GEMM over all rows) pick their tiling by shape, so the
+  conditioning terms may differ in the last bit; the deepmind rows (no conditioning) and RAW
+  labels are compared exactly.
 * Config 4's shape: 8 utterances of the rnn-896 block-sparse model in one launch of the sparse
   XCD kernel vs 8 separate calls.  Config 5's: 32 deepmind rows vs 32 single-row calls.
 * A loop handle that ran the many-row kernel must still run the one-row kernel afterwards
@@ -12,6 +16,8 @@ models/fatchord_version.py:169-264, models/deepmind_version.py:75-165."""
 import numpy as np
 import pytest
 import torch
+
+from tests.golden import fixtures as gf
 
 from wavernn_amd import synthetic as syn
 from wavernn_amd.pruning import prune_state
@@ -30,6 +36,13 @@ def _model(d, seed, prune=0.0):
     return m
 
 
+def _close(a, b, what):
+    assert a.dtype == np.float64 and a.shape == b.shape, what
+    err = np.abs(a - b).max()
+    print(f"{what}: max |Δ| {err:.3g}")
+    assert err <= 2 * gf.MOL_TOL, (what, err)
+
+
 def _mels(d, frames, seed0):
     return [torch.from_numpy(syn.make_mel(d.feat_dims, T, seed0 + i))[None] for i, T in enumerate(frames)]
 
@@ -45,8 +58,7 @@ def test_generate_many_unbatched_equals_single_calls(frames):
     for i, mel in enumerate(mels):
         ref = m.generate(mel, None, False, 11000, 550, True, seed=123, row_offset=i, verbose=False)
         assert m.loop_handle().info["last_path"] == path_many
-        assert got[i].dtype == np.float64 and got[i].shape == ref.shape
-        assert np.array_equal(got[i], ref), i
+        _close(got[i], ref, f"utterance {i}")
 
 
 def test_generate_many_batched_folds_keyed_by_global_row():
@@ -60,7 +72,7 @@ def test_generate_many_batched_folds_keyed_by_global_row():
     r0 = 10
     for i, mel in enumerate(mels):
         ref = m.generate(mel, None, True, target, overlap, True, seed=5, row_offset=r0, verbose=False)
-        assert np.array_equal(got[i], ref), i
+        _close(got[i], ref, f"utterance {i}")
         r0 += rows[i]
 
 
@@ -74,7 +86,7 @@ def test_generate_many_sparse896_eight_utterances():
     assert h.info["last_path"] == 6 and h.info["sparse_blocks"] > 0, h.info
     for i, mel in enumerate(mels):
         ref = m.generate(mel, None, False, 11000, 550, True, seed=31, row_offset=i, verbose=False)
-        assert np.array_equal(got[i], ref), i
+        _close(got[i], ref, f"sparse utterance {i}")
 
 
 def test_deepmind_batch32_equals_single_rows():
@@ -115,3 +127,15 @@ def test_one_row_kernel_after_many_row_kernel_on_one_handle():
     assert torch.equal(y1, y2)
     loop.close()
     other.close()
+
+
+def test_generate_many_raw_labels_exact():
+    """RAW (bits) rows of one launch vs single calls: the mu-law-decoded waveforms, i.e. the
+    integer labels, identical (config 1's model; the many-row kernel's softmax head)."""
+    d = syn.DEFAULT_RAW
+    m = _model(d, 6)
+    mels = _mels(d, (25, 28), 120)
+    got = m.generate_many(mels, None, False, 11000, 550, True, seed=8)
+    for i, mel in enumerate(mels):
+        ref = m.generate(mel, None, False, 11000, 550, True, seed=8, row_offset=i, verbose=False)
+        assert np.array_equal(got[i], ref), i

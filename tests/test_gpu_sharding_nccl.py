@@ -1,7 +1,8 @@
 """generate_sharded under the "nccl" backend (RCCL) on the GPU box: world_size 1, one process,
 127.0.0.1 rendezvous.  The gathered float64 audio (one generate_many launch per rank) equals
-each utterance's own generate() bit-for-bit under the same Philox keying by global row id; the
-deepmind variant likewise."""
+each utterance's own generate() under the same Philox keying by global row id, within the MoL
+tolerance between launches of different shapes (tests/test_gpu_many.py); the deepmind variant's
+integer outputs bit for bit."""
 import os
 import socket
 
@@ -36,7 +37,8 @@ def test_generate_sharded_nccl_world1():
         assert dist.get_backend() == "nccl" and len(got) == 3
         for i, mel in enumerate(mels):
             ref = m.generate(mel, None, False, 11000, 550, True, seed=77, row_offset=i, verbose=False)
-            assert got[i].dtype == np.float64 and np.array_equal(got[i], ref)
+            assert got[i].dtype == np.float64 and got[i].shape == ref.shape
+            assert np.abs(got[i] - ref).max() <= 2e-5, i
         from wavernn_amd.deepmind_version import WaveRNN as DM
         dd = syn.DEFAULT_DM
         dm = DM(**dd.ctor_kwargs()).to(dev)

@@ -1,6 +1,6 @@
 """§8(f)4: the training-side teacher-forced forward (models/fatchord_version.py:131-167;
 deepmind_version.py:36-72) runs on the MI355X with the GRUs on MIOpen (torch.nn.GRU on ROCm) —
-forward (1e-4) and backward (2e-3 of each parameter's largest gradient) against the same module
+forward (1e-4) and backward (1e-3 of each parameter's largest gradient) against the same module
 on the CPU (ATen): fp32 tolerances for the different kernels' summation orders."""
 import numpy as np
 import pytest
@@ -48,14 +48,14 @@ def test_fatchord_training_forward_backward_on_miopen(mode):
     for (n, pc), (_, pg) in zip(cpu.named_parameters(), gpu.named_parameters()):
         if pc.grad is None:
             continue
-        # reductions over B·T = 2 200 rows in other orders and MIOpen's GRU backward: observed
-        # 4.7e-4 of a parameter's largest gradient (fc2.weight, RAW, profiles/r03_v4_pytest_gpu.log);
-        # a wrong backward is off by O(1)
         err = (pg.grad.cpu() - pc.grad).abs().max().item()
         rel[n] = err / (pc.grad.abs().max().item() + 1e-12)
-        assert err <= 2e-3 * pc.grad.abs().max().item() + 1e-7, (n, err)
-    worst = max(rel, key=rel.get)
-    print(f"\n{mode}: largest relative gradient error {rel[worst]:.2e} ({worst})")
+    worst = sorted(rel, key=rel.get)[-3:]
+    print(f"\n{mode}: largest relative gradient errors " + ", ".join(f"{n} {rel[n]:.2e}" for n in worst))
+    # reductions over B·T = 2 200 rows in other orders and MIOpen's GRU backward through 1 100
+    # steps: observed 4.7e-4 (RAW fc2.weight, profiles/r03_v4_pytest_gpu.log), 2.3e-4 / 6.8e-5 (MoL /
+    # RAW, profiles/r04_pytest_gpu_v2.log) of a parameter's largest gradient; a wrong backward is off by O(1)
+    assert rel[worst[-1]] <= 1e-3, worst
 
 
 def test_deepmind_training_forward_on_gpu():

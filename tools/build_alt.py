@@ -1,6 +1,6 @@
 """Build an alternative library for A/B timing (tools/ab_libs.sh): the in-tree objects, with
-ONE source recompiled under extra flags, linked to tools/_alt/<name>.so.
-    python tools/build_alt.py <name> <source.hip> [-DFLAG=V ...]"""
+named sources (comma-separated) recompiled under extra flags, linked to tools/_alt/<name>.so.
+    python tools/build_alt.py <name> <source.hip>[,<source2>] [-DFLAG=V ...]"""
 import os
 import subprocess
 import sys
@@ -18,7 +18,7 @@ def main(name, src, *flags):
     for s in hb.SOURCES:
         base = os.path.basename(s)
         obj = os.path.join(objdir, base + ".o")
-        if base == src:
+        if base in src.split(","):
             obj = os.path.join(alt, f"{name}_{base}.o")
             cmd = [hb.hipcc(), f"--offload-arch={hb.ARCH}", "-O3", "-std=c++17", "-fPIC",
                    "-I" + os.path.join(hb.REPO, "include"), *hb.EXTRA_FLAGS.get(base, []), *flags, "-c", s, "-o", obj]

@@ -8,9 +8,12 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from oracle import oracle  # noqa: E402
+from wavernn_amd import _native  # noqa: E402
 from wavernn_amd import synthetic as syn  # noqa: E402
 from wavernn_amd.loop import FatchordLoop  # noqa: E402
 
+if os.environ.get("TIME_DM_LIB"):   # a build under A/B (diagnostics only)
+    _native.LIB_PATH = os.environ["TIME_DM_LIB"]
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 115
 L = int(sys.argv[2]) if len(sys.argv) > 2 else 200
 seed = int(sys.argv[3]) if len(sys.argv) > 3 else 815

@@ -995,11 +995,11 @@ void pack_xcd_terms_weights(const wrnn_ctx &h, std::vector<float> &Wt) {
     }
 }
 
-// Many-row kernel: its compact terms record (kMRing slots per workgroup) SEGMENTED by type
-// (fatchord_xcdm.h, mterm_off) with the columns in the split input order X'' = [mel | a1 | 1 | a2 |
-// a3 | a4 | 1 | 0 0] (pack_cond_input_kernel, split = M + A): P1 and cI depend on mel‖a1 and their
-// bias only, P2 also on a2, V1 / V2 on a3 / a4 and their biases — generate_xcdm runs one GEMM per
-// segment group over just those columns (xcdm_terms_gemms).
+// Many-row kernel: its compact terms record (kMRing slots per workgroup, MT_ order) segmented by
+// GEMM group (fatchord_xcdm.h, mterm_off) with the columns in the split input order X'' = [mel |
+// a1 | 1 | a2 | a3 | a4 | 1 | 0 0] (pack_cond_input_kernel, split = M + A): P1 and cI depend on
+// mel‖a1 and their bias only, P2 also on a2, V1 / V2 on a3 / a4 and their biases — generate_xcdm
+// runs one GEMM per group over just those columns (xcdm_terms_gemms).
 void pack_xcdm_terms_weights(const wrnn_ctx &h, std::vector<float> &Wm) {
     std::vector<float> Wt;
     pack_xcd_terms_weights(h, Wt);
@@ -1007,15 +1007,15 @@ void pack_xcdm_terms_weights(const wrnn_ctx &h, std::vector<float> &Wm) {
     Wm.assign((size_t)kXcdWgs * kMRing * KX, 0.0f);
     for (int c = 0; c < kXcdWgs; ++c)
         for (int s = 0; s < kMRing; ++s) {
-            const float *src = Wt.data() + ((size_t)c * kXTerms + s) * KX;
+            const float *src = Wt.data() + ((size_t)c * kXTerms + mterm_xt(s)) * KX;
             float *dst = Wm.data() + (size_t)mterm_off(c, s) * KX;
             for (int j = 0; j < CD; ++j) dst[j < split ? j : j + 1] = src[j];
-            dst[s >= XT_V1 ? CD + 1 : split] = src[CD];          // the bias → its type's ones column
+            dst[s >= MT_V1 ? CD + 1 : split] = src[CD];          // the bias → its group's ones column
         }
 }
 
-// (segment rows, first input column, depth): [P1 | cI] on mel‖a1‖1, P2 on mel‖a1‖1‖a2, [V1 | V2]
-// on a3‖a4‖1 — the depths rounded up to a multiple of 4 over columns whose weights are zero
+// (record rows, first input column, depth) of each group: [P1 | cI] on mel‖a1‖1, P2 on
+// mel‖a1‖1‖a2, [V1 | V2] on a3‖a4‖1 — depths rounded up to a multiple of 4 over zero weights
 struct XcdmGemm {
     int row0, rows, col0, k;
 };
@@ -1023,9 +1023,9 @@ void xcdm_terms_gemms(const wrnn_ctx &h, XcdmGemm (&g)[3]) {
     const int M = h.cfg.feat_dims, A = h.cfg.aux_dims, split = M + A;
     auto up4 = [](int n) { return (n + 3) / 4 * 4; };
     const int v0 = (split + 1 + A) / 4 * 4;                     // first column of a3, rounded down
-    g[0] = {kMSegP1, kMSegP2 - kMSegP1, 0, std::min(up4(split + 1), h.KXc)};
-    g[1] = {kMSegP2, kMSegV1 - kMSegP2, 0, std::min(up4(split + 1 + A), h.KXc)};
-    g[2] = {kMSegV1, kMSegEnd - kMSegV1, v0, std::min(up4(h.CD + 2 - v0), h.KXc - v0)};
+    g[0] = {kMG0, kMG1 - kMG0, 0, std::min(up4(split + 1), h.KXc)};
+    g[1] = {kMG1, kMG2 - kMG1, 0, std::min(up4(split + 1 + A), h.KXc)};
+    g[2] = {kMG2, kMGEnd - kMG2, v0, std::min(up4(h.CD + 2 - v0), h.KXc - v0)};
 }
 
 // ---- XCD-resident block-sparse kernel (fatchord_xcds.h): workgroup c of an XCD owns units
@@ -1792,11 +1792,13 @@ int generate_xcdm(wrnn_t *h, const float *cond, int B, int L, const float *noise
                 return fail(h, WRNN_EINVAL, "xcdm: terms workspace too small");
             HIP_TRY(h, launch_pack_cond_input(cond, h->CD, B, b0, nb, t0, Lc, h->KXc, h->d_X, st,
                                               h->cfg.feat_dims + h->cfg.aux_dims));
-            for (const XcdmGemm &g : gemms)
-                if (rocblas_sgemm(h->blas, rocblas_operation_transpose, rocblas_operation_none, g.rows, Lc * nb, g.k, &one,
+            for (const XcdmGemm &g : gemms) {
+                const rocblas_status rs =
+                    rocblas_sgemm(h->blas, rocblas_operation_transpose, rocblas_operation_none, g.rows, Lc * nb, g.k, &one,
                                   h->d_xmWt + (size_t)g.row0 * h->KXc + g.col0, h->KXc, h->d_X + g.col0, h->KXc, &zero,
-                                  h->d_T + g.row0, N) != rocblas_status_success)
-                    return fail(h, WRNN_EHIP, "rocblas_sgemm (conditioning terms) failed");
+                                  h->d_T + g.row0, N);
+                if (rs != rocblas_status_success) return fail(h, WRNN_EHIP, "rocblas_sgemm (conditioning terms) failed");
+            }
             HIP_TRY(h, hipMemsetAsync(h->d_members, 0, kXcds * sizeof(int), st));
             XcdmArgs a{};
             a.slab = h->d_xmslab;

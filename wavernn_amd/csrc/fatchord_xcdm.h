@@ -74,23 +74,27 @@ struct XcdmSlab {
     int total;
 };
 
-// Terms of one step for one row (the XCD kernels' terms GEMM, XTerm slots): P1 [0,48), P2 [48,96),
-// cI [96,112), V1 [112,128), V2 [128,144) — the first kMRing floats of the 160-float record; this
-// kernel's GEMM produces only those (compact weights d_xmWt: 32 × 144 rows, 10 % fewer FLOPs)
+// Terms of one step for one row: P1 (48), cI (16), P2 (48), V1 (16), V2 (16) — the 144 of the XCD
+// kernels' 160-slot record this kernel uses (compact weights d_xmWt: 32 × 144 rows)
 constexpr int kMRing = 144;
-// The record of one row-step is SEGMENTED by term type across the 32 workgroups — [P1 | cI | P2 |
-// V1 | V2] — so that each type's part of the terms GEMM reads only the input columns it depends
-// on (capi.cpp, generate_xcdm: 53 % of the FLOPs of one full-depth GEMM); compact slot s of
-// workgroup c lives at mterm_off(c, s) (4-float groups never straddle a segment).
-constexpr int kMSegP1 = 0, kMSegCI = kMSegP1 + 32 * 48, kMSegP2 = kMSegCI + 32 * 16, kMSegV1 = kMSegP2 + 32 * 48,
-              kMSegV2 = kMSegV1 + 32 * 16, kMSegEnd = kMSegV2 + 32 * 16;
-static_assert(kMSegEnd == kXcdWgs * kMRing, "segmented terms record");
+// The terms GEMM is split into three groups so that each reads only the input columns it
+// depends on (capi.cpp, generate_xcdm: 53 % of the FLOPs of one full-depth GEMM): [P1 | cI] on
+// mel‖a1‖1, P2 on mel‖a1‖1‖a2, [V1 | V2] on a3‖a4‖1.  The record of one row-step is segmented by
+// group, workgroup-major inside each — [(P1 ‖ cI) of wg 0..31 | P2 of wg 0..31 | (V1 ‖ V2) of
+// wg 0..31] — so each group is one plain GEMM writing a contiguous row range, and a workgroup
+// reads three runs of a row-step's record (256 B, 192 B, 128 B; measured against one 576-B run
+// per workgroup and five runs segmented by type, profiles/r04_ab_terms_gemm.log).  The LDS ring
+// keeps the workgroup's terms in run order (MT_ slots): float4 f of the runs is ring float4 f.
+enum MTerm { MT_P1 = 0, MT_CI = 48, MT_P2 = 64, MT_V1 = 112, MT_V2 = 128 };
+constexpr int kMG0 = 0, kMG1 = 32 * 64, kMG2 = kMG1 + 32 * 48, kMGEnd = kMG2 + 32 * 32;   // group offsets
+static_assert(kMGEnd == kXcdWgs * kMRing, "segmented terms record");
+// record offset of ring slot s (MT_ order) of workgroup c
 __host__ __device__ inline int mterm_off(int c, int s) {
-    return s < XT_P2   ? kMSegP1 + c * 48 + s
-           : s < XT_CI ? kMSegP2 + c * 48 + (s - XT_P2)
-           : s < XT_V1 ? kMSegCI + c * 16 + (s - XT_CI)
-           : s < XT_V2 ? kMSegV1 + c * 16 + (s - XT_V1)
-                       : kMSegV2 + c * 16 + (s - XT_V2);
+    return s < MT_P2 ? kMG0 + c * 64 + s : s < MT_V1 ? kMG1 + c * 48 + (s - MT_P2) : kMG2 + c * 32 + (s - MT_V1);
+}
+// the XT_ slot (XCD kernels' terms-GEMM weight rows, pack_xcd_terms_weights) of ring slot s
+__host__ __device__ inline int mterm_xt(int s) {
+    return s < MT_CI ? XT_P1 + s : s < MT_P2 ? XT_CI + (s - MT_CI) : s < MT_V1 ? XT_P2 + (s - MT_P2) : s;
 }
 constexpr int kMNoise = 12;                // 11 MoL sampler terms per row and step, padded
 

@@ -542,7 +542,7 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
     const int t_end = a.t0 + a.Lc;
     unsigned long long *xg = a.xg + (size_t)k * kMXcdStride;
     const float *S = a.slab + (size_t)c * a.s.total;
-    // the segmented record of (step t, row n): float4 f of this workgroup's terms at + mterm_off(c, 4f)
+    // the terms record of (step t, row n): ring float4 f of this workgroup at + mterm_off(c, 4f)
     auto TERMS = [&](int t, int n) { return a.terms + ((size_t)(t - a.t0) * a.nb + (k + kXcds * n)) * N; };
 
     // ---- register-resident MFMA A operands: the wave's K window of all eleven sets
@@ -638,9 +638,9 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
             float sr, sz, gin, ghn;
             {
                 const int i0 = gu, i1 = 16 + gu, i2 = 32 + gu;
-                sr = (gh1[i0 * NR + gn] + cst[MC_BHH1 + i0]) + (tr[XT_P1 + gu * 3 + 0] + cst[MC_BIH1 + i0]);
-                sz = (gh1[i1 * NR + gn] + cst[MC_BHH1 + i1]) + (tr[XT_P1 + gu * 3 + 1] + cst[MC_BIH1 + i1]);
-                gin = tr[XT_P1 + gu * 3 + 2] + cst[MC_BIH1 + i2];
+                sr = (gh1[i0 * NR + gn] + cst[MC_BHH1 + i0]) + (tr[MT_P1 + gu * 3 + 0] + cst[MC_BIH1 + i0]);
+                sz = (gh1[i1 * NR + gn] + cst[MC_BHH1 + i1]) + (tr[MT_P1 + gu * 3 + 1] + cst[MC_BIH1 + i1]);
+                gin = tr[MT_P1 + gu * 3 + 2] + cst[MC_BIH1 + i2];
                 ghn = gh1[i2 * NR + gn] + cst[MC_BHH1 + i2];
             }
             const float r = sigmoid_(fmaf(x, cst[MC_Q1 + gu], sr));
@@ -674,11 +674,11 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
 #pragma unroll
             for (int q = 0; q < 3; ++q) {
                 const int i = q * 16 + gu;
-                gi[q] = mpart<NQ>(pbig, i, gn) + (fmaf(x, cst[MC_Q2 + i], tr[XT_P2 + gu * 3 + q]) + cst[MC_BIH2 + i]);
+                gi[q] = mpart<NQ>(pbig, i, gn) + (fmaf(x, cst[MC_Q2 + i], tr[MT_P2 + gu * 3 + q]) + cst[MC_BIH2 + i]);
                 gh[q] = gh2[i * NR + gn] + cst[MC_BHH2 + i];
             }
             h2v = gru_gate_math(gi[0], gi[1], gi[2], gh[0], gh[1], gh[2], h2v);
-            const float xi = fmaf(cst[MC_WI0 + gu], x, tr[XT_CI + gu]);
+            const float xi = fmaf(cst[MC_WI0 + gu], x, tr[MT_CI + gu]);
             const float y = (xi + h1v) + h2v;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the slot clears of B first
             ppub(pvec(xg, MH_Y, t) + gn * 512 + 16 * c + gu, y);
@@ -703,7 +703,7 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         MST(9);
         // ---- F: fc1 epilogue → f1; Σ W_hh1·h1 for the next GRU1
         if (gru) {
-            const float f = mpart<NQ>(pfc1, gu, gn) + rg[gn * kMRing + XT_V1 + gu];
+            const float f = mpart<NQ>(pfc1, gu, gn) + rg[gn * kMRing + MT_V1 + gu];
             ppub(pvec(xg, MH_F1, t) + gn * 512 + 16 * c + gu, f > 0.0f ? f : 0.0f);
             if (aux_w0 >= kMWaves) {
 #pragma unroll
@@ -782,7 +782,7 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         };
         // ---- I: fc2 epilogue → f2 (LDS); Σ W_hh2·h2 for the next GRU2
         if (gru) {
-            const float f = mpart<NQ>(pfc2, gu, gn) + rg[gn * kMRing + XT_V2 + gu];
+            const float f = mpart<NQ>(pfc2, gu, gn) + rg[gn * kMRing + MT_V2 + gu];
             if constexpr (kRaw) ppub(pvec(xg, MH_F2, t) + gn * 512 + 16 * c + gu, f > 0.0f ? f : 0.0f);
             else f2s[gn * kMW3Stride + gu] = f > 0.0f ? f : 0.0f;
             if (aux_w0 >= kMWaves) {
