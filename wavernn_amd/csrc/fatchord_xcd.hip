@@ -45,6 +45,12 @@ namespace wrnn {
 #ifndef WRNN_XCD_SKIP_H2
 #define WRNN_XCD_SKIP_H2 0
 #endif
+// diagnostics: 1 = skip ALL the off-critical recurrent work (W_hh1·h1 → the GRU1 terms S and
+// their exchange, the h2 exchange, W_hh2·h2): the critical path alone, timing only — the ceiling
+// of moving that work off this XCD (DESIGN.md §9.1's two-XCD-per-row idea)
+#ifndef WRNN_XCD_SKIP_RECUR
+#define WRNN_XCD_SKIP_RECUR 0
+#endif
 #ifndef WRNN_XCD_PRIO
 #define WRNN_XCD_PRIO 0         // s_setprio of wave 0 (the poller / sampler)
 #endif
@@ -303,7 +309,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
         // (l & 15) < 2 publish row 8h + (l & 1) + 2·(l >> 4)
         const int jq = lane & 1, rho = jq + 2 * (lane >> 4);
         if (wave == 0) {
-            if (more) {
+            if (more && !WRNN_XCD_SKIP_RECUR) {
                 float gh[5];
                 gh1_dots(gh);
                 wait_flag(ygot, tag);
@@ -389,7 +395,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
             const float A = (jq == 0 ? o[0] : o[1]) + v1;
             if ((lane & 15) < 2) xpub(XG(XH_F1) + c * kXFcRows + rg, tag, A > 0.0f ? A : 0.0f);
             XSTAMPW(4, 1);
-            if (more) {   // h2 out; after f1 gathered: a quarter of the next S; W_hh2 LDS rows 28 + 10h + 2p + e
+            if (more && !WRNN_XCD_SKIP_RECUR) {   // h2 out; after f1 gathered: a quarter of the next S; W_hh2 LDS rows 28 + 10h + 2p + e
                 pub_h2();
                 wait_flag(f1got, tag);
                 if (!WRNN_XCD_SKIP_SG) {
@@ -411,7 +417,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
             }
         } else if (wave < kXWaveFc2 + 2) {
             const int hf = wave - kXWaveFc2;
-            if (more) {   // W_hh1 rows; after y gathered their terms and h2 out
+            if (more && !WRNN_XCD_SKIP_RECUR) {   // W_hh1 rows; after y gathered their terms and h2 out
                 float gh[5];
                 gh1_dots(gh);
                 wait_flag(ygot, tag);
@@ -466,6 +472,17 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
             // ---- waves 5..7: W_hh1 rows (5, 7) → after y gathered their terms and h2 out; after
             // f1 gathered: h2 (wave 6, then flag), S quarters (5, 6), the ring (7); after h2
             // gathered: W_hh2·h2 (VGPR rows)
+            if (WRNN_XCD_SKIP_RECUR) {
+                if (wave == 7) {
+                    wait_flag(f1got, tag);
+                    if (t + 2 >= a.t0 + 3) {
+                        if (t + 2 <= t_terms && lane < kXTerms / 4)
+                            reinterpret_cast<f4v *>(RING(t + 2))[lane] = reinterpret_cast<const f4v *>(TERMS(t + 2))[lane];
+                        if (t + 2 < a.L && lane < 11) NZ(t + 2)[lane] = noise_term(t + 2);
+                    }
+                }
+                goto step_end;
+            }
             if (wave != 6) {
                 float gh[5];
                 gh1_dots(gh);
@@ -513,6 +530,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
                 XSTAMPW(13, 5);
             }
         }
+    step_end:
         bar();
         // next step's x, GRU1 terms and the abort word: one LDS round trip
         const int ab = *abort_flag;
