@@ -47,6 +47,10 @@
 
 namespace wrnn {
 
+#ifndef WRNN_XCDM_FC3_LOCAL_MINQ
+#define WRNN_XCDM_FC3_LOCAL_MINQ 1
+#endif
+
 // Σ of the wave's four k-slices (lanes l, l ^ 16, l ^ 32, l ^ 48): identical bits in all four
 __device__ __forceinline__ f4v kslice_sum(f4v d) {
     return f4v{cross_rows(d.x), cross_rows(d.y), cross_rows(d.z), cross_rows(d.w)};
@@ -514,6 +518,9 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int NR = 4 * NQ;
     constexpr bool kTwoLevel = NQ >= 2;
+    // fc3 partials by the waves that own the rows, no barrier (WRNN_XCDM_FC3_LOCAL_MINQ: from how
+    // many quads on; measured in profiles/r04_ab_xcdm_fc3_local.log)
+    constexpr bool kFc3Local = NQ >= WRNN_XCDM_FC3_LOCAL_MINQ;
     constexpr int N = kXcdWgs * kMRing;   // the compact terms record (capi.cpp: d_xmWt)
     const XcdmLds ll = xcdm_lds_layout(NQ, kDbg, kRaw);
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -802,6 +809,35 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
             mlayer_lds<NQ>(A, a3s + wave * kMJ * 64, stg, pfc1, lane, wave);
             bar();
             if (gru) xpub(xg + kMHopOff[MH_LG] + gn * 512 + 16 * c + gu, tag, mpart<NQ>(pfc1, gu, gn) + cst[MC_B3 + gu]);
+        } else if (kFc3Local) {
+            // fc3 (:223) partial logits of the own 16 f2 rows, by the wave that wrote those rows' f2
+            // (gru threads: row gn = tid >> 4, whole waves): a wave-local LDS round trip instead of
+            // a workgroup barrier; lane l: logits (l & 15) and (l & 15) + 16 of row 4·wave + (l >> 4)
+            if (gru) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+                const int fn = 4 * wave + (lane >> 4);
+                f4v fv[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) fv[q] = lds4(f2s + fn * kMW3Stride + 4 * q);
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh) {
+                    const int fj = (lane & 15) + 16 * hh;
+                    f4v wv[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) wv[q] = lds4(w3s + fj * kMW3Stride + 4 * q);
+                    float p = 0.0f;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        p = fmaf(wv[q].x, fv[q].x, p);
+                        p = fmaf(wv[q].y, fv[q].y, p);
+                        p = fmaf(wv[q].z, fv[q].z, p);
+                        p = fmaf(wv[q].w, fv[q].w, p);
+                    }
+                    xpub(xg + kMHopOff[MH_F2] + (fn * kXcdWgs + c) * 32 + fj, tag, p);
+                }
+            }
+            MST(17);
         } else {
             bar();
             MST(17);
