@@ -39,6 +39,11 @@ def test_generate_sharded_nccl_world1():
             ref = m.generate(mel, None, False, 11000, 550, True, seed=77, row_offset=i, verbose=False)
             assert got[i].dtype == np.float64 and got[i].shape == ref.shape
             assert np.abs(got[i] - ref).max() <= 2e-5, i
+        # one utterance's folds sharded (at world 1: every fold on this rank) = generate(batched=True)
+        mel = torch.from_numpy(syn.make_mel(d.feat_dims, 60, 99))[None]
+        wav = sharding.generate_sharded_folds(m, mel, 3000, 150, True, base_seed=5, device=dev)
+        ref = m.generate(mel, None, True, 3000, 150, True, seed=5, verbose=False)
+        assert wav.dtype == np.float64 and wav.shape == ref.shape and np.abs(wav - ref).max() <= 2e-5
         from wavernn_amd.deepmind_version import WaveRNN as DM
         dd = syn.DEFAULT_DM
         dm = DM(**dd.ctor_kwargs()).to(dev)

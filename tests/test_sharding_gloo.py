@@ -61,9 +61,14 @@ def _worker(rank, world, port, n_items, batched, q):
         dm = sharding.generate_sharded_deepmind(None, n_items, 5, device=torch.device("cpu"),
                                                 generate_fn=lambda ii, r0: [np.arange(5) * 1000 - 32768 + i
                                                                             for i in ii])
+        # one utterance's folds across the ranks: fold i "generates" fake_audio(i)[:64] (float32)
+        folds = sharding.generate_sharded_folds(_RowsModel(), mels[-1], 0, 0, False, device=torch.device("cpu"),
+                                                fold_fn=lambda ii: np.stack([fake_audio(i)[:64].astype(np.float32)
+                                                                             for i in ii]),
+                                                post_fn=lambda y: y)
         if rank == 0:
             q.put(([None if o is None else o.tolist() for o in out], [d.tolist() for d in dm],
-                   [str(d.dtype) for d in dm]))
+                   [str(d.dtype) for d in dm], folds.tolist()))
     finally:
         dist.destroy_process_group()
 
@@ -77,7 +82,7 @@ def test_sharded_gather_reassembles_in_order(n_items, batched):
     procs = [ctx.Process(target=_worker, args=(r, world, port, n_items, batched, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got, dm, dm_dtypes = q.get(timeout=120)
+    got, dm, dm_dtypes, folds = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -89,6 +94,9 @@ def test_sharded_gather_reassembles_in_order(n_items, batched):
     assert dm_dtypes == ["int64"] * n_items
     for i, d in enumerate(dm):
         np.testing.assert_array_equal(d, np.arange(5) * 1000 - 32768 + i)
+    n_folds = _RowsModel.rows_of(20 + 7 * (n_items - 1), True, 0, 0)
+    np.testing.assert_array_equal(np.asarray(folds, np.float32),
+                                  np.stack([fake_audio(i)[:64].astype(np.float32) for i in range(n_folds)]))
 
 
 def test_shard_indices_partition():

@@ -107,3 +107,46 @@ def generate_sharded_deepmind(model, n_utterances: int, seq_len: int, base_seed:
     outs = (generate_fn or _gen)(idx, idx[0]) if idx else []
     got = gather_audio({i: np.asarray(o, dtype=np.float64) for i, o in zip(idx, outs)}, n_utterances, device, group)
     return None if got is None else [g.astype(np.int64) for g in got]
+
+
+def generate_sharded_folds(model, mel, target: int, overlap: int, mu_law: bool, base_seed: int = 0,
+                           device: Optional[torch.device] = None, group=None,
+                           fold_fn: Optional[Callable] = None, post_fn: Optional[Callable] = None
+                           ) -> Optional[np.ndarray]:
+    """ONE long utterance's fold-batched generate() (fatchord_version.py:169-264 with
+    batched=True; SURVEY.md §8(e): "the 60 s single-utterance case can shard folds across GPUs")
+    over the process group: rank r runs the contiguous block of folds shard_indices(folds, r, world)
+    as the rows of one loop launch keyed by the GLOBAL fold index (Philox row = fold), the fold
+    outputs are all-gathered (float32 carried as float64: exact) and rank 0 runs the float64
+    cross-fade / unfold / fade on the device.  Rank 0 returns the waveform, other ranks None; it
+    equals model.generate(mel, None, True, target, overlap, mu_law, seed=base_seed) up to the
+    MoL tolerance between launches of different shapes (RAW labels exactly).
+    fold_fn(fold_indices) -> [n][steps] and post_fn([folds][steps] float32) -> waveform replace the
+    device work (host tests)."""
+    from . import condition
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if fold_fn is None:
+        if device is None:
+            device = next(model.parameters()).device
+        cond, wave_len = model.conditioning(mel, True, target, overlap)
+        n_folds = cond.shape[1]
+        mu = mu_law if model.mode == 'RAW' else False
+
+        def fold_fn(ii):
+            y, _ = model.loop_handle().generate(cond[:, ii[0]:ii[-1] + 1].contiguous(), seed=base_seed,
+                                                row_offset=ii[0])
+            return y.cpu().numpy()
+
+        def post_fn(y_all):
+            y = torch.from_numpy(np.ascontiguousarray(y_all, dtype=np.float32)).to(device)
+            return condition.postprocess(y, True, overlap, mu, model.n_classes, wave_len,
+                                         20 * model.hop_length).cpu().numpy()
+    else:
+        n_folds = model.rows_of(np.shape(mel)[-1], True, target, overlap)
+    idx = shard_indices(n_folds, rank, world)
+    local = fold_fn(idx) if idx else np.zeros((0, 0), np.float32)
+    got = gather_audio({i: np.asarray(local[j], dtype=np.float64) for j, i in enumerate(idx)}, n_folds, device, group)
+    if got is None:
+        return None
+    return post_fn(np.stack(got).astype(np.float32))
