@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define WRNN_ABI_VERSION 5
+#define WRNN_ABI_VERSION 6
 
 enum wrnn_status {
     WRNN_OK = 0,
@@ -170,6 +170,26 @@ int wrnn_cond_shape(const wrnn_upsample_cfg *cfg, int B, int T, int target, int 
  *   cond  [steps][rows][feat_dims + res_out_dims]  (device; row = b·num_folds + fold) */
 int wrnn_upsample_pack(const wrnn_upsample_cfg *cfg, const float *mel, const float *aux, int B, int T,
                        int target, int overlap, float *cond, void *stream);
+
+/* wrnn_upsample_pack + wrnn_generate in one call, from the generate() inputs at FRAME rate
+ * (ABI 6): mel [U][feat_dims][T] and aux [U][res_out_dims][T] (MelResNet of the padded mel) for U
+ * utterances of T frames each; rows / steps as wrnn_cond_shape (target <= 0: unbatched, row u =
+ * utterance u; else utterance u's folds are rows u·nf .. u·nf + nf − 1).  noise, seed, row_offset,
+ * out, labels as wrnn_generate.
+ * The UpsampleNetwork is linear and frame-shift-invariant, so on the XCD-resident paths the
+ * conditioning terms W·[mel_up | aux | 1] are formed as W·(frames) — a GEMM over T frames instead
+ * of hop·T samples — plus a per-sample sum of ≤ 8 frame rows weighted by the stretch/conv
+ * cascade's response (csrc/frame_terms.hip); the other paths get wrnn_upsample_pack's records.
+ * Replaces fatchord_version.py:183-241 (pad → upsample → fold → sample loop). */
+int wrnn_generate_frames(wrnn_t *h, const wrnn_upsample_cfg *ucfg, const float *mel, const float *aux, int U, int T,
+                         int target, int overlap, const float *noise, uint64_t seed, int64_t row_offset, float *out,
+                         int32_t *labels, void *stream);
+
+/* The frame weights wrnn_generate_frames uses (host, stateless): mel_up(p) = Σ_k coef[φ][k] ·
+ * mel[f + k + jlo] for p = f·hop + φ, 0 <= k < nJ — the Stretch2d/Conv2d cascade's response to
+ * one frame, float64 rounded to fp32.  coef (nullable) [hop][nJ], coef_cap floats.
+ * WRNN_EUNSUPPORTED when pad frames do not cover the response's reach or nJ > 8. */
+int wrnn_frame_weights(const wrnn_upsample_cfg *ucfg, int *hop, int *nJ, int *jlo, float *coef, int coef_cap);
 
 /* generate()'s float64 post-processing on the device (fatchord_version.py:243-258):
  * decode_mu_law (utils/dsp.py:98-103, mu = n_classes) when `mu_law`, xfade_and_unfold

@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_lib", "libwavernn_amd.so")
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 MODE_RAW, MODE_MOL, MODE_DM = 0, 1, 2
 STATUS = {0: "WRNN_OK", -1: "WRNN_EINVAL", -2: "WRNN_EHIP", -3: "WRNN_ENOWEIGHTS", -4: "WRNN_ETIMEOUT",
           -5: "WRNN_ENOMEM", -6: "WRNN_EUNSUPPORTED"}
@@ -18,7 +18,8 @@ STATUS = {0: "WRNN_OK", -1: "WRNN_EINVAL", -2: "WRNN_EHIP", -3: "WRNN_ENOWEIGHTS
 # Every symbol include/wavernn_amd.h declares (tests check the .so exports all of them).
 EXPORTS = ("wrnn_create", "wrnn_set_weights", "wrnn_generate", "wrnn_check", "wrnn_elapsed_ms",
            "wrnn_query", "wrnn_last_error", "wrnn_destroy", "wrnn_cond_shape", "wrnn_upsample_pack",
-           "wrnn_postprocess", "wrnn_cond_last_error")
+           "wrnn_postprocess", "wrnn_cond_last_error", "wrnn_generate_frames",
+           "wrnn_frame_weights")
 
 
 class WrnnError(RuntimeError):
@@ -86,6 +87,11 @@ def lib() -> ctypes.CDLL:
     L.wrnn_upsample_pack.restype = i32
     L.wrnn_postprocess.argtypes = [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp]
     L.wrnn_postprocess.restype = i32
+    L.wrnn_generate_frames.argtypes = [vp, ctypes.POINTER(UpsampleCfg), vp, vp, i32, i32, i32, i32, vp, u64, i64, vp,
+                                       vp, vp]
+    L.wrnn_generate_frames.restype = i32
+    L.wrnn_frame_weights.argtypes = [ctypes.POINTER(UpsampleCfg), pi, pi, pi, vp, i32]
+    L.wrnn_frame_weights.restype = i32
     L.wrnn_cond_last_error.argtypes = []
     L.wrnn_cond_last_error.restype = ctypes.c_char_p
     _lib = L

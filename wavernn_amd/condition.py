@@ -51,11 +51,29 @@ class UpsampleSpec:
         res_out = upsample.resnet.conv_out.out_channels
         return cls(feat_dims, res_out, pad, scales, taps)
 
+    def with_res_out(self, res_out_dims: int) -> "UpsampleSpec":
+        """The same cascade for an aux input of res_out_dims channels (zero-padded dims)."""
+        return UpsampleSpec(self.cfg.feat_dims, res_out_dims, self.cfg.pad, self.scales, self._taps)
+
     def shape(self, B: int, T: int, target: int, overlap: int) -> Tuple[int, int]:
         steps, rows = ctypes.c_int(), ctypes.c_int()
         nat.check_cond(nat.lib().wrnn_cond_shape(ctypes.byref(self.cfg), B, T, target, overlap,
                                                  ctypes.byref(steps), ctypes.byref(rows)))
         return steps.value, rows.value
+
+
+def frame_weights(spec: UpsampleSpec) -> Tuple[int, int, np.ndarray]:
+    """(jlo, nJ, coef [hop][nJ]) with mel_up(f·hop + φ) = Σ_k coef[φ][k]·mel[f + k + jlo] — the
+    cascade's frame weights wrnn_generate_frames forms the conditioning terms with (host call)."""
+    hop, nJ, jlo = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    rc = nat.lib().wrnn_frame_weights(ctypes.byref(spec.cfg), ctypes.byref(hop), ctypes.byref(nJ), ctypes.byref(jlo),
+                                      None, 0)
+    if rc != 0:
+        raise nat.WrnnError(rc, "the upsample cascade has no exact frame-rate form (pad frames < its reach)")
+    coef = np.zeros((hop.value, nJ.value), np.float32)
+    nat.check_cond(nat.lib().wrnn_frame_weights(ctypes.byref(spec.cfg), None, None, None,
+                                                coef.ctypes.data_as(ctypes.c_void_p), coef.size))
+    return jlo.value, nJ.value, coef
 
 
 def _stream(dev: torch.device) -> ctypes.c_void_p:

@@ -28,7 +28,12 @@ namespace wrnn {
 hipError_t launch_ci_gemm(const float *cond, int CD, int Bt, int b0, int Bc, int t0, int L, const float *W, int ldw,
                           const float *bias, int N, int K, float *cI, int ldc, hipStream_t st);
 hipError_t launch_pack_cond_input(const float *cond, int CD, int Bt, int b0, int B, int t0, int Lc, int KX, float *X,
-                                  hipStream_t st, int split = 0);
+                                  hipStream_t st, int split = 0, float one = 1.0f);
+hipError_t launch_frame_cond(const float *mel, const float *aux, int U, int feat, int A4, int NF, int frames, int jlo,
+                             int kind, float *rec, hipStream_t st);
+hipError_t launch_terms_interp(const float *FT, const float *AT, const float *coef, float *T, int N, int U, int NF,
+                               int NFF, int hop, int nJ, int nf, int stride, int b0, int nb, int t0, int nt,
+                               hipStream_t st);
 hipError_t launch_pack_terms_input(const float *cond, int CD, int Bt, int b0, int B, int t0, int Lc, int feat, int A,
                                    int R, int KX, float *X, hipStream_t st);
 hipError_t launch_rows(const RowsArgs &a, const RowsGroup *g1, size_t lds_bytes, hipStream_t st);
@@ -161,6 +166,12 @@ struct wrnn_ctx {
     size_t dxnoise_cap = 0;
     unsigned long long *d_dxxg = nullptr;
     unsigned long long *d_xmxg = nullptr;
+    // frame-rate conditioning terms (wrnn_generate_frames, frame_terms.hip): the cascade's
+    // per-phase frame weights, W·(mel frame) and W·(aux frame, ones) rows, their GEMM input
+    // records, and the per-sample conditioning of the paths that still take it
+    float *d_coef = nullptr, *d_FT = nullptr, *d_AT = nullptr, *d_frec = nullptr, *d_cond = nullptr;
+    size_t coef_cap = 0, FT_cap = 0, AT_cap = 0, frec_cap = 0, cond_cap = 0;
+    std::vector<float> coef_host;                   // the table d_coef holds (re-uploaded when it changes)
 };
 
 namespace {
@@ -1657,6 +1668,87 @@ int generate_split(wrnn_t *h, const float *cond, int B, int L, const float *nois
     return WRNN_OK;
 }
 
+// ---- frame-rate conditioning terms (frame_terms.hip) -------------------------------------
+// A loop row's terms come from its utterance's frame rows: row r is utterance r / nf starting at
+// step (r % nf)·stride (fold_with_overlap, fatchord_version.py:317-330; unbatched nf = 1).
+struct FrameSrc {
+    const float *mel = nullptr, *aux = nullptr;   // [U][feat][NF], [U][4·aux][NF] (device)
+    int U = 0, NF = 0, nf = 1, stride = 0;
+    int hop = 1, nJ = 1, jlo = 0;
+    const float *coef = nullptr;                  // [hop][nJ] (device)
+};
+
+// The UpsampleNetwork's frame weights (fatchord_version.py:64-89): the response κ of pad →
+// Stretch2d(s_i) → Conv2d(1, 2s_i+1, pad s_i) (×n) to one unit frame, in float64, as
+// coef[φ][k] = κ(φ − hop·(k + jlo)).  Each stage spreads a frame by ±s_i samples at its rate,
+// E = Σ s_i·hop / r_i samples at the output rate (r_i = s_1···s_i): κ lives on [−E, hop − 1 + E].
+// Exact (equal to the stage-wise zero-padded cascade over the cropped output) when the pad
+// frames cover that reach: pad·hop ≥ E.  Returns false otherwise (the caller keeps the
+// per-sample conditioning path).
+bool frame_weights(const wrnn_upsample_cfg &c, int *hop_out, int *nJ_out, int *jlo_out, std::vector<float> &coef) {
+    int hop = 1;
+    for (int i = 0; i < c.n_scales; ++i) hop *= c.scales[i];
+    long long E = 0;
+    for (int i = 0, r = 1; i < c.n_scales; ++i) {
+        r *= c.scales[i];
+        E += (long long)c.scales[i] * (hop / r);
+    }
+    if ((long long)c.pad * hop < E) return false;
+    const int jlo = -(int)((hop - 1 + E) / hop), jhi = (int)((E + hop - 1) / hop);
+    const int nJ = jhi - jlo + 1;
+    if (nJ > 8) return false;
+    // unit frame at index W of 2W + 1 frames, W beyond the reach
+    const int W = jhi - jlo + 1;
+    std::vector<double> x(2 * W + 1, 0.0);
+    x[W] = 1.0;
+    for (int i = 0; i < c.n_scales; ++i) {
+        const int s = c.scales[i];
+        std::vector<double> y(x.size() * s), z(x.size() * s, 0.0);
+        for (size_t n = 0; n < y.size(); ++n) y[n] = x[n / s];
+        for (long long n = 0; n < (long long)z.size(); ++n) {
+            double acc = 0.0;
+            for (int m = 0; m <= 2 * s; ++m) {
+                const long long q = n + m - s;
+                if (q >= 0 && q < (long long)y.size()) acc += (double)c.taps[i][m] * y[q];
+            }
+            z[n] = acc;
+        }
+        x.swap(z);
+    }
+    coef.assign((size_t)hop * nJ, 0.0f);
+    for (int ph = 0; ph < hop; ++ph)
+        for (int k = 0; k < nJ; ++k) {
+            const long long d = ph - (long long)hop * (k + jlo);   // output offset from the frame's first sample
+            const long long n = d + (long long)W * hop;
+            if (n >= 0 && n < (long long)x.size()) coef[(size_t)ph * nJ + k] = (float)x[n];
+        }
+    *hop_out = hop;
+    *nJ_out = nJ;
+    *jlo_out = jlo;
+    return true;
+}
+
+// FT [NF + nJ − 1][U][N] = W·[mel frame | 0 | 0] and AT [NF + 1][U][N] = W·[0 | aux frame | 1]
+// (row NF: W·[0 | 0 | 1]) through the path's own terms GEMM(s): gemm(X, m, C) writes
+// C[m][N] = W·X for X [m][KX] as pack_cond_input lays it out (`split`).
+template <typename Gemm>
+int frame_terms(wrnn_t *h, const FrameSrc &fs, int N, int KX, int split, hipStream_t st, Gemm gemm) {
+    const int feat = h->cfg.feat_dims, A4 = h->CD - feat;
+    const int NFF = fs.NF + fs.nJ - 1, NFA = fs.NF + 1, fmax = std::max(NFF, NFA);
+    if (grow(h, h->d_frec, h->frec_cap, (size_t)fmax * fs.U * h->CD) ||
+        grow(h, h->d_X, h->X_cap, (size_t)fmax * fs.U * KX) || grow(h, h->d_FT, h->FT_cap, (size_t)NFF * fs.U * N) ||
+        grow(h, h->d_AT, h->AT_cap, (size_t)NFA * fs.U * N))
+        return WRNN_EHIP;
+    for (int kind = 0; kind < 2; ++kind) {
+        const int frames = kind ? NFA : NFF;
+        HIP_TRY(h, launch_frame_cond(fs.mel, fs.aux, fs.U, feat, A4, fs.NF, frames, fs.jlo, kind, h->d_frec, st));
+        HIP_TRY(h, launch_pack_cond_input(h->d_frec, h->CD, fs.U, 0, fs.U, 0, frames, KX, h->d_X, st, split,
+                                          kind ? 1.0f : 0.0f));
+        if (int rc = gemm(h->d_X, frames * fs.U, kind ? h->d_AT : h->d_FT)) return rc;
+    }
+    return WRNN_OK;
+}
+
 // MoL rows through the XCD-resident kernel: up to 8 rows per launch (row k on XCD k), time
 // chunks sized so terms + GEMM input stay within WRNN_TERMS_MB (default 8192 MiB).  Each chunk's
 // terms cover one step past its end (step t publishes the GRU1 terms of t + 1); the recurrent
@@ -1667,13 +1759,23 @@ int generate_split(wrnn_t *h, const float *cond, int B, int L, const float *nois
 // the terms of step t + 1), the recurrent state carried per workgroup between chunks.
 // n_terms = terms per workgroup and step, state_w = carried floats per workgroup.
 template <typename Args, typename Slab>
-int generate_xcd_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed,
-                      int64_t row_offset, float *out, hipStream_t st, int n_terms, int state_w, const Slab &slab,
-                      hipError_t (*launch)(const Args &, hipStream_t)) {
+int generate_xcd_rows(wrnn_t *h, const float *cond, const FrameSrc *fs, int B, int L, const float *noise,
+                      uint64_t seed, int64_t row_offset, float *out, hipStream_t st, int n_terms, int state_w,
+                      const Slab &slab, hipError_t (*launch)(const Args &, hipStream_t)) {
     const int N = kXcdWgs * n_terms;
     if (!h->blas && rocblas_create_handle(&h->blas) != rocblas_status_success)
         return fail(h, WRNN_EHIP, "rocblas_create_handle failed");
     if (rocblas_set_stream(h->blas, st) != rocblas_status_success) return fail(h, WRNN_EHIP, "rocblas_set_stream failed");
+    if (fs) {   // frame-rate terms: W·(frames) once, then per chunk the nJ-tap sum (frame_terms.hip)
+        const float one = 1.0f, zero = 0.0f;
+        const int rc = frame_terms(h, *fs, N, h->KXc, 0, st, [&](const float *X, int m, float *C) -> int {
+            if (rocblas_sgemm(h->blas, rocblas_operation_transpose, rocblas_operation_none, N, m, h->KXc, &one,
+                              h->d_xWt, h->KXc, X, h->KXc, &zero, C, N) != rocblas_status_success)
+                return fail(h, WRNN_EHIP, "rocblas_sgemm (frame terms) failed");
+            return WRNN_OK;
+        });
+        if (rc) return rc;
+    }
     const char *mb_env = std::getenv("WRNN_TERMS_MB");
     const double budget = (mb_env ? std::atof(mb_env) : 8192.0) * (1 << 20) / 4.0;   // floats
     const size_t xg_words = (size_t)kXcds * kXXcdStride;
@@ -1701,10 +1803,15 @@ int generate_xcd_rows(wrnn_t *h, const float *cond, int B, int L, const float *n
         for (int t0 = 0; t0 < L; t0 += Lc_max) {
             const int Lc = std::min(Lc_max, L - t0);
             const int rows = std::min(Lc + 1, L - t0);     // terms rows: steps [t0, t0 + rows)
-            HIP_TRY(h, launch_pack_cond_input(cond, h->CD, B, b0, nb, t0, rows, h->KXc, h->d_X, st));
-            if (rocblas_sgemm(h->blas, rocblas_operation_transpose, rocblas_operation_none, N, rows * nb, h->KXc, &one,
-                              h->d_xWt, h->KXc, h->d_X, h->KXc, &zero, h->d_T, N) != rocblas_status_success)
-                return fail(h, WRNN_EHIP, "rocblas_sgemm (conditioning terms) failed");
+            if (fs) {
+                HIP_TRY(h, launch_terms_interp(h->d_FT, h->d_AT, fs->coef, h->d_T, N, fs->U, fs->NF, fs->NF + fs->nJ - 1,
+                                               fs->hop, fs->nJ, fs->nf, fs->stride, b0, nb, t0, rows, st));
+            } else {
+                HIP_TRY(h, launch_pack_cond_input(cond, h->CD, B, b0, nb, t0, rows, h->KXc, h->d_X, st));
+                if (rocblas_sgemm(h->blas, rocblas_operation_transpose, rocblas_operation_none, N, rows * nb, h->KXc,
+                                  &one, h->d_xWt, h->KXc, h->d_X, h->KXc, &zero, h->d_T, N) != rocblas_status_success)
+                    return fail(h, WRNN_EHIP, "rocblas_sgemm (conditioning terms) failed");
+            }
             HIP_TRY(h, hipMemsetAsync(h->d_members, 0, kXcds * sizeof(int), st));
             Args a{};
             a.slab = h->d_xslab;
@@ -1734,23 +1841,23 @@ int generate_xcd_rows(wrnn_t *h, const float *cond, int B, int L, const float *n
     return WRNN_OK;
 }
 
-int generate_xcd(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed, int64_t row_offset,
-                 float *out, hipStream_t st) {
-    return generate_xcd_rows<XcdArgs>(h, cond, B, L, noise, seed, row_offset, out, st, kXTerms, kXStateW, h->xs,
+int generate_xcd(wrnn_t *h, const float *cond, const FrameSrc *fs, int B, int L, const float *noise, uint64_t seed,
+                 int64_t row_offset, float *out, hipStream_t st) {
+    return generate_xcd_rows<XcdArgs>(h, cond, fs, B, L, noise, seed, row_offset, out, st, kXTerms, kXStateW, h->xs,
                                       launch_xcd);
 }
 
-int generate_xcds(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed, int64_t row_offset,
-                  float *out, hipStream_t st) {
-    return generate_xcd_rows<XcdsArgs>(h, cond, B, L, noise, seed, row_offset, out, st, kSTerms, kSStateW, h->xss,
+int generate_xcds(wrnn_t *h, const float *cond, const FrameSrc *fs, int B, int L, const float *noise, uint64_t seed,
+                  int64_t row_offset, float *out, hipStream_t st) {
+    return generate_xcd_rows<XcdsArgs>(h, cond, fs, B, L, noise, seed, row_offset, out, st, kSTerms, kSStateW, h->xss,
                                        launch_xcds);
 }
 
 // MoL rows through the XCD-resident many-row kernel: up to kMRowsMax rows per launch (launch row
 // r on XCD r % 8, its row r / 8 there), time chunks sized so terms + GEMM input stay within
 // WRNN_TERMS_MB (default 8192 MiB); the recurrent state is carried per workgroup in d_xmstate.
-int generate_xcdm(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed, int64_t row_offset,
-                  float *out, int32_t *labels, hipStream_t st) {
+int generate_xcdm(wrnn_t *h, const float *cond, const FrameSrc *fs, int B, int L, const float *noise, uint64_t seed,
+                  int64_t row_offset, float *out, int32_t *labels, hipStream_t st) {
     const int N = kXcdWgs * kMRing;   // compact terms record (d_xmWt)
     const bool raw = h->cfg.mode == WRNN_MODE_RAW;
     const int NK = raw ? kMRawNC : 11;              // draws per row-step: Exp(1) per class / MoL uniforms
@@ -1767,6 +1874,20 @@ int generate_xcdm(wrnn_t *h, const float *cond, int B, int L, const float *noise
     const float one = 1.0f, zero = 0.0f;
     XcdmGemm gemms[3];
     xcdm_terms_gemms(*h, gemms);
+    // the segmented terms GEMMs writing C[m][N] for X [m][KXc]
+    auto terms_gemm = [&](const float *X, int m, float *C) -> int {
+        for (const XcdmGemm &g : gemms) {
+            const rocblas_status rs =
+                rocblas_sgemm(h->blas, rocblas_operation_transpose, rocblas_operation_none, g.rows, m, g.k, &one,
+                              h->d_xmWt + (size_t)g.row0 * h->KXc + g.col0, h->KXc, X + g.col0, h->KXc, &zero,
+                              C + g.row0, N);
+            if (rs != rocblas_status_success) return fail(h, WRNN_EHIP, "rocblas_sgemm (conditioning terms) failed");
+        }
+        return WRNN_OK;
+    };
+    if (fs) {   // frame-rate terms (frame_terms.hip)
+        if (int rc = frame_terms(h, *fs, N, h->KXc, h->cfg.feat_dims + h->cfg.aux_dims, st, terms_gemm)) return rc;
+    }
     // diagnostics: WRNN_DEBUG_STAMPS=1 WRNN_DEBUG_FILE=<path>: per-wave phase stamps of the first
     // launch ([256 · kMWaves][kMDbgSteps][kMStamps] shader clocks, int32 header)
     const char *dbg_env = std::getenv("WRNN_DEBUG_STAMPS");
@@ -1790,14 +1911,13 @@ int generate_xcdm(wrnn_t *h, const float *cond, int B, int L, const float *noise
             const int Lc = std::min(Lc_max, L - t0);
             if ((size_t)Lc * nb * h->KXc > h->X_cap || (size_t)Lc * nb * N > h->T_cap)
                 return fail(h, WRNN_EINVAL, "xcdm: terms workspace too small");
-            HIP_TRY(h, launch_pack_cond_input(cond, h->CD, B, b0, nb, t0, Lc, h->KXc, h->d_X, st,
-                                              h->cfg.feat_dims + h->cfg.aux_dims));
-            for (const XcdmGemm &g : gemms) {
-                const rocblas_status rs =
-                    rocblas_sgemm(h->blas, rocblas_operation_transpose, rocblas_operation_none, g.rows, Lc * nb, g.k, &one,
-                                  h->d_xmWt + (size_t)g.row0 * h->KXc + g.col0, h->KXc, h->d_X + g.col0, h->KXc, &zero,
-                                  h->d_T + g.row0, N);
-                if (rs != rocblas_status_success) return fail(h, WRNN_EHIP, "rocblas_sgemm (conditioning terms) failed");
+            if (fs) {
+                HIP_TRY(h, launch_terms_interp(h->d_FT, h->d_AT, fs->coef, h->d_T, N, fs->U, fs->NF, fs->NF + fs->nJ - 1,
+                                               fs->hop, fs->nJ, fs->nf, fs->stride, b0, nb, t0, Lc, st));
+            } else {
+                HIP_TRY(h, launch_pack_cond_input(cond, h->CD, B, b0, nb, t0, Lc, h->KXc, h->d_X, st,
+                                                  h->cfg.feat_dims + h->cfg.aux_dims));
+                if (int rc = terms_gemm(h->d_X, Lc * nb, h->d_T)) return rc;
             }
             HIP_TRY(h, hipMemsetAsync(h->d_members, 0, kXcds * sizeof(int), st));
             XcdmArgs a{};
@@ -2263,20 +2383,13 @@ int wrnn_set_weights(wrnn_t *h, const wrnn_tensor *tensors, int n) {
 constexpr int kXcdDefaultRows = 48;
 constexpr int kXcdmMinRows = 9;
 
-int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed,
-                  int64_t row_offset, float *out, int32_t *labels, void *stream) {
-    if (!h) return WRNN_EINVAL;
-    if (!h->ready) return fail(h, WRNN_ENOWEIGHTS, "weights not (fully) set");
-    if (B <= 0 || L <= 0 || !out || (!cond && !h->dm)) return fail(h, WRNN_EINVAL, "need B > 0, L > 0, cond and out");
-    if (labels && h->cfg.mode == WRNN_MODE_MOL) return fail(h, WRNN_EINVAL, "labels are a RAW / DM output");
-    HIP_TRY(h, hipSetDevice(h->device));
-    hipStream_t st = (hipStream_t)stream;
-    // path: MoL rnn / fc 512 with few rows → the XCD-resident kernel; else one MoL row → the
-    // role-split kernel; otherwise the latency kernel while the rows fit its LDS layout in one
-    // launch, else the multi-row kernel.  WRNN_PATH=xcd|split|latency|rows forces one (tests,
-    // benchmarks)
+// The loop path for B rows (WRNN_PATH=xcd|xcdm|split|latency|rows forces one: tests, benchmarks).
+enum LoopPath { P_LATENCY = 1, P_ROWS = 2, P_DM = 3, P_SPLIT = 4, P_XCD = 5, P_XCDS = 6, P_XCDM = 7, P_DX = 8 };
+static LoopPath choose_path(const wrnn_t *h, int B) {
     const char *path_env = std::getenv("WRNN_PATH");
     const std::string pe = path_env ? path_env : "";
+    // deepmind hidden 896 / quantisation 256: the XCD-resident kernel (WRNN_PATH=rows: the multi-row one)
+    if (h->dm) return h->dx_ok && pe != "rows" ? P_DX : P_DM;
     bool rows = h->max_rows < 1 || B > h->max_rows;
     if (pe == "rows") rows = true;
     if (pe == "latency" && h->max_rows >= 1) rows = false;
@@ -2285,29 +2398,112 @@ int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise
     // beyond that the multi-row kernel's throughput wins)
     // MoL rnn / fc 512, more than kXcdmMinRows rows: the many-row XCD-resident kernel (MFMA)
     // (RAW 512-class: the many-row kernel for every row count — it is the only XCD-resident RAW one)
-    const bool xcdm = h->xcdm_ok &&
-                      (pe == "xcdm" || (pe.empty() && (B >= kXcdmMinRows || h->cfg.mode == WRNN_MODE_RAW)));
-    const bool xcd = !xcdm && h->xcd_ok && (pe == "xcd" || (pe.empty() && B <= kXcdDefaultRows));
+    if (h->xcdm_ok && (pe == "xcdm" || (pe.empty() && (B >= kXcdmMinRows || h->cfg.mode == WRNN_MODE_RAW))))
+        return P_XCDM;
+    if (h->xcd_ok && (pe == "xcd" || (pe.empty() && B <= kXcdDefaultRows))) return P_XCD;
     // MoL rnn 896 with block-sparse GRU weights likewise: the XCD-resident sparse kernel
-    const bool xcds = !xcd && h->xcds_ok && (pe == "xcd" || (pe.empty() && B <= kXcdDefaultRows));
-    const bool split = !xcd && !xcds && h->split_ok && (pe == "split" || (pe.empty() && B == 1));
+    if (h->xcds_ok && (pe == "xcd" || (pe.empty() && B <= kXcdDefaultRows))) return P_XCDS;
+    if (h->split_ok && (pe == "split" || (pe.empty() && B == 1))) return P_SPLIT;
+    return rows ? P_ROWS : P_LATENCY;
+}
+
+// One loop run over the chosen path, between the two timing events.  `fs` (frame-rate terms)
+// only for the XCD-resident paths.
+static int run_loop(wrnn_t *h, LoopPath path, const float *cond, const FrameSrc *fs, int B, int L, const float *noise,
+             uint64_t seed, int64_t row_offset, float *out, int32_t *labels, hipStream_t st) {
     HIP_TRY(h, hipMemsetAsync(h->d_ctl, 0, kCtlWords * sizeof(int), st));
     HIP_TRY(h, hipEventRecord(h->ev0, st));
-    // deepmind hidden 896 / quantisation 256: the XCD-resident kernel (WRNN_PATH=rows: the multi-row one)
-    const bool dx = h->dm && h->dx_ok && pe != "rows";
-    h->last_path = dx ? 8 : h->dm ? (h->dm_gw ? 10 : 3) : xcdm ? 7 : xcd ? 5 : xcds ? 6 : split ? 4 : rows ? (h->rows_gw ? 9 : 2) : 1;
-    const int rc = dx       ? generate_dx(h, B, L, noise, seed, row_offset, out, labels, st)
-                   : h->dm  ? generate_dm(h, B, L, noise, seed, row_offset, out, labels, st)
-                   : xcdm  ? generate_xcdm(h, cond, B, L, noise, seed, row_offset, out, labels, st)
-                   : xcd   ? generate_xcd(h, cond, B, L, noise, seed, row_offset, out, st)
-                   : xcds  ? generate_xcds(h, cond, B, L, noise, seed, row_offset, out, st)
-                   : split ? generate_split(h, cond, B, L, noise, seed, row_offset, out, st)
-                   : rows  ? generate_rows(h, cond, B, L, noise, seed, row_offset, out, labels, st)
-                           : generate_latency(h, cond, B, L, noise, seed, row_offset, out, labels, st);
+    h->last_path = path == P_ROWS && h->rows_gw ? 9 : path == P_DM && h->dm_gw ? 10 : (int)path;
+    int rc = WRNN_OK;
+    switch (path) {
+        case P_DX: rc = generate_dx(h, B, L, noise, seed, row_offset, out, labels, st); break;
+        case P_DM: rc = generate_dm(h, B, L, noise, seed, row_offset, out, labels, st); break;
+        case P_XCDM: rc = generate_xcdm(h, cond, fs, B, L, noise, seed, row_offset, out, labels, st); break;
+        case P_XCD: rc = generate_xcd(h, cond, fs, B, L, noise, seed, row_offset, out, st); break;
+        case P_XCDS: rc = generate_xcds(h, cond, fs, B, L, noise, seed, row_offset, out, st); break;
+        case P_SPLIT: rc = generate_split(h, cond, B, L, noise, seed, row_offset, out, st); break;
+        case P_ROWS: rc = generate_rows(h, cond, B, L, noise, seed, row_offset, out, labels, st); break;
+        default: rc = generate_latency(h, cond, B, L, noise, seed, row_offset, out, labels, st); break;
+    }
     if (rc != WRNN_OK) return rc;
     HIP_TRY(h, hipEventRecord(h->ev1, st));
     h->timed = true;
     return WRNN_OK;
+}
+
+int wrnn_generate(wrnn_t *h, const float *cond, int B, int L, const float *noise, uint64_t seed,
+                  int64_t row_offset, float *out, int32_t *labels, void *stream) {
+    if (!h) return WRNN_EINVAL;
+    if (!h->ready) return fail(h, WRNN_ENOWEIGHTS, "weights not (fully) set");
+    if (B <= 0 || L <= 0 || !out || (!cond && !h->dm)) return fail(h, WRNN_EINVAL, "need B > 0, L > 0, cond and out");
+    if (labels && h->cfg.mode == WRNN_MODE_MOL) return fail(h, WRNN_EINVAL, "labels are a RAW / DM output");
+    HIP_TRY(h, hipSetDevice(h->device));
+    return run_loop(h, choose_path(h, B), cond, nullptr, B, L, noise, seed, row_offset, out, labels,
+                    (hipStream_t)stream);
+}
+
+int wrnn_frame_weights(const wrnn_upsample_cfg *ucfg, int *hop, int *nJ, int *jlo, float *coef, int coef_cap) {
+    if (!ucfg || ucfg->n_scales < 1 || ucfg->n_scales > 4) return WRNN_EINVAL;
+    for (int i = 0; i < ucfg->n_scales; ++i)
+        if (ucfg->scales[i] < 1 || !ucfg->taps[i]) return WRNN_EINVAL;
+    int hh = 1, nj = 1, jl = 0;
+    std::vector<float> c;
+    if (!frame_weights(*ucfg, &hh, &nj, &jl, c)) return WRNN_EUNSUPPORTED;
+    if (hop) *hop = hh;
+    if (nJ) *nJ = nj;
+    if (jlo) *jlo = jl;
+    if (coef) {
+        if (coef_cap < (int)c.size()) return WRNN_EINVAL;
+        std::memcpy(coef, c.data(), c.size() * sizeof(float));
+    }
+    return WRNN_OK;
+}
+
+int wrnn_generate_frames(wrnn_t *h, const wrnn_upsample_cfg *ucfg, const float *mel, const float *aux, int U, int T,
+                         int target, int overlap, const float *noise, uint64_t seed, int64_t row_offset, float *out,
+                         int32_t *labels, void *stream) {
+    if (!h) return WRNN_EINVAL;
+    if (!h->ready) return fail(h, WRNN_ENOWEIGHTS, "weights not (fully) set");
+    if (h->dm) return fail(h, WRNN_EINVAL, "deepmind handles take no conditioning (wrnn_generate)");
+    if (!ucfg || !mel || !out || U <= 0 || T <= 0) return fail(h, WRNN_EINVAL, "need ucfg, mel, out, U > 0, T > 0");
+    if (labels && h->cfg.mode == WRNN_MODE_MOL) return fail(h, WRNN_EINVAL, "labels are a RAW / DM output");
+    if (ucfg->feat_dims != h->cfg.feat_dims || ucfg->res_out_dims != h->CD - h->cfg.feat_dims)
+        return fail(h, WRNN_EINVAL, "upsample config does not match the handle's feat / aux dims");
+    if (ucfg->res_out_dims > 0 && !aux) return fail(h, WRNN_EINVAL, "need aux (MelResNet output)");
+    int L = 0, B = 0;
+    if (int rc = wrnn_cond_shape(ucfg, U, T, target, overlap, &L, &B))
+        return fail(h, rc, std::string("conditioning shape: ") + wrnn_cond_last_error());
+    HIP_TRY(h, hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    const LoopPath path = choose_path(h, B);
+    FrameSrc fs;
+    std::vector<float> coef;
+    bool frames = (path == P_XCD || path == P_XCDS || path == P_XCDM) && std::getenv("WRNN_NO_FRAME_TERMS") == nullptr &&
+                  frame_weights(*ucfg, &fs.hop, &fs.nJ, &fs.jlo, coef);
+    if (frames) {
+        const int N = kXcdWgs * (path == P_XCD ? kXTerms : path == P_XCDS ? kSTerms : kMRing);
+        frames = N % 4 == 0;
+    }
+    if (!frames) {   // the per-sample conditioning (wrnn_upsample_pack) into a handle workspace
+        if (grow(h, h->d_cond, h->cond_cap, (size_t)L * B * h->CD)) return WRNN_EHIP;
+        if (int rc = wrnn_upsample_pack(ucfg, mel, aux, U, T, target, overlap, h->d_cond, stream))
+            return fail(h, rc, std::string("upsample_pack: ") + wrnn_cond_last_error());
+        return run_loop(h, path, h->d_cond, nullptr, B, L, noise, seed, row_offset, out, labels, st);
+    }
+    if (coef != h->coef_host) {
+        if (grow(h, h->d_coef, h->coef_cap, coef.size())) return WRNN_EHIP;
+        HIP_TRY(h, hipMemcpyAsync(h->d_coef, coef.data(), coef.size() * 4, hipMemcpyHostToDevice, st));
+        HIP_TRY(h, hipStreamSynchronize(st));   // `coef` is a local: the copy completes before it goes
+        h->coef_host = coef;
+    }
+    fs.mel = mel;
+    fs.aux = aux;
+    fs.U = U;
+    fs.NF = T;
+    fs.nf = B / U;
+    fs.stride = target > 0 ? target + overlap : 0;
+    fs.coef = h->d_coef;
+    return run_loop(h, path, nullptr, &fs, B, L, noise, seed, row_offset, out, labels, st);
 }
 
 int wrnn_check(wrnn_t *h, void *stream) {
@@ -2398,7 +2594,8 @@ void wrnn_destroy(wrnn_t *h) {
                     (void *)h->d_sWt, (void *)h->g2.d_slab, (void *)h->g2.d_Wt, (void *)h->dm2.d_slab,
                     (void *)h->d_gact, (void *)h->d_xslab, (void *)h->d_xWt, (void *)h->d_xstate, (void *)h->d_xgx,
                     (void *)h->d_members, (void *)h->d_xmslab, (void *)h->d_xmstate, (void *)h->d_xmxg, (void *)h->d_xmnoise,
-                    (void *)h->d_xmWt,
+                    (void *)h->d_xmWt, (void *)h->d_coef, (void *)h->d_FT, (void *)h->d_AT, (void *)h->d_frec,
+                    (void *)h->d_cond,
                     (void *)h->d_dxslab, (void *)h->d_dxstate, (void *)h->d_dxnoise, (void *)h->d_dxxg})
         if (p) (void)hipFree(p);
     if (h->blas) (void)rocblas_destroy_handle(h->blas);

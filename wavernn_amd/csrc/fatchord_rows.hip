@@ -559,26 +559,27 @@ __global__ void pack_terms_input_kernel(const float *__restrict__ cond, int CD, 
 // split == 0: X' = [cond record | 1 | 0 ...]; split > 0 (the many-row kernel's segmented terms
 // GEMM): X'' = [cond[:split] | 1 | cond[split:] | 1 | 0 ...] — a ones column after mel‖a1 and
 // another after a4, so the P and V term types each find their bias column inside their K range
+// `one`: the value of the ones columns (0 for the frame-rate mel terms, frame_terms.hip)
 __global__ void pack_cond_input_kernel(const float *__restrict__ cond, int CD, int Bt, int b0, int B, int t0, int M,
-                                       int KX, int split, float *__restrict__ X) {
+                                       int KX, int split, float one, float *__restrict__ X) {
     const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (m >= M) return;
     const int tl = m / B, b = m - tl * B;
     const float *src = cond + ((size_t)(t0 + tl) * Bt + b0 + b) * CD;
     float *dst = X + (size_t)m * KX;
     if (split == 0) {
-        for (int k = threadIdx.x & 63; k < KX; k += 64) dst[k] = k < CD ? src[k] : (k == CD ? 1.0f : 0.0f);
+        for (int k = threadIdx.x & 63; k < KX; k += 64) dst[k] = k < CD ? src[k] : (k == CD ? one : 0.0f);
     } else {
         for (int k = threadIdx.x & 63; k < KX; k += 64)
-            dst[k] = k < split ? src[k] : k == split ? 1.0f : k <= CD ? src[k - 1] : (k == CD + 1 ? 1.0f : 0.0f);
+            dst[k] = k < split ? src[k] : k == split ? one : k <= CD ? src[k - 1] : (k == CD + 1 ? one : 0.0f);
     }
 }
 
 hipError_t launch_pack_cond_input(const float *cond, int CD, int Bt, int b0, int B, int t0, int Lc, int KX, float *X,
-                                  hipStream_t st, int split) {
+                                  hipStream_t st, int split, float one) {
     const int M = Lc * B;
     hipLaunchKernelGGL(pack_cond_input_kernel, dim3((M + 3) / 4), dim3(256), 0, st, cond, CD, Bt, b0, B, t0, M, KX,
-                       split, X);
+                       split, one, X);
     return hipGetLastError();
 }
 

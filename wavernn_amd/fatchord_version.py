@@ -189,10 +189,10 @@ class WaveRNN(nn.Module):
         return self._up_spec
 
     @torch.no_grad()
-    def conditioning(self, mels, batched, target, overlap):
-        """pad → upsample → (fold) → time-major [L][B][feat + 4·aux] (fatchord_version.py:183-190).
-        MelResNet runs as torch modules in eval mode (BatchNorm running statistics) like
-        generate(); everything after it is the `wrnn_upsample_pack` HIP kernel."""
+    def frames(self, mels):
+        """generate()'s inputs at frame rate: (mel [U][feat][T], MelResNet(pad_tensor(mel))
+        [U][res_out][T], wave_len) — fatchord_version.py:183-186 up to the upsampling, which the
+        loop entry (wrnn_generate_frames) or condition.upsample_pack performs on the device."""
         device = next(self.parameters()).device
         if device.type != 'cuda':
             raise RuntimeError("WaveRNN.generate runs on the MI355X HIP path: move the model to a GPU "
@@ -204,9 +204,17 @@ class WaveRNN(nn.Module):
             wave_len = (mels.size(-1) - 1) * self.hop_length
             padded = self.pad_tensor(mels.transpose(1, 2), pad=self.pad, side='both').transpose(1, 2)
             aux = self.upsample.resnet(padded)
-            cond = condition.upsample_pack(self._upsample_spec(), mels, aux, target if batched else 0, overlap)
         finally:
             self.train(was_training)
+        return mels.contiguous(), aux.contiguous().float(), wave_len
+
+    @torch.no_grad()
+    def conditioning(self, mels, batched, target, overlap):
+        """pad → upsample → (fold) → time-major [L][B][feat + 4·aux] (fatchord_version.py:183-190).
+        MelResNet runs as torch modules in eval mode (BatchNorm running statistics) like
+        generate(); everything after it is the `wrnn_upsample_pack` HIP kernel."""
+        mels, aux, wave_len = self.frames(mels)
+        cond = condition.upsample_pack(self._upsample_spec(), mels, aux, target if batched else 0, overlap)
         return cond, wave_len
 
     def generate(self, mels, save_path: Union[str, Path, None], batched, target, overlap, mu_law, *,
@@ -222,15 +230,18 @@ class WaveRNN(nn.Module):
         mu_law = mu_law if self.mode == 'RAW' else False
         start = time.time()
         with torch.no_grad():
-            cond, wave_len = self.conditioning(mels, batched, target, overlap)
-            seq_len, b_size, _ = cond.shape
+            # the loop takes the frames: pad → upsample → fold happen inside wrnn_generate_frames
+            # (the conditioning terms formed at frame rate, csrc/frame_terms.hip)
+            mel_f, aux, wave_len = self.frames(mels)
             loop = self.loop_handle()
             nz = None
             if noise is not None:
-                nz = torch.as_tensor(noise, dtype=torch.float32).to(cond.device).contiguous()
+                nz = torch.as_tensor(noise, dtype=torch.float32).to(mel_f.device).contiguous()
             if seed is None:
                 seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-            out, _ = loop.generate(cond, noise=nz, seed=seed, row_offset=row_offset)
+            out, _ = loop.generate_frames(self._upsample_spec(), mel_f, aux, target if batched else 0, overlap,
+                                          noise=nz, seed=seed, row_offset=row_offset)
+            b_size, seq_len = out.shape
             # mu-law, xfade_and_unfold / row 0, trim, fade-out (:243-258) in float64 on the device
             output = condition.postprocess(out, batched, overlap, mu_law, self.n_classes, wave_len,
                                            20 * self.hop_length).cpu().numpy()
@@ -247,6 +258,14 @@ class WaveRNN(nn.Module):
             return 1
         return self.fold_count(n_frames * self.hop_length, target, overlap)[0]
 
+    def _mel_list(self, mels: Sequence) -> List[torch.Tensor]:
+        device = next(self.parameters()).device
+        ms = [torch.as_tensor(m, device=device).to(torch.float32) for m in mels]
+        ms = [m if m.dim() == 3 else m[None] for m in ms]
+        if not ms or any(m.dim() != 3 or m.shape[0] != 1 or m.shape[1] != self.feat_dims for m in ms):
+            raise ValueError(f"mels must be a non-empty sequence of (1, {self.feat_dims}, T) arrays")
+        return ms
+
     @torch.no_grad()
     def conditioning_many(self, mels: Sequence, batched: bool, target: int, overlap: int):
         """Conditioning of several utterances as the rows of ONE loop launch.
@@ -256,11 +275,8 @@ class WaveRNN(nn.Module):
         samples depend only on earlier steps, so trimming to L_i is exact).  Batched: the folds
         of utterance i are rows [r_i, r_i + nf_i), all folds sharing the window target + 2·overlap.
         Mels of one length go through MelResNet and the upsample kernel together."""
-        device = next(self.parameters()).device
-        ms = [torch.as_tensor(m, device=device).to(torch.float32) for m in mels]
-        ms = [m if m.dim() == 3 else m[None] for m in ms]
-        if not ms or any(m.dim() != 3 or m.shape[0] != 1 or m.shape[1] != self.feat_dims for m in ms):
-            raise ValueError(f"mels must be a non-empty sequence of (1, {self.feat_dims}, T) arrays")
+        ms = self._mel_list(mels)
+        device = ms[0].device
         if len({m.shape[2] for m in ms}) == 1:
             cond, wave_len = self.conditioning(torch.cat(ms, 0), batched, target, overlap)
             per = cond.shape[1] // len(ms)
@@ -290,21 +306,29 @@ class WaveRNN(nn.Module):
         mu_law = mu_law if self.mode == 'RAW' else False
         start = time.time()
         with torch.no_grad():
-            cond, spans = self.conditioning_many(mels, batched, target, overlap)
+            ms = self._mel_list(mels)
             loop = self.loop_handle()
-            nz = None
-            if noise is not None:
-                nz = torch.as_tensor(noise, dtype=torch.float32).to(cond.device).contiguous()
             if seed is None:
                 seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-            out, _ = loop.generate(cond, noise=nz, seed=seed, row_offset=row_offset)
+            dev = next(self.parameters()).device
+            nz = None if noise is None else torch.as_tensor(noise, dtype=torch.float32).to(dev).contiguous()
+            if len({m.shape[2] for m in ms}) == 1:
+                # one length: the frames of all utterances go to the loop entry together
+                mel_f, aux, wave_len = self.frames(torch.cat(ms, 0))
+                out, _ = loop.generate_frames(self._upsample_spec(), mel_f, aux, target if batched else 0, overlap,
+                                              noise=nz, seed=seed, row_offset=row_offset)
+                per = out.shape[0] // len(ms)
+                spans = [(i * per, per, out.shape[1], wave_len) for i in range(len(ms))]
+            else:
+                cond, spans = self.conditioning_many(ms, batched, target, overlap)
+                out, _ = loop.generate(cond, noise=nz, seed=seed, row_offset=row_offset)
             waves = [condition.postprocess(out[r0:r0 + n, :steps], batched, overlap, mu_law, self.n_classes,
                                            wave_len, 20 * self.hop_length)
                      for r0, n, steps, wave_len in spans]
             outputs = [w.cpu().numpy() for w in waves]
         self.last_gen_seconds = time.time() - start
         if verbose:
-            self.gen_display(cond.shape[0] - 1, cond.shape[0], cond.shape[1], start)
+            self.gen_display(out.shape[1] - 1, out.shape[1], out.shape[0], start)
         for i, output in enumerate(outputs):
             if save_paths is not None and save_paths[i] is not None:
                 dsp.save_wav(output, save_paths[i], self.sample_rate)

@@ -178,6 +178,48 @@ class FatchordLoop:
             self.check(stream)
         return out, labels
 
+    def generate_frames(self, spec, mel: torch.Tensor, aux: torch.Tensor, target: int = 0, overlap: int = 0,
+                        noise: Optional[torch.Tensor] = None, seed: int = 0, row_offset: int = 0,
+                        want_labels: bool = False, stream=None,
+                        check: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+        """The loop from the generate() inputs at frame rate (C-ABI wrnn_generate_frames):
+        mel [U][feat][T], aux [U][4·aux][T] (MelResNet of the padded mel) fp32 on this GPU, with
+        `spec` the UpsampleNetwork's condition.UpsampleSpec → samples [rows][steps] (+ labels),
+        rows / steps as condition.upsample_pack would lay them out (target <= 0: unbatched)."""
+        for name, t in (("mel", mel), ("aux", aux)):
+            if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.dim() == 3):
+                raise ValueError(f"{name} must be a contiguous fp32 CUDA tensor [U][C][T]")
+        U, feat, T = mel.shape
+        if feat != self.feat_dims or tuple(aux.shape) != (U, 4 * self.aux_dims, T):
+            raise ValueError(f"mel {tuple(mel.shape)} / aux {tuple(aux.shape)} do not match the loop dims")
+        if getattr(self, "_padded", False) and self._dims_p[2] != self.aux_dims:   # aux quarters zero-padded
+            A, Ap = self.aux_dims, self._dims_p[2]
+            ap = torch.zeros(U, 4 * Ap, T, dtype=aux.dtype, device=aux.device)
+            for j in range(4):
+                ap[:, j * Ap:j * Ap + A] = aux[:, j * A:(j + 1) * A]
+            aux = ap
+            spec = spec.with_res_out(4 * Ap)
+        steps, rows = spec.shape(U, T, target, overlap)
+        if noise is not None:
+            if not (noise.is_cuda and noise.dtype == torch.float32 and noise.is_contiguous()):
+                raise ValueError("noise must be a contiguous fp32 CUDA tensor [L][B][K]")
+            if tuple(noise.shape) != (steps, rows, self.noise_k):
+                raise ValueError(f"noise shape {tuple(noise.shape)} != {(steps, rows, self.noise_k)}")
+        out = torch.empty(rows, steps, dtype=torch.float32, device=mel.device)
+        labels = None
+        if want_labels and self.mode == "RAW":
+            labels = torch.empty(rows, steps, dtype=torch.int32, device=mel.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(mel.device).cuda_stream
+        rc = nat.lib().wrnn_generate_frames(self._h, ctypes.byref(spec.cfg), mel.data_ptr(), aux.data_ptr(), U, T,
+                                            target, overlap, noise.data_ptr() if noise is not None else None,
+                                            ctypes.c_uint64(seed & (2 ** 64 - 1)), row_offset, out.data_ptr(),
+                                            labels.data_ptr() if labels is not None else None, stream)
+        nat.check(self._h, rc)
+        if check:
+            self.check(stream)
+        return out, labels
+
     def check(self, stream=None) -> None:
         """Synchronise and raise if the persistent kernel aborted (timeout)."""
         if stream is None:
