@@ -47,8 +47,11 @@
 
 namespace wrnn {
 
+// fc3 partials wave-local (no barrier) from this many quads per XCD on: at B = 115 (4 quads)
+// 12.97 → 12.87 µs/step; at 1 quad (B ≤ 32) the barrier form is faster (5.29 vs 5.35 at B = 10,
+// 6.00 vs 6.12 at B = 32), at 2 quads neutral (profiles/r04_ab_xcdm_fc3_local.log)
 #ifndef WRNN_XCDM_FC3_LOCAL_MINQ
-#define WRNN_XCDM_FC3_LOCAL_MINQ 1
+#define WRNN_XCDM_FC3_LOCAL_MINQ 3
 #endif
 
 // Σ of the wave's four k-slices (lanes l, l ^ 16, l ^ 32, l ^ 48): identical bits in all four
