@@ -54,7 +54,8 @@ def main():
             dense = dense or model(syn.DEFAULT_MOL)
             m = dense
         fn, samples = run(case, m)
-        for mode in ("frames", "per-sample", "frames"):
+        modes = ("frames", "per-sample", "frames") if not os.environ.get("AB_ONLY") else (os.environ["AB_ONLY"],)
+        for mode in modes:
             if mode == "per-sample":
                 os.environ["WRNN_NO_FRAME_TERMS"] = "1"
             else:
