@@ -181,7 +181,8 @@ def other_configs(dev, warm: bool = True, cpu_steps: int = 0, threads: int = 1) 
     outs, dt = _timed(lambda: model.generate_many(mels, None, False, 11000, 550, True, seed=2))
     ms, L2 = model.loop_handle().elapsed_ms(), T5 * d.hop_length
     n = sum(o.shape[0] for o in outs)
-    res["config2_8_streams"] = {"samples_per_s": n / dt, "rtf_per_stream": n / 8 / dt / sr, "rows": 8,
+    res["config2_8_streams"] = {"samples_per_s": n / dt, "rtf_per_gpu": n / dt / sr, "rtf_per_stream": n / 8 / dt / sr,
+                                "rows": 8,
                                 "loop_steps": L2, "device_ms": ms, "wall_s": dt, "us_per_loop_step": ms * 1e3 / L2,
                                 "kernel_path": model.loop_handle().info["last_path"],
                                 "roofline": hbm_roofline(loop_weight_bytes(d) + 8 * COND_BYTES_PER_ROW_STEP, ms * 1e3 / L2,

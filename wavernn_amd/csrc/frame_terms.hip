@@ -59,42 +59,56 @@ struct InterpArgs {
 };
 
 constexpr int kInterpThreads = 256;
-constexpr int kInterpRecs = 8;     // records per workgroup (the column slice's coef / row loads amortised)
+constexpr int kInterpSteps = 32;   // consecutive steps of one row per workgroup: a frame's rows (hop ≥ 32
+                                   // steps) are loaded once and stay in registers
 constexpr int kInterpMaxJ = 8;
 
-// One workgroup: a 1024-float column slice (a float4 per lane) of kInterpRecs consecutive records.
-// Record-uniform values (frame, phase, coefficients) are wave-uniform: scalar loads.
+// One workgroup: a 1 024-float column slice (a float4 per lane) of kInterpSteps consecutive steps of
+// ONE loop row.  The frame rows FT[f .. f + nJ) and AT[f] are reloaded only when the step crosses
+// into another frame (wave-uniform branch), so the pass reads ≈ 6/32 of what it writes: it is
+// bound by the terms it writes, not by re-reading cached rows (8 records of 8 rows per workgroup
+// reloaded all six rows per record: 2.2 TB/s effective).
 __global__ __launch_bounds__(kInterpThreads) void terms_interp_kernel(InterpArgs a) {
     const int c4 = blockIdx.y * kInterpThreads + threadIdx.x;   // float4 column
-    const bool col = 4 * c4 < a.N;
-    const int m0 = blockIdx.x * kInterpRecs;
-    const int M = a.nt * a.nb;
+    if (4 * c4 >= a.N) return;
+    const int nblk = (a.nt + kInterpSteps - 1) / kInterpSteps;
+    const int k = blockIdx.x / nblk, tb = (blockIdx.x - k * nblk) * kInterpSteps;
+    const int r = a.b0 + k, u = r / a.nf;
+    const int s0 = (r - u * a.nf) * a.stride + a.t0;            // utterance position of step t0
     const int L_utt = a.NF * a.hop;
-    for (int m = m0; m < min(m0 + kInterpRecs, M); ++m) {
-        const int tl = m / a.nb, k = m - tl * a.nb;
-        const int r = a.b0 + k, u = r / a.nf;
-        const int p = (r - u * a.nf) * a.stride + a.t0 + tl;
-        if (!col) continue;
-        float4 acc;
-        if (p < L_utt) {
-            const int f = p / a.hop, ph = p - f * a.hop;
-            acc = *reinterpret_cast<const float4 *>(a.AT + ((size_t)f * a.U + u) * a.N + 4 * c4);
-            const float *cf = a.coef + (size_t)ph * a.nJ;
+    const size_t rs = (size_t)a.U * a.N;                         // frame-row stride
+    const float *A0 = a.AT + (size_t)u * a.N + 4 * c4, *F0 = a.FT + (size_t)u * a.N + 4 * c4;
+    float4 fr[kInterpMaxJ], ar = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    int loaded = -1;
+    for (int i = 0; i < kInterpSteps; ++i) {
+        const int tl = tb + i;
+        if (tl >= a.nt) break;
+        const int p = s0 + tl;
+        const int f = p < L_utt ? p / a.hop : a.NF;               // a.NF: past the utterance (W·[0 | 0 | 1])
+        if (f != loaded) {
+            ar = *reinterpret_cast<const float4 *>(A0 + (size_t)f * rs);
+            if (f < a.NF) {
+#pragma unroll
+                for (int j = 0; j < kInterpMaxJ; ++j)
+                    if (j < a.nJ) fr[j] = *reinterpret_cast<const float4 *>(F0 + (size_t)(f + j) * rs);
+            }
+            loaded = f;
+        }
+        float4 acc = ar;
+        if (f < a.NF) {
+            const float *cf = a.coef + (size_t)(p - f * a.hop) * a.nJ;
 #pragma unroll
             for (int j = 0; j < kInterpMaxJ; ++j) {
                 if (j < a.nJ) {
                     const float w = cf[j];
-                    const float4 x = *reinterpret_cast<const float4 *>(a.FT + ((size_t)(f + j) * a.U + u) * a.N + 4 * c4);
-                    acc.x = fmaf(w, x.x, acc.x);
-                    acc.y = fmaf(w, x.y, acc.y);
-                    acc.z = fmaf(w, x.z, acc.z);
-                    acc.w = fmaf(w, x.w, acc.w);
+                    acc.x = fmaf(w, fr[j].x, acc.x);
+                    acc.y = fmaf(w, fr[j].y, acc.y);
+                    acc.z = fmaf(w, fr[j].z, acc.z);
+                    acc.w = fmaf(w, fr[j].w, acc.w);
                 }
             }
-        } else {
-            acc = *reinterpret_cast<const float4 *>(a.AT + ((size_t)a.NF * a.U + u) * a.N + 4 * c4);
         }
-        *reinterpret_cast<float4 *>(a.T + (size_t)m * a.N + 4 * c4) = acc;
+        *reinterpret_cast<float4 *>(a.T + ((size_t)tl * a.nb + k) * a.N + 4 * c4) = acc;
     }
 }
 
@@ -103,7 +117,7 @@ hipError_t launch_terms_interp(const float *FT, const float *AT, const float *co
                                int NFF, int hop, int nJ, int nf, int stride, int b0, int nb, int t0, int nt,
                                hipStream_t st) {
     InterpArgs a{FT, AT, coef, T, N, U, NF, NFF, hop, nJ, nf, stride, b0, nb, t0, nt};
-    const dim3 grid((nt * nb + kInterpRecs - 1) / kInterpRecs, (N / 4 + kInterpThreads - 1) / kInterpThreads);
+    const dim3 grid(nb * ((nt + kInterpSteps - 1) / kInterpSteps), (N / 4 + kInterpThreads - 1) / kInterpThreads);
     hipLaunchKernelGGL(terms_interp_kernel, grid, dim3(kInterpThreads), 0, st, a);
     return hipGetLastError();
 }
