@@ -37,6 +37,10 @@
 #include "wrnn_device.h"
 #include "xcd_device.h"
 
+#ifndef WRNN_DX_ORDERED_ARGMAX
+#define WRNN_DX_ORDERED_ARGMAX 1   // samplers: lane l holds classes 4l..4l+3, value-only max + ballot
+#endif
+
 namespace wrnn {
 
 namespace {
@@ -502,8 +506,8 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
             unsigned spins = 0;
             for (;;) {
-                const u4v v0 = ld16_sc1(rl, (wave * kDxQ + 2 * lane) * 8);
-                const u4v v1 = ld16_sc1(rl, (wave * kDxQ + 2 * lane + 128) * 8);
+                const u4v v0 = ld16_sc1(rl, (wave * kDxQ + (WRNN_DX_ORDERED_ARGMAX ? 4 * lane : 2 * lane)) * 8);
+                const u4v v1 = ld16_sc1(rl, (wave * kDxQ + (WRNN_DX_ORDERED_ARGMAX ? 4 * lane + 2 : 2 * lane + 128)) * 8);
                 const bool ok = (v0.y == tag) & (v0.w == tag) & (v1.y == tag) & (v1.w == tag);
                 if (__ballot(!ok) == 0) {
                     lv = f4v{__uint_as_float(v0.x), __uint_as_float(v0.z), __uint_as_float(v1.x), __uint_as_float(v1.z)};
@@ -520,15 +524,26 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
                 }
             }
             // argmax_c l_c − log q_c ≡ argmax_c p_c / q_c (softmax, Categorical renormalisation and
-            // the draw's scale cancel): lane l holds classes 2l, 2l + 1, 2l + 128, 2l + 129
+            // the draw's scale cancel): lane l holds classes 4l .. 4l + 3, so the winner is the first
+            // lane holding the wave's max (wave_argmax_ordered: no index through the DPP stages)
             const float *lq = nzr + ((t & 1) * 4 + wave) * 2 * kDxQ + half * kDxQ;
-            const f2v q0 = lds2(lq + 2 * lane), q1 = lds2(lq + 2 * lane + 128);
-            float bv = lv.x - q0.x;
-            int bi = 2 * lane;
-            am_merge(bv, bi, lv.y - q0.y, 2 * lane + 1);
-            am_merge(bv, bi, lv.z - q1.x, 2 * lane + 128);
-            am_merge(bv, bi, lv.w - q1.y, 2 * lane + 129);
-            return wave_argmax(bv, bi);
+            if constexpr (WRNN_DX_ORDERED_ARGMAX) {
+                const f4v q = lds4(lq + 4 * lane);
+                float bv = lv.x - q.x;
+                int bi = 4 * lane;
+                am_merge(bv, bi, lv.y - q.y, 4 * lane + 1);
+                am_merge(bv, bi, lv.z - q.z, 4 * lane + 2);
+                am_merge(bv, bi, lv.w - q.w, 4 * lane + 3);
+                return wave_argmax_ordered(bv, bi);
+            } else {   // (round 3: classes 2l, 2l + 1, 2l + 128, 2l + 129, index through the DPP stages)
+                const f2v q0 = lds2(lq + 2 * lane), q1 = lds2(lq + 2 * lane + 128);
+                float bv = lv.x - q0.x;
+                int bi = 2 * lane;
+                am_merge(bv, bi, lv.y - q0.y, 2 * lane + 1);
+                am_merge(bv, bi, lv.z - q1.x, 2 * lane + 128);
+                am_merge(bv, bi, lv.w - q1.y, 2 * lane + 129);
+                return wave_argmax(bv, bi);
+            }
         };
         if (wave < RX) {
             const int cl = sample_row(DX_LC, 0);

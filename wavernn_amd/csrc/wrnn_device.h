@@ -73,6 +73,18 @@ __device__ __forceinline__ int wave_argmax(float v, int i) {
     return bi;
 }
 
+// wave_argmax for layouts whose indices grow with the lane (every index of lane l below every
+// index of lane l + 1, each lane's own candidates merged by am_merge in index order): the same
+// winner — largest value, ties to the smallest index — from a value-only max reduction and the
+// first lane holding it (ballot), instead of carrying the index through every DPP stage.
+// (No lane equals the max only when a NaN is present: then the general reduction decides.)
+__device__ __forceinline__ int wave_argmax_ordered(float v, int i) {
+    const float m = wave_max(v);
+    const unsigned long long hit = __ballot(v == m);
+    if (hit == 0) return wave_argmax(v, i);
+    return __builtin_amdgcn_readlane(i, (int)__builtin_ctzll(hit));
+}
+
 // NR dot products against one shared vector: acc[r] += W[r]·x over K4 float4 chunks,
 // row r at w0 + r·wstride.  Lane l takes chunks l, l+64, … (contiguous 16 B per lane:
 // conflict-free ds_read_b128).
