@@ -9,6 +9,9 @@
 
 namespace wrnn {
 
+#ifndef WRNN_XCD_ORDERED_ARGMAX
+#define WRNN_XCD_ORDERED_ARGMAX 1   // MoL argmax: value-only max over lanes 0..7 + ballot (0: index through DPP)
+#endif
 #ifndef WRNN_XCD_FAST_EXP
 #define WRNN_XCD_FAST_EXP 1     // sampler scale e^s by v_exp_f32 (A/B vs libm expf: 3.92 -> 3.88 us/step, parity unchanged)
 #endif
@@ -74,9 +77,27 @@ __device__ __forceinline__ float mol_sample_pairs(float la, float lb, float ua, 
         int oi = __builtin_amdgcn_mov_dpp(i, (ctrl), 0xF, 0xF, false);                \
         am_merge(v, i, ov, oi);                                                       \
     }
-    WRNN_AM_STAGE(0xB1) WRNN_AM_STAGE(0x4E) WRNN_AM_STAGE(0x141) WRNN_AM_STAGE(0x140)
+    int k;
+    if constexpr (WRNN_XCD_ORDERED_ARGMAX) {
+        // the components grow with the lane (lane jp: 2jp, 2jp + 1), so the winner is the first of
+        // lanes 0..4 holding the max: three value-only DPP stages cover lanes 0..7 (every DPP row
+        // holds the same bits), a ballot finds the lane (wave_argmax_ordered, specialised)
+        float mv = fmaxf(v, WRNN_DPP(v, 0xB1));
+        mv = fmaxf(mv, WRNN_DPP(mv, 0x4E));
+        mv = fmaxf(mv, WRNN_DPP(mv, 0x141));
+        const float m = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, mv)));
+        const unsigned long long hit = __ballot(v == m) & 0x1Full;
+        if (hit != 0) {
+            k = __builtin_amdgcn_readlane(i, (int)__builtin_ctzll(hit));
+        } else {   // a NaN among the logits: the general reduction
+            WRNN_AM_STAGE(0xB1) WRNN_AM_STAGE(0x4E) WRNN_AM_STAGE(0x141) WRNN_AM_STAGE(0x140)
+            k = __builtin_amdgcn_readlane(i, 0);
+        }
+    } else {
+        WRNN_AM_STAGE(0xB1) WRNN_AM_STAGE(0x4E) WRNN_AM_STAGE(0x141) WRNN_AM_STAGE(0x140)
+        k = __builtin_amdgcn_readlane(i, 0);
+    }
 #undef WRNN_AM_STAGE
-    const int k = __builtin_amdgcn_readlane(i, 0);
     return lane_bcast((k & 1) ? xb : xa, 5 + (k >> 1));
 }
 
