@@ -500,7 +500,7 @@ __device__ __forceinline__ int rsample(const unsigned long long *lg, int n, uint
         am_merge(bv, bi, (e[2 * i] / s2) / q[i].x, 2 * (lane + 64 * i));
         am_merge(bv, bi, (e[2 * i + 1] / s2) / q[i].y, 2 * (lane + 64 * i) + 1);
     }
-    return wave_argmax(bv, bi);
+    return WRNN_XCD_ORDERED_ARGMAX ? wave_argmax_fast(bv, bi) : wave_argmax(bv, bi);
 }
 
 // diagnostics (template kDbg, WRNN_DEBUG_STAMPS=1): lane 0 of every wave stamps the shader clock

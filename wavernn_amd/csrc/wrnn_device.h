@@ -85,6 +85,16 @@ __device__ __forceinline__ int wave_argmax_ordered(float v, int i) {
     return __builtin_amdgcn_readlane(i, (int)__builtin_ctzll(hit));
 }
 
+// wave_argmax for any layout: a value-only max reduction, then the lane holding it (ballot); only
+// when several lanes hold the maximum (an exact tie across lanes) or a NaN is present does the
+// (value, index) reduction decide.  Same winner as wave_argmax.
+__device__ __forceinline__ int wave_argmax_fast(float v, int i) {
+    const float m = wave_max(v);
+    const unsigned long long hit = __ballot(v == m);
+    if (__builtin_popcountll(hit) == 1) return __builtin_amdgcn_readlane(i, (int)__builtin_ctzll(hit));
+    return wave_argmax(v, i);
+}
+
 // NR dot products against one shared vector: acc[r] += W[r]·x over K4 float4 chunks,
 // row r at w0 + r·wstride.  Lane l takes chunks l, l+64, … (contiguous 16 B per lane:
 // conflict-free ds_read_b128).
