@@ -48,6 +48,18 @@ def main():
     cyc_per_us = step / (real / 100.0)
     print(f"B={B}: {live.sum()} workgroups, median stamped step {step:.0f} cycles = {real / 100:.3f} us "
           f"(shader clock {cyc_per_us / 1e3:.2f} GHz); launch incl. the stamp dump {ms * 1e3 / L:.3f} us/step")
+    # step-start skew between the workgroups of one XCD (workgroup b sits on XCD b % 8): the
+    # s_memrealtime stamp (10 ns ticks) of wave 0 at each step start, max − min over the XCD
+    blk = np.nonzero(live)[0]
+    skews = []
+    for x in range(8):
+        sel = st[(blk % 8) == x, 0, :, K - 1]
+        if sel.shape[0] > 1:
+            skews.append(sel.max(0) - sel.min(0))
+    if skews:
+        sk = np.concatenate(skews) / 100.0
+        print(f"step-start skew over an XCD's workgroups: median {np.median(sk):.3f} us, 90th pct "
+              f"{np.percentile(sk, 90):.3f} us, max {sk.max():.3f} us")
     for w in range(waves):
         rel = st[:, w, :, :] - base[:, w]
         print(f"-- wave {w}")
