@@ -91,6 +91,24 @@ def test_frames_xcdm_raw_labels_exact():
     np.testing.assert_array_equal(got, ref)
 
 
+def test_frames_single_fold_longer_than_the_utterance():
+    """target past the utterance: one fold (fold_with_overlap's remainder branch), most of its
+    window the zero tail."""
+    m = _model(syn.DEFAULT_MOL, 8)
+    got, ref, _, _, path = _both(m, 1, 30, 20000, 550, seed=17)   # 8 250 samples, window 21 100
+    assert got.shape == (1, 21100) and path == 5
+    _close(got, ref, "single fold")
+
+
+def test_frames_entry_on_a_non_xcd_path_takes_the_records():
+    """Dims no XCD-resident kernel runs (rnn 64): wrnn_generate_frames builds the per-sample
+    records itself (wrnn_upsample_pack into a handle workspace) — bit-identical to the two calls."""
+    m = _model(syn.TINY_MOL, 2)
+    got, ref, _, _, path = _both(m, 2, 14, 0, 0, seed=18)
+    assert path not in (5, 6, 7)
+    np.testing.assert_array_equal(got, ref)
+
+
 def test_frames_env_fallback_is_the_per_sample_route(monkeypatch):
     monkeypatch.setenv("WRNN_NO_FRAME_TERMS", "1")
     m = _model(syn.DEFAULT_MOL, 3)

@@ -17,7 +17,7 @@ NAMES = {0: "step start", 1: "coarse gates + publish h_c", 2: "h_c poll + stage 
          9: "c_t sampled + barrier", 10: "fine gates + publish h_f", 11: "h_f poll + stage",
          12: "O3 MFMAs + barrier", 13: "O3 epilogue + publish o3", 14: "R fine half MFMAs + partials",
          15: "o3 poll done + staged", 16: "O4 MFMAs + barrier", 17: "O4 epilogue + publish logits",
-         18: "f_t sampled (+ output)"}
+         18: "f_t sampled (+ output)", 19: "w0: h_c published", 20: "h_c poll starts (after vmcnt(0))"}
 
 
 def main():
@@ -60,11 +60,29 @@ def main():
         sk = np.concatenate(skews) / 100.0
         print(f"step-start skew over an XCD's workgroups: median {np.median(sk):.3f} us, 90th pct "
               f"{np.percentile(sk, 90):.3f} us, max {sk.max():.3f} us")
+    # the h_c hop in real time (10 ns ticks): last publish over the XCD's workgroups (slot 22, wave
+    # 0) → each wave's poll done (slot 21); and each workgroup's own publish after its step start
+    hop, own = [], []
+    for x in range(8):
+        m = (blk % 8) == x
+        if m.sum() < 2:
+            continue
+        pub = st[m, 0, :, 22]
+        last = pub.max(0)
+        for w in range(waves):
+            hop.append(st[m, w, :, 21] - last[None, :])
+        own.append(pub - st[m, 0, :, K - 1])
+    if hop:
+        hp, ow = np.concatenate(hop).ravel() / 100.0, np.concatenate(own).ravel() / 100.0
+        ok = (hp > -5) & (hp < 20)
+        print(f"h_c publish after the own step start: median {np.median(ow):.3f} us, max {ow.max():.3f} us; "
+              f"h_c poll done after the XCD's last publish: median {np.median(hp[ok]):.3f} us, "
+              f"90th pct {np.percentile(hp[ok], 90):.3f} us")
     for w in range(waves):
         rel = st[:, w, :, :] - base[:, w]
         print(f"-- wave {w}")
         prev = 0.0
-        for k in range(1, K - 1):
+        for k in [k for k in range(1, K - 1) if k not in (21, 22)]:
             v = rel[..., k]
             v = v[(v > 0) & (v < 10 * step)]
             if v.size == 0:

@@ -303,6 +303,12 @@ __device__ __forceinline__ float dx_o24sum(const float *P, int r, int n) {
 
 }  // namespace
 
+#define DSTR(kk)                                                                                             \
+    do {                                                                                                     \
+        if (kDbg && lane == 0 && (unsigned)(t - a.t0 - kDxDbgSkip) < (unsigned)kDxDbgSteps)                 \
+            dbgs[((t - a.t0 - kDxDbgSkip) * kDxWaves + wave) * kDxStamps + (kk)] =                           \
+                (unsigned)__builtin_amdgcn_s_memrealtime();                                                  \
+    } while (0)
 #define DST(kk)                                                                                              \
     do {                                                                                                     \
         if (kDbg && lane == 0 && (unsigned)(t - a.t0 - kDxDbgSkip) < (unsigned)kDxDbgSteps)                 \
@@ -430,6 +436,8 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             const float ee = tanh_((rr * Rg[2] + I[2]) + cst[DC_BE + gu]);
             hc = uu * hc + (1.0f - uu) * ee;
             xpub(xg + kDxHopOff[DX_HC] + gn * kDxS + kDxU * c + gu, tag, hc);
+            DST(19);
+            DSTR(22);   // (s_memrealtime: the h_c hop measured across workgroups, tools/stamps_dx.py)
         }
         // row group B (WG-local rows 48..83: fine gate rows only) of R·h_{t-1}, both halves from the
         // still-staged h_c(t-1) / h_f(t-1) slices: waves 1..3 while wave 0 runs the coarse gates,
@@ -440,7 +448,9 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         {
             u4v v[4];
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            DST(20);
             dx_poll(hop_rsrc(xg + kDxHopOff[DX_HC]), wave, tag, a.ctl, a.timeout_ticks, t, DX_HC, abort_flag, lane, v);
+            DSTR(21);
             dx_stage(stg_of(2), lane, v);
         }
         // the draws of step t + 1 → registers of waves 1..3; their logs go into the ring while
