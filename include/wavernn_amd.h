@@ -191,6 +191,24 @@ int wrnn_generate_frames(wrnn_t *h, const wrnn_upsample_cfg *ucfg, const float *
  * WRNN_EUNSUPPORTED when pad frames do not cover the response's reach or nJ > 8. */
 int wrnn_frame_weights(const wrnn_upsample_cfg *ucfg, int *hop, int *nJ, int *jlo, float *coef, int coef_cap);
 
+/* The UpsampleNetwork's MelResNet (fatchord_version.py:13-48) in inference form, one kernel:
+ * conv_in (k = 2·pad + 1) → BN → ReLU → res_blocks × [1×1 conv → BN → ReLU → 1×1 conv → BN →
+ * + residual] → conv_out, each BatchNorm (running statistics) folded into its conv on the host.
+ *   packed [wrnn_melresnet_floats(cfg)] (device): conv_in W[(c·K + tap)][C] + bias[C], per block
+ *          W1[C][C] + b1[C] + W2[C][C] + b2[C], conv_out W[C][R] + bias[R] (k-major matrices)
+ *   mel    [U][in_dims][T + 2·pad]  pad_tensor'd mel (device);  aux [U][R][T] (device)
+ * WRNN_EUNSUPPORTED for channel counts the kernel's thread layout does not cover. */
+typedef struct {
+    int32_t in_dims;         /* num_mels (80) */
+    int32_t compute_dims;    /* C (128) */
+    int32_t res_out_dims;    /* R (128) */
+    int32_t res_blocks;      /* 10 */
+    int32_t pad;             /* voc_pad (2): conv_in kernel 2·pad + 1 */
+} wrnn_melresnet_cfg;
+int wrnn_melresnet_floats(const wrnn_melresnet_cfg *cfg);
+int wrnn_melresnet(const wrnn_melresnet_cfg *cfg, const float *packed, const float *mel, int U, int T, float *aux,
+                   void *stream);
+
 /* generate()'s float64 post-processing on the device (fatchord_version.py:243-258):
  * decode_mu_law (utils/dsp.py:98-103, mu = n_classes) when `mu_law`, xfade_and_unfold
  * (:342-405) of the `rows` folds when `batched` (else row 0), trim to wave_len, and

@@ -54,12 +54,15 @@ def main():
             dense = dense or model(syn.DEFAULT_MOL)
             m = dense
         fn, samples = run(case, m)
-        modes = ("frames", "per-sample", "frames") if not os.environ.get("AB_ONLY") else (os.environ["AB_ONLY"],)
+        modes = ("frames", "torch-melresnet", "per-sample", "frames") if not os.environ.get("AB_ONLY") \
+            else (os.environ["AB_ONLY"],)
         for mode in modes:
+            os.environ.pop("WRNN_NO_FRAME_TERMS", None)
+            os.environ.pop("WRNN_TORCH_MELRESNET", None)
             if mode == "per-sample":
                 os.environ["WRNN_NO_FRAME_TERMS"] = "1"
-            else:
-                os.environ.pop("WRNN_NO_FRAME_TERMS", None)
+            elif mode == "torch-melresnet":   # MelResNet through the torch module (MIOpen), not the fused kernel
+                os.environ["WRNN_TORCH_MELRESNET"] = "1"
             fn()
             torch.cuda.synchronize()
             best = 1e9

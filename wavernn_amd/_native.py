@@ -19,7 +19,11 @@ STATUS = {0: "WRNN_OK", -1: "WRNN_EINVAL", -2: "WRNN_EHIP", -3: "WRNN_ENOWEIGHTS
 EXPORTS = ("wrnn_create", "wrnn_set_weights", "wrnn_generate", "wrnn_check", "wrnn_elapsed_ms",
            "wrnn_query", "wrnn_last_error", "wrnn_destroy", "wrnn_cond_shape", "wrnn_upsample_pack",
            "wrnn_postprocess", "wrnn_cond_last_error", "wrnn_generate_frames",
-           "wrnn_frame_weights")
+           "wrnn_frame_weights", "wrnn_melresnet_floats", "wrnn_melresnet")
+
+
+class MelResNetCfg(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("in_dims", "compute_dims", "res_out_dims", "res_blocks", "pad")]
 
 
 class WrnnError(RuntimeError):
@@ -92,6 +96,10 @@ def lib() -> ctypes.CDLL:
     L.wrnn_generate_frames.restype = i32
     L.wrnn_frame_weights.argtypes = [ctypes.POINTER(UpsampleCfg), pi, pi, pi, vp, i32]
     L.wrnn_frame_weights.restype = i32
+    L.wrnn_melresnet_floats.argtypes = [ctypes.POINTER(MelResNetCfg)]
+    L.wrnn_melresnet_floats.restype = i32
+    L.wrnn_melresnet.argtypes = [ctypes.POINTER(MelResNetCfg), vp, vp, i32, i32, vp, vp]
+    L.wrnn_melresnet.restype = i32
     L.wrnn_cond_last_error.argtypes = []
     L.wrnn_cond_last_error.restype = ctypes.c_char_p
     _lib = L

@@ -10,7 +10,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "_lib", "libwavernn_amd.so")
-SOURCES = [os.path.join(CSRC, f) for f in ("fatchord_loop.hip", "fatchord_split.hip", "fatchord_xcd.hip", "fatchord_xcds.hip", "fatchord_xcdm.hip", "fatchord_rows.hip", "deepmind_rows.hip", "deepmind_xcd.hip", "condition.hip", "frame_terms.hip", "capi.cpp")]
+SOURCES = [os.path.join(CSRC, f) for f in ("fatchord_loop.hip", "fatchord_split.hip", "fatchord_xcd.hip", "fatchord_xcds.hip", "fatchord_xcdm.hip", "fatchord_rows.hip", "deepmind_rows.hip", "deepmind_xcd.hip", "condition.hip", "frame_terms.hip", "melresnet.hip", "capi.cpp")]
 HEADERS = [os.path.join(CSRC, f) for f in ("fatchord_loop.h", "fatchord_split.h", "fatchord_xcd.h", "fatchord_xcds.h", "fatchord_xcdm.h", "deepmind_xcd.h", "mfma_device.h", "xcd_device.h", "fatchord_rows.h", "deepmind_rows.h", "wrnn_device.h",
                                            "rows_device.h")] + \
     [os.path.join(REPO, "include", "wavernn_amd.h")]

@@ -76,6 +76,54 @@ def frame_weights(spec: UpsampleSpec) -> Tuple[int, int, np.ndarray]:
     return jlo.value, nJ.value, coef
 
 
+def melresnet_cfg(resnet) -> "nat.MelResNetCfg":
+    """The wrnn_melresnet_cfg of a MelResNet module (reference layout, fatchord_version.py:30-48)."""
+    cfg = nat.MelResNetCfg()
+    cfg.in_dims = resnet.conv_in.in_channels
+    cfg.compute_dims = resnet.conv_in.out_channels
+    cfg.res_out_dims = resnet.conv_out.out_channels
+    cfg.res_blocks = len(resnet.layers)
+    cfg.pad = (resnet.conv_in.kernel_size[0] - 1) // 2
+    return cfg
+
+
+@torch.no_grad()
+def melresnet_pack(resnet) -> torch.Tensor:
+    """wrnn_melresnet's packed weights from a MelResNet module: each BatchNorm (running statistics,
+    eval form) folded into the conv before it — W' = W·γ/√(var + ε), b' = β − μ·γ/√(var + ε), in
+    float64 — matrices k-major.  Lives on the module's device."""
+    def fold(w, bn):
+        s = bn.weight.double() / torch.sqrt(bn.running_var.double() + bn.eps)
+        return w.double() * s.view(-1, *([1] * (w.dim() - 1))), bn.bias.double() - bn.running_mean.double() * s
+
+    parts = []
+    w0, b0 = fold(resnet.conv_in.weight, resnet.batch_norm)            # [C][in][K]
+    parts += [w0.permute(1, 2, 0).reshape(-1), b0]                     # [(c·K + tap)][C]
+    for blk in resnet.layers:
+        w1, b1 = fold(blk.conv1.weight[:, :, 0], blk.batch_norm1)
+        w2, b2 = fold(blk.conv2.weight[:, :, 0], blk.batch_norm2)
+        parts += [w1.t().reshape(-1), b1, w2.t().reshape(-1), b2]
+    parts += [resnet.conv_out.weight[:, :, 0].double().t().reshape(-1), resnet.conv_out.bias.double()]
+    return torch.cat([p.reshape(-1) for p in parts]).float().contiguous()
+
+
+def melresnet(cfg, packed: torch.Tensor, mel_padded: torch.Tensor) -> torch.Tensor:
+    """MelResNet(pad_tensor(mel)) in one HIP kernel: mel_padded [U][in][T + 2·pad] → aux [U][R][T].
+    Raises WrnnError(WRNN_EUNSUPPORTED) for channel counts the kernel does not cover."""
+    _need_gpu(mel_padded, packed)
+    x = mel_padded.contiguous().float()
+    U, cin, Tp = x.shape
+    T = Tp - 2 * cfg.pad
+    if cin != cfg.in_dims or T < 1 or packed.numel() != nat.lib().wrnn_melresnet_floats(ctypes.byref(cfg)):
+        raise ValueError("mel / packed weights do not match the MelResNet config")
+    aux = torch.empty(U, cfg.res_out_dims, T, device=x.device, dtype=torch.float32)
+    rc = nat.lib().wrnn_melresnet(ctypes.byref(cfg), packed.data_ptr(), x.data_ptr(), U, T, aux.data_ptr(),
+                                  _stream(x.device))
+    if rc != 0:
+        raise nat.WrnnError(rc, "wrnn_melresnet")
+    return aux
+
+
 def _stream(dev: torch.device) -> ctypes.c_void_p:
     return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
 

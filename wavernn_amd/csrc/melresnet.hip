@@ -1,0 +1,184 @@
+// melresnet.hip — the UpsampleNetwork's MelResNet (models/fatchord_version.py:13-48) in inference
+// form as ONE kernel: conv_in (k = 2·pad + 1, no padding) → BatchNorm → ReLU → res_blocks ×
+// [1×1 conv → BN → ReLU → 1×1 conv → BN → + residual] → conv_out (1×1, bias), every BatchNorm
+// (eval: running statistics) folded into the preceding conv's weights and a bias on the host
+// (condition.py: melresnet_pack).  The torch module is 2 + 2·res_blocks convolutions and as many
+// BatchNorm / ReLU / add kernels (≈ 80 launches at res_blocks = 10); here a workgroup carries a tile
+// of kMrF frames of one utterance through all layers with the activations in LDS.
+//
+// Packed weights (floats), every matrix k-major ("Wt[k][out]": a wave's 64 lanes read 64
+// consecutive outputs of one k, coalesced):
+//   conv_in  Wt[(c·K + tap)][C], bias[C]          (K = 2·pad + 1, c < in_dims)
+//   block i  Wt1[C][C], b1[C], Wt2[C][C], b2[C]
+//   conv_out Wt[C][R], bias[R]
+// Layer outputs: thread t owns output row t % Cout and kMrFpt = Cout·kMrF / 256 consecutive frames
+// ((t / Cout)·kMrFpt ...): per input k one weight load and kMrFpt / 4 float4 LDS reads (a wave's
+// lanes share the frames: broadcast).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "wavernn_amd.h"
+
+namespace wrnn {
+
+constexpr int kMrThreads = 256;
+constexpr int kMrF = 16;          // frames per workgroup
+
+// (weights from L2: 16 loads issued ahead of their FMAs, so a layer pays ≈ Kin / 16 round trips)
+template <int FPT>
+__device__ __forceinline__ void mr_layer(const float *__restrict__ Wt, const float *__restrict__ bias,
+                                         const float *in, int Kin, int Cout, float (&acc)[FPT], int row, int f0) {
+#pragma unroll
+    for (int i = 0; i < FPT; ++i) acc[i] = bias[row];
+    int k = 0;
+    for (; k + 16 <= Kin; k += 16) {
+        float w[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) w[j] = Wt[(size_t)(k + j) * Cout + row];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const float *x = in + (k + j) * kMrF + f0;
+#pragma unroll
+            for (int i = 0; i < FPT; ++i) acc[i] = fmaf(w[j], x[i], acc[i]);
+        }
+    }
+    for (; k < Kin; ++k) {
+        const float w = Wt[(size_t)k * Cout + row];
+        const float *x = in + k * kMrF + f0;
+#pragma unroll
+        for (int i = 0; i < FPT; ++i) acc[i] = fmaf(w, x[i], acc[i]);
+    }
+}
+
+struct MrArgs {
+    const float *w;       // packed weights (device)
+    const float *mel;     // [U][in_dims][T + 2·pad]  the pad_tensor'd mel
+    float *aux;           // [U][R][T]
+    int U, T, in_dims, C, R, blocks, K;
+};
+
+template <int FPT_C, int FPT_R>
+__global__ __launch_bounds__(kMrThreads) void melresnet_kernel(MrArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int u = blockIdx.y, t0 = blockIdx.x * kMrF, tid = threadIdx.x;
+    const int Tp = a.T + a.K - 1, KF = kMrF + a.K - 1;
+    float *xin = lds;                              // [in_dims][kMrF + K − 1]  the mel tile (+ halo)
+    float *act = xin + a.in_dims * KF;             // [C][kMrF]
+    float *tmp = act + a.C * kMrF;                 // [C][kMrF]
+    for (int i = tid; i < a.in_dims * KF; i += kMrThreads) {
+        const int c = i / KF, f = i - c * KF;
+        xin[i] = t0 + f < Tp ? a.mel[((size_t)u * a.in_dims + c) * Tp + t0 + f] : 0.0f;
+    }
+    __syncthreads();
+    const int row = tid % a.C, fc = (tid / a.C) * FPT_C;
+    const bool live_c = tid < a.C * (kMrF / FPT_C);
+    const float *W = a.w;
+    // conv_in + BN + ReLU: input index (c, tap) reads frame f + tap of the tile
+    {
+        float acc[FPT_C];
+        if (live_c) {
+#pragma unroll
+            for (int i = 0; i < FPT_C; ++i) acc[i] = W[(size_t)a.in_dims * a.K * a.C + row];
+            const int Kin = a.in_dims * a.K;
+            int k = 0;
+            for (; k + 16 <= Kin; k += 16) {
+                float w[16];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) w[j] = W[(size_t)(k + j) * a.C + row];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const int c = (k + j) / a.K, tap = (k + j) - c * a.K;
+                    const float *x = xin + c * KF + tap + fc;
+#pragma unroll
+                    for (int i = 0; i < FPT_C; ++i) acc[i] = fmaf(w[j], x[i], acc[i]);
+                }
+            }
+            for (; k < Kin; ++k) {
+                const int c = k / a.K, tap = k - c * a.K;
+                const float w = W[(size_t)k * a.C + row];
+                const float *x = xin + c * KF + tap + fc;
+#pragma unroll
+                for (int i = 0; i < FPT_C; ++i) acc[i] = fmaf(w, x[i], acc[i]);
+            }
+#pragma unroll
+            for (int i = 0; i < FPT_C; ++i) act[row * kMrF + fc + i] = fmaxf(acc[i], 0.0f);
+        }
+        W += (size_t)a.in_dims * a.K * a.C + a.C;
+    }
+    __syncthreads();
+    for (int blk = 0; blk < a.blocks; ++blk) {
+        float acc[FPT_C];
+        if (live_c) {
+            mr_layer<FPT_C>(W, W + (size_t)a.C * a.C, act, a.C, a.C, acc, row, fc);
+#pragma unroll
+            for (int i = 0; i < FPT_C; ++i) tmp[row * kMrF + fc + i] = fmaxf(acc[i], 0.0f);
+        }
+        W += (size_t)a.C * a.C + a.C;
+        __syncthreads();
+        if (live_c) {
+            mr_layer<FPT_C>(W, W + (size_t)a.C * a.C, tmp, a.C, a.C, acc, row, fc);
+#pragma unroll
+            for (int i = 0; i < FPT_C; ++i) act[row * kMrF + fc + i] = acc[i] + act[row * kMrF + fc + i];
+        }
+        W += (size_t)a.C * a.C + a.C;
+        __syncthreads();
+    }
+    // conv_out (bias) → aux
+    const int orow = tid % a.R, fr = (tid / a.R) * FPT_R;
+    if (tid < a.R * (kMrF / FPT_R)) {
+        float acc[FPT_R];
+        mr_layer<FPT_R>(W, W + (size_t)a.C * a.R, act, a.C, a.R, acc, orow, fr);
+#pragma unroll
+        for (int i = 0; i < FPT_R; ++i)
+            if (t0 + fr + i < a.T) a.aux[((size_t)u * a.R + orow) * a.T + t0 + fr + i] = acc[i];
+    }
+}
+
+// frames per thread for Cout outputs over kMrF frames and 256 threads (0: unsupported)
+inline int mr_fpt(int cout) {
+    if (cout < 1 || cout > kMrThreads) return 0;
+    const int out = cout * kMrF;
+    if (out <= kMrThreads) return 1;
+    if (out % kMrThreads) return 0;
+    const int f = out / kMrThreads;
+    return kMrF % f == 0 ? f : 0;
+}
+
+}  // namespace wrnn
+
+extern "C" {
+
+int wrnn_melresnet_floats(const wrnn_melresnet_cfg *cfg) {
+    if (!cfg || cfg->in_dims < 1 || cfg->compute_dims < 1 || cfg->res_out_dims < 1 || cfg->res_blocks < 0 ||
+        cfg->pad < 0)
+        return -1;
+    const long long C = cfg->compute_dims, R = cfg->res_out_dims, K = 2LL * cfg->pad + 1;
+    return (int)(cfg->in_dims * K * C + C + cfg->res_blocks * 2 * (C * C + C) + C * R + R);
+}
+
+int wrnn_melresnet(const wrnn_melresnet_cfg *cfg, const float *packed, const float *mel, int U, int T, float *aux,
+                   void *stream) {
+    using namespace wrnn;
+    if (wrnn_melresnet_floats(cfg) < 0 || !packed || !mel || !aux || U < 1 || T < 1) return WRNN_EINVAL;
+    const int fc = mr_fpt(cfg->compute_dims), fr = mr_fpt(cfg->res_out_dims);
+    const int K = 2 * cfg->pad + 1;
+    const size_t lds = ((size_t)cfg->in_dims * (kMrF + K - 1) + 2 * (size_t)cfg->compute_dims * kMrF) * 4;
+    if (!fc || !fr || lds > 64 * 1024) return WRNN_EUNSUPPORTED;
+    MrArgs a{packed, mel, aux, U, T, cfg->in_dims, cfg->compute_dims, cfg->res_out_dims, cfg->res_blocks, K};
+    const dim3 grid((T + kMrF - 1) / kMrF, U);
+    hipStream_t st = (hipStream_t)stream;
+#define WRNN_MR_CASE(A, B)                                                                          \
+    if (fc == A && fr == B) {                                                                       \
+        hipLaunchKernelGGL((melresnet_kernel<A, B>), grid, dim3(kMrThreads), lds, st, a);           \
+        return hipGetLastError() == hipSuccess ? WRNN_OK : WRNN_EHIP;                              \
+    }
+    WRNN_MR_CASE(8, 8) WRNN_MR_CASE(1, 1) WRNN_MR_CASE(2, 2) WRNN_MR_CASE(4, 4) WRNN_MR_CASE(16, 16)
+    WRNN_MR_CASE(8, 1) WRNN_MR_CASE(8, 2) WRNN_MR_CASE(8, 4) WRNN_MR_CASE(8, 16)
+    WRNN_MR_CASE(1, 8) WRNN_MR_CASE(2, 8) WRNN_MR_CASE(4, 8) WRNN_MR_CASE(16, 8)
+#undef WRNN_MR_CASE
+    return WRNN_EUNSUPPORTED;
+}
+
+}  // extern "C"

@@ -16,6 +16,7 @@ crosses to the host.
 """
 from __future__ import annotations
 
+import os
 import time
 from pathlib import Path
 from typing import List, Optional, Sequence, Union
@@ -25,6 +26,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import _native as nat
 from . import condition, dsp
 from .loop import LOOP_KEYS, FatchordLoop, noise_width
 
@@ -203,10 +205,29 @@ class WaveRNN(nn.Module):
             mels = torch.as_tensor(mels, device=device).to(torch.float32)
             wave_len = (mels.size(-1) - 1) * self.hop_length
             padded = self.pad_tensor(mels.transpose(1, 2), pad=self.pad, side='both').transpose(1, 2)
-            aux = self.upsample.resnet(padded)
+            aux = self._melresnet(padded)
         finally:
             self.train(was_training)
         return mels.contiguous(), aux.contiguous().float(), wave_len
+
+    def _melresnet(self, padded):
+        """MelResNet(padded) through the fused HIP kernel (wrnn_melresnet: every BatchNorm folded,
+        one launch); the torch module (MIOpen) only for channel counts the kernel does not cover."""
+        res = self.upsample.resnet
+        if os.environ.get("WRNN_TORCH_MELRESNET"):   # A/B: the torch module (MIOpen)
+            return res(padded)
+        key = tuple((p.data_ptr(), p._version) for p in res.parameters()) + \
+            tuple((b.data_ptr(), b._version) for b in res.buffers())
+        if getattr(self, "_mr_key", None) != key:
+            self._mr_cfg = condition.melresnet_cfg(res)
+            self._mr_packed = condition.melresnet_pack(res)
+            self._mr_key = key
+        try:
+            return condition.melresnet(self._mr_cfg, self._mr_packed, padded)
+        except nat.WrnnError as e:
+            if e.code != -6:   # WRNN_EUNSUPPORTED
+                raise
+            return res(padded)
 
     @torch.no_grad()
     def conditioning(self, mels, batched, target, overlap):
