@@ -4,8 +4,9 @@
 * `upsample_pack` turns the generate() mel input and the MelResNet output into the loop's
   time-major conditioning records in one HIP kernel: pad_tensor, the UpsampleNetwork's
   Stretch2d/Conv2d chain and crop, resnet_stretch, fold_with_overlap and the cat/transpose
-  (models/fatchord_version.py:82-89, :183-205, :293-340).  MelResNet itself stays a torch
-  module (MIOpen convolutions).
+  (models/fatchord_version.py:82-89, :183-205, :293-340).
+* `melresnet` runs the UpsampleNetwork's MelResNet (:13-48) as one HIP kernel on weights packed by
+  `melresnet_pack` (every BatchNorm folded into its conv; csrc/melresnet.hip).
 * `postprocess` is generate()'s float64 tail on the device: decode_mu_law (utils/dsp.py:98-103),
   xfade_and_unfold (:342-405), trim and the 20·hop linear fade-out (:243-258).
 

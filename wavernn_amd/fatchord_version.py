@@ -232,8 +232,8 @@ class WaveRNN(nn.Module):
     @torch.no_grad()
     def conditioning(self, mels, batched, target, overlap):
         """pad → upsample → (fold) → time-major [L][B][feat + 4·aux] (fatchord_version.py:183-190).
-        MelResNet runs as torch modules in eval mode (BatchNorm running statistics) like
-        generate(); everything after it is the `wrnn_upsample_pack` HIP kernel."""
+        MelResNet in eval form (BatchNorm running statistics, folded) is the `wrnn_melresnet` HIP
+        kernel; everything after it the `wrnn_upsample_pack` HIP kernel."""
         mels, aux, wave_len = self.frames(mels)
         cond = condition.upsample_pack(self._upsample_spec(), mels, aux, target if batched else 0, overlap)
         return cond, wave_len
