@@ -11,12 +11,14 @@
 //   conv_in  Wt[(c·K + tap)][C], bias[C]          (K = 2·pad + 1, c < in_dims)
 //   block i  Wt1[C][C], b1[C], Wt2[C][C], b2[C]
 //   conv_out Wt[C][R], bias[R]
-// Layer outputs: thread t owns output row t % Cout and kMrFpt = Cout·kMrF / 256 consecutive frames
-// ((t / Cout)·kMrFpt ...): per input k one weight load and kMrFpt / 4 float4 LDS reads (a wave's
-// lanes share the frames: broadcast).
+// Layer outputs: thread t owns output row t % Cout and Cout·kMrF / 256 consecutive frames; each
+// layer's weights pass through LDS 128 input channels at a time (every thread loading its share at
+// once: one round trip per chunk), read back conflict-free (a wave's lanes: consecutive outputs)
+// while the activations are LDS broadcasts (a wave's lanes share the frames).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <string>
 
 #include "wavernn_amd.h"
@@ -26,29 +28,42 @@ namespace wrnn {
 constexpr int kMrThreads = 256;
 constexpr int kMrF = 16;          // frames per workgroup
 
-// (weights from L2: 16 loads issued ahead of their FMAs, so a layer pays ≈ Kin / 16 round trips)
-template <int FPT>
-__device__ __forceinline__ void mr_layer(const float *__restrict__ Wt, const float *__restrict__ bias,
-                                         const float *in, int Kin, int Cout, float (&acc)[FPT], int row, int f0) {
-#pragma unroll
-    for (int i = 0; i < FPT; ++i) acc[i] = bias[row];
-    int k = 0;
-    for (; k + 16 <= Kin; k += 16) {
-        float w[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) w[j] = Wt[(size_t)(k + j) * Cout + row];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const float *x = in + (k + j) * kMrF + f0;
-#pragma unroll
-            for (int i = 0; i < FPT; ++i) acc[i] = fmaf(w[j], x[i], acc[i]);
-        }
+constexpr int kMrKc = 128;        // weight rows (input channels) staged through LDS at a time
+
+// Rows [k0, k0 + kc) of a k-major weight matrix (Cout wide) → LDS, every thread loading its share
+// at once (one round trip per chunk instead of one per input channel)
+__device__ __forceinline__ void mr_stage(const float *__restrict__ Wt, int k0, int kc, int Cout, float *wbuf) {
+    __syncthreads();
+    const float *src = Wt + (size_t)k0 * Cout;
+    const int n = kc * Cout;
+    if ((n & 3) == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+        for (int i = 4 * threadIdx.x; i < n; i += 4 * kMrThreads)
+            *reinterpret_cast<float4 *>(wbuf + i) = *reinterpret_cast<const float4 *>(src + i);
+    } else {
+        for (int i = threadIdx.x; i < n; i += kMrThreads) wbuf[i] = src[i];
     }
-    for (; k < Kin; ++k) {
-        const float w = Wt[(size_t)k * Cout + row];
-        const float *x = in + k * kMrF + f0;
+    __syncthreads();
+}
+
+// acc = bias + W·in over the thread's frames, the weights staged through LDS chunk by chunk.
+// `live`: this thread owns outputs (all threads stage).  X(k, i): input k at the thread's frame i.
+template <int FPT, typename X>
+__device__ __forceinline__ void mr_layer(const float *__restrict__ Wt, const float *__restrict__ bias, int Kin,
+                                         int Cout, float *wbuf, bool live, int row, float (&acc)[FPT], X x) {
+    if (live) {
 #pragma unroll
-        for (int i = 0; i < FPT; ++i) acc[i] = fmaf(w, x[i], acc[i]);
+        for (int i = 0; i < FPT; ++i) acc[i] = bias[row];
+    }
+    for (int k0 = 0; k0 < Kin; k0 += kMrKc) {
+        const int kc = min(kMrKc, Kin - k0);
+        mr_stage(Wt, k0, kc, Cout, wbuf);
+        if (live) {
+            for (int k = 0; k < kc; ++k) {
+                const float w = wbuf[k * Cout + row];
+#pragma unroll
+                for (int i = 0; i < FPT; ++i) acc[i] = fmaf(w, x(k0 + k, i), acc[i]);
+            }
+        }
     }
 }
 
@@ -64,75 +79,57 @@ __global__ __launch_bounds__(kMrThreads) void melresnet_kernel(MrArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int u = blockIdx.y, t0 = blockIdx.x * kMrF, tid = threadIdx.x;
     const int Tp = a.T + a.K - 1, KF = kMrF + a.K - 1;
-    float *xin = lds;                              // [in_dims][kMrF + K − 1]  the mel tile (+ halo)
-    float *act = xin + a.in_dims * KF;             // [C][kMrF]
+    float *act = lds;                              // [C][kMrF]
     float *tmp = act + a.C * kMrF;                 // [C][kMrF]
+    float *wbuf = tmp + a.C * kMrF;                // [kMrKc][max(C, R)]
+    float *xin = wbuf + kMrKc * max(a.C, a.R);     // [in_dims][kMrF + K − 1]  the mel tile (+ halo)
     for (int i = tid; i < a.in_dims * KF; i += kMrThreads) {
         const int c = i / KF, f = i - c * KF;
         xin[i] = t0 + f < Tp ? a.mel[((size_t)u * a.in_dims + c) * Tp + t0 + f] : 0.0f;
     }
-    __syncthreads();
     const int row = tid % a.C, fc = (tid / a.C) * FPT_C;
     const bool live_c = tid < a.C * (kMrF / FPT_C);
     const float *W = a.w;
-    // conv_in + BN + ReLU: input index (c, tap) reads frame f + tap of the tile
-    {
-        float acc[FPT_C];
-        if (live_c) {
+    float acc[FPT_C];
+    // conv_in + BN + ReLU: input k = c·K + tap reads frame f + tap of the tile
+    const int Kin0 = a.in_dims * a.K;
+    mr_layer<FPT_C>(W, W + (size_t)Kin0 * a.C, Kin0, a.C, wbuf, live_c, row, acc, [&](int k, int i) {
+        const int c = k / a.K;
+        return xin[c * KF + (k - c * a.K) + fc + i];
+    });
+    if (live_c) {
 #pragma unroll
-            for (int i = 0; i < FPT_C; ++i) acc[i] = W[(size_t)a.in_dims * a.K * a.C + row];
-            const int Kin = a.in_dims * a.K;
-            int k = 0;
-            for (; k + 16 <= Kin; k += 16) {
-                float w[16];
-#pragma unroll
-                for (int j = 0; j < 16; ++j) w[j] = W[(size_t)(k + j) * a.C + row];
-#pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    const int c = (k + j) / a.K, tap = (k + j) - c * a.K;
-                    const float *x = xin + c * KF + tap + fc;
-#pragma unroll
-                    for (int i = 0; i < FPT_C; ++i) acc[i] = fmaf(w[j], x[i], acc[i]);
-                }
-            }
-            for (; k < Kin; ++k) {
-                const int c = k / a.K, tap = k - c * a.K;
-                const float w = W[(size_t)k * a.C + row];
-                const float *x = xin + c * KF + tap + fc;
-#pragma unroll
-                for (int i = 0; i < FPT_C; ++i) acc[i] = fmaf(w, x[i], acc[i]);
-            }
-#pragma unroll
-            for (int i = 0; i < FPT_C; ++i) act[row * kMrF + fc + i] = fmaxf(acc[i], 0.0f);
-        }
-        W += (size_t)a.in_dims * a.K * a.C + a.C;
+        for (int i = 0; i < FPT_C; ++i) act[row * kMrF + fc + i] = fmaxf(acc[i], 0.0f);
     }
-    __syncthreads();
+    W += (size_t)Kin0 * a.C + a.C;
     for (int blk = 0; blk < a.blocks; ++blk) {
-        float acc[FPT_C];
+        // (mr_stage's leading barrier orders these layers' LDS reads after the previous writes)
+        mr_layer<FPT_C>(W, W + (size_t)a.C * a.C, a.C, a.C, wbuf, live_c, row, acc,
+                        [&](int k, int i) { return act[k * kMrF + fc + i]; });
         if (live_c) {
-            mr_layer<FPT_C>(W, W + (size_t)a.C * a.C, act, a.C, a.C, acc, row, fc);
 #pragma unroll
             for (int i = 0; i < FPT_C; ++i) tmp[row * kMrF + fc + i] = fmaxf(acc[i], 0.0f);
         }
         W += (size_t)a.C * a.C + a.C;
-        __syncthreads();
+        mr_layer<FPT_C>(W, W + (size_t)a.C * a.C, a.C, a.C, wbuf, live_c, row, acc,
+                        [&](int k, int i) { return tmp[k * kMrF + fc + i]; });
+        __syncthreads();   // every thread has read act (conv1 above) before it is overwritten
         if (live_c) {
-            mr_layer<FPT_C>(W, W + (size_t)a.C * a.C, tmp, a.C, a.C, acc, row, fc);
 #pragma unroll
             for (int i = 0; i < FPT_C; ++i) act[row * kMrF + fc + i] = acc[i] + act[row * kMrF + fc + i];
         }
         W += (size_t)a.C * a.C + a.C;
-        __syncthreads();
     }
     // conv_out (bias) → aux
     const int orow = tid % a.R, fr = (tid / a.R) * FPT_R;
-    if (tid < a.R * (kMrF / FPT_R)) {
-        float acc[FPT_R];
-        mr_layer<FPT_R>(W, W + (size_t)a.C * a.R, act, a.C, a.R, acc, orow, fr);
+    const bool live_r = tid < a.R * (kMrF / FPT_R);
+    float acc_r[FPT_R];
+    mr_layer<FPT_R>(W, W + (size_t)a.C * a.R, a.C, a.R, wbuf, live_r, orow, acc_r,
+                    [&](int k, int i) { return act[k * kMrF + fr + i]; });
+    if (live_r) {
 #pragma unroll
         for (int i = 0; i < FPT_R; ++i)
-            if (t0 + fr + i < a.T) a.aux[((size_t)u * a.R + orow) * a.T + t0 + fr + i] = acc[i];
+            if (t0 + fr + i < a.T) a.aux[((size_t)u * a.R + orow) * a.T + t0 + fr + i] = acc_r[i];
     }
 }
 
@@ -164,13 +161,18 @@ int wrnn_melresnet(const wrnn_melresnet_cfg *cfg, const float *packed, const flo
     if (wrnn_melresnet_floats(cfg) < 0 || !packed || !mel || !aux || U < 1 || T < 1) return WRNN_EINVAL;
     const int fc = mr_fpt(cfg->compute_dims), fr = mr_fpt(cfg->res_out_dims);
     const int K = 2 * cfg->pad + 1;
-    const size_t lds = ((size_t)cfg->in_dims * (kMrF + K - 1) + 2 * (size_t)cfg->compute_dims * kMrF) * 4;
-    if (!fc || !fr || lds > 64 * 1024) return WRNN_EUNSUPPORTED;
+    const size_t lds = ((size_t)cfg->in_dims * (kMrF + K - 1) + 2 * (size_t)cfg->compute_dims * kMrF +
+                        (size_t)kMrKc * std::max(cfg->compute_dims, cfg->res_out_dims)) * 4;
+    if (!fc || !fr || lds > 160 * 1024) return WRNN_EUNSUPPORTED;
     MrArgs a{packed, mel, aux, U, T, cfg->in_dims, cfg->compute_dims, cfg->res_out_dims, cfg->res_blocks, K};
     const dim3 grid((T + kMrF - 1) / kMrF, U);
     hipStream_t st = (hipStream_t)stream;
 #define WRNN_MR_CASE(A, B)                                                                          \
     if (fc == A && fr == B) {                                                                       \
+        if (lds > 64 * 1024 &&                                                                      \
+            hipFuncSetAttribute((const void *)melresnet_kernel<A, B>,                               \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) \
+            return WRNN_EHIP;                                                                       \
         hipLaunchKernelGGL((melresnet_kernel<A, B>), grid, dim3(kMrThreads), lds, st, a);           \
         return hipGetLastError() == hipSuccess ? WRNN_OK : WRNN_EHIP;                              \
     }
