@@ -158,17 +158,13 @@ def _timed(fn):
 
 
 def other_configs(dev, warm: bool = True, cpu_steps: int = 0, threads: int = 1) -> dict:
-    """BASELINE configs 1 and 3-5 on one GPU, every one through the drop-in API (upsample and
+    """BASELINE configs 1 and 3 on this rank's GPU, through the drop-in API (upsample and
     post-processing included), synthetic inputs, random weights of each architecture:
       1: RAW 9-bit generate(), 1 s unbatched and 5 s fold-batched;
       3: MoL fold-batched generate() of one 60 s utterance (115 folds x 12 100 steps);
-      4: rnn 896 with 95 % 4x4 block-sparse GRU weights, 8 utterances of 5 s in one
-         generate_many() launch (the per-GPU share of 64 over 8 GPUs);
-      5: deepmind dual softmax, 32 utterances of 1 s at 16 kHz in one generate(batch=32);
     plus the headline architecture serving 8 utterances at once (generate_many, one per XCD).
+    Configs 4 and 5 are utterance batches sharded over the ranks: `sharded_configs`.
     `warm` = an untimed first call per config (the PMC child runs each config once)."""
-    from wavernn_amd.deepmind_version import WaveRNN as DeepmindWaveRNN
-    from wavernn_amd.pruning import prune_state
     res = {}
     sr = 22050
     # config 2 architecture, 8 concurrent unbatched utterances (per-stream latency unchanged)
@@ -241,62 +237,159 @@ def other_configs(dev, warm: bool = True, cpu_steps: int = 0, threads: int = 1) 
                       f"upsample + fold of the whole 60 s mel, {n} of 12100 loop steps x 115 folds, float64 post of "
                       f"the whole utterance; value = loop-step samples / (loop time + {n / 12100:.3f} x pre/post)"}
     del model
-    # config 4: 8 utterances of 5 s per GPU through generate_many (upsample included)
-    d4 = syn.SPARSE896_MOL
-    model = _mol_model(d4, dev, prune_state(syn.make_fatchord_state(d4, 0), 0.95))
-    mels = [torch.from_numpy(syn.make_mel(d4.feat_dims, T5, 60 + i))[None] for i in range(8)]
-    if warm:
-        model.generate_many(mels, None, False, 11000, 550, True, seed=1)
-    outs, dt = _timed(lambda: model.generate_many(mels, None, False, 11000, 550, True, seed=2))
-    h = model.loop_handle()
-    ms, L4 = h.elapsed_ms(), T5 * d4.hop_length
+    return res
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+
+
+def _timed_ranks(fn, world: int, dev):
+    """fn() between barrier + synchronize pairs on every rank; (result, max elapsed over ranks)."""
+    _sync(dev)
+    if world > 1:
+        dist.barrier()
+    t = time.perf_counter()
+    out = fn()
+    _sync(dev)
+    if world > 1:
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    return out, float(el[0])
+
+
+def _max_over_ranks(x: float, world: int, dev) -> float:
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0])
+
+
+UTT4_PER_RANK, UTT5_PER_RANK, L5 = 8, 32, 16000
+
+
+def _config4_record(outs, dt, ms, world, L4, info) -> dict:
+    n4 = UTT4_PER_RANK * world
     n = sum(o.shape[0] for o in outs)
-    res["config4_sparse896_8utt"] = {"samples_per_s": n / dt, "rtf": n / dt / sr, "rows": 8, "loop_steps": L4,
-                                     "device_ms": ms, "wall_s": dt, "us_per_loop_step": ms * 1e3 / L4,
-                                     "loop_samples_per_s": 8 * L4 / ms * 1e3,
-                                     "sparse_blocks_per_gate_row": h.info["sparse_blocks"],
-                                     "kernel_path": h.info["last_path"],
-                                     "roofline": hbm_roofline(SPARSE896_BYTES_PER_STEP + 8 * COND_BYTES_PER_ROW_STEP,
-                                                              ms * 1e3 / L4,
-                                                              "SURVEY.md 8(d) bytes per step (sparse weights + int16 "
-                                                              "block indices once + 836 B per row) / step time; "
-                                                              "blocks resident, latency-bound"),
-                                     "note": "WaveRNN(rnn_dims=896).generate_many of 8 synthetic 5 s mels (the per-GPU "
-                                             "share of 64 utterances over 8 GPUs) in ONE launch of fatchord_xcds_kernel "
-                                             "(path 6, one utterance per XCD); samples_per_s over the whole call "
-                                             "(MelResNet + upsample, loop incl. the conditioning-terms GEMM, post)"}
-    del model
-    # config 5: 32 utterances of 1 s at 16 kHz per GPU through the deepmind drop-in
-    dm = syn.DEFAULT_DM
-    B5, L5 = 32, 16000
-    state5 = syn.make_deepmind_state(dm, 0)
-    model = DeepmindWaveRNN(**dm.ctor_kwargs()).to(dev)
-    model.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in state5.items()})
+    return {
+        "samples_per_s": n / dt, "rtf": n / dt / 22050, "rtf_per_gpu": n / dt / 22050 / world,
+        "utterances": n4, "n_gpus": world, "rows_per_gpu": UTT4_PER_RANK, "loop_steps": L4,
+        "device_ms": ms, "wall_s": dt, "us_per_loop_step": ms * 1e3 / L4,
+        "loop_samples_per_s": n4 * L4 / ms * 1e3,
+        "sparse_blocks_per_gate_row": info["sparse_blocks"], "kernel_path": info["last_path"],
+        "roofline": hbm_roofline(SPARSE896_BYTES_PER_STEP + UTT4_PER_RANK * COND_BYTES_PER_ROW_STEP, ms * 1e3 / L4,
+                                 "SURVEY.md 8(d) bytes per step (sparse weights + int16 block indices once + "
+                                 "836 B per row) / step time of the slowest rank's launch; blocks resident, "
+                                 "latency-bound"),
+        "note": f"{n4} synthetic 5 s mels through sharding.generate_sharded over {world} GPU(s): each rank runs "
+                "its 8 as ONE launch of fatchord_xcds_kernel (path 6, one utterance per XCD), the audio is "
+                "all-gathered to rank 0; samples_per_s = all utterances' samples / max-over-ranks wall time "
+                "(MelResNet + upsample, loop incl. the conditioning terms, post, gather)"}
+
+
+def _config5_record(outs, dt, ms, world, info) -> dict:
+    n5 = UTT5_PER_RANK * world
+    n = sum(o.size for o in outs)
+    return {
+        "samples_per_s": n / dt, "rtf": n / dt / 16000.0, "rtf_per_gpu": n / dt / 16000.0 / world,
+        "utterances": n5, "n_gpus": world, "rows_per_gpu": UTT5_PER_RANK, "loop_steps": L5,
+        "device_ms": ms, "wall_s": dt, "us_per_loop_step": ms * 1e3 / L5,
+        "loop_samples_per_s": n5 * L5 / ms * 1e3, "kernel_path": info["last_path"],
+        "roofline": hbm_roofline(DM_BYTES_PER_STEP + 4 * UTT5_PER_RANK, ms * 1e3 / L5,
+                                 "SURVEY.md 8(d) bytes per step (weights once + 4 B per row) / step time of the "
+                                 "slowest rank's launch; weights resident in each XCD's registers + LDS (path 8 = "
+                                 "deepmind_xcd_kernel, 4 rows per XCD), hand-off-latency-bound"),
+        "note": f"{n5} utterances of 16000 samples through sharding.generate_sharded_deepmind over {world} GPU(s) "
+                "(32 rows per rank in one generate(batch=32) launch, outputs all-gathered to rank 0); rate over "
+                "the max-over-ranks wall time incl. the label D2H and the gather"}
+
+
+def sharded_configs(dev, world: int, rank: int, warm: bool = True, cpu_steps: int = 0, threads: int = 1,
+                    stub: bool = False) -> dict:
+    """BASELINE configs 4 and 5 as stated — utterance batches sharded over the GPUs of the node
+    (`wavernn_amd.sharding`: contiguous blocks, one persistent launch per rank, the finished audio
+    all-gathered to rank 0 over RCCL) — at 8 and 32 utterances PER RANK (weak scaling: at N = 8
+    that is BASELINE's 64 and 256):
+      4: rnn 896 with 95 % 4x4 block-sparse GRU weights, 5 s MoL utterances, unbatched
+         (gen_wavernn.py:11-35 vocodes a list; generate_sharded);
+      5: deepmind dual softmax, 1 s at 16 kHz (deepmind_version.py:75-165; generate_sharded_deepmind).
+    Each leg is timed between barriers on every rank, elapsed = max over ranks, samples = all
+    ranks'.  rank 0 returns the records (cpu_baseline beside each, timed after the legs).
+    `stub`: no GPU — the same sharding, gather, timing and records around a stand-in generation
+    (tests of the N > 1 contract on gloo ranks)."""
+    from wavernn_amd import sharding
+    res = {}
+    d4 = syn.SPARSE896_MOL
+    T5 = syn.frames_for_seconds(5.0, d4.sample_rate, d4.hop_length)
+    L4 = T5 * d4.hop_length
+    n4, n5 = UTT4_PER_RANK * world, UTT5_PER_RANK * world
+    mels = [syn.make_mel(d4.feat_dims, T5, 60 + i)[None] for i in range(n4)]
+    # ---- config 4
+    if stub:
+        model, state4 = None, None
+        stub4 = lambda ii, ms, r0: [np.zeros((T5 - 1) * d4.hop_length) for _ in ii]   # noqa: E731
+        one_row = type("OneRow", (), {"rows_of": staticmethod(lambda T, b, t, o: 1)})   # unbatched: 1 row each
+        run4 = lambda seed: sharding.generate_sharded(one_row, mels, False, 11000, 550, True,  # noqa: E731
+                                                      base_seed=seed, device=dev, generate_fn=stub4)
+    else:
+        from wavernn_amd.pruning import prune_state
+        state4 = prune_state(syn.make_fatchord_state(d4, 0), 0.95)
+        model = _mol_model(d4, dev, state4)
+        run4 = lambda seed: sharding.generate_sharded(model, mels, False, 11000, 550, True,  # noqa: E731
+                                                      base_seed=seed, device=dev)
     if warm:
-        model.generate(100, batch=B5, seed=1)
-    (out5, _, _), dt = _timed(lambda: model.generate(L5, batch=B5, seed=2))
-    h = model.loop_handle()
-    ms = h.elapsed_ms()
-    res["config5_deepmind_32utt"] = {"samples_per_s": out5.size / dt, "rtf": out5.size / dt / 16000.0, "rows": B5,
-                                     "loop_steps": L5, "device_ms": ms, "wall_s": dt, "us_per_loop_step": ms * 1e3 / L5,
-                                     "loop_samples_per_s": B5 * L5 / ms * 1e3,
-                                     "kernel_path": h.info["last_path"],
-                                     "roofline": hbm_roofline(DM_BYTES_PER_STEP + 4 * B5, ms * 1e3 / L5,
-                                                              "SURVEY.md 8(d) bytes per step (weights once + 4 B per "
-                                                              "row) / step time; weights resident in each XCD's "
-                                                              "registers + LDS (path 8 = deepmind_xcd_kernel, 4 rows "
-                                                              "per XCD), hand-off-latency-bound"),
-                                     "note": "deepmind WaveRNN.generate(16000, batch=32) (the per-GPU share of 256 "
-                                             "utterances over 8 GPUs), rate over the whole call incl. the label D2H"}
-    if cpu_steps > 0:
+        run4(1)
+    outs, dt = _timed_ranks(lambda: run4(2), world, dev)
+    info = {"sparse_blocks": 0, "last_path": 0} if stub else model.loop_handle().info
+    ms = _max_over_ranks(dt * 1e3 if stub else model.loop_handle().elapsed_ms(), world, dev)
+    if rank == 0:
+        res["config4_sparse896_8utt"] = _config4_record(outs, dt, ms, world, L4, info)
+    del model
+    # ---- config 5
+    dm = syn.DEFAULT_DM
+    if stub:
+        model, state5 = None, None
+        run5 = lambda seed, L=L5: sharding.generate_sharded_deepmind(  # noqa: E731
+            None, n5, L, base_seed=seed, device=dev, generate_fn=lambda ii, r0: [np.zeros(L) for _ in ii])
+    else:
+        from wavernn_amd.deepmind_version import WaveRNN as DeepmindWaveRNN
+        state5 = syn.make_deepmind_state(dm, 0)
+        model = DeepmindWaveRNN(**dm.ctor_kwargs()).to(dev)
+        model.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in state5.items()})
+        run5 = lambda seed, L=L5: sharding.generate_sharded_deepmind(model, n5, L, base_seed=seed,  # noqa: E731
+                                                                     device=dev)
+    if warm:
+        run5(1, 100)
+    outs5, dt = _timed_ranks(lambda: run5(2), world, dev)
+    info = {"last_path": 0} if stub else model.loop_handle().info
+    ms = _max_over_ranks(dt * 1e3 if stub else model.loop_handle().elapsed_ms(), world, dev)
+    if rank == 0:
+        res["config5_deepmind_32utt"] = _config5_record(outs5, dt, ms, world, info)
+    del model
+    if rank == 0 and cpu_steps > 0 and not stub:
         from oracle import torch_cpu
+        n = min(cpu_steps, L4)
+        noise = syn.make_noise("MOL", 1, n, d4.n_classes, 7)
+        r = torch_cpu.timed_generate(state4, d4, mels[0][0], False, 11000, 550, True, noise, loop_steps=n,
+                                     threads=threads)
+        t_cpu = r["loop_s"] + n / L4 * (r["pre_s"] + r["post_s"])
+        res["config4_sparse896_8utt"]["cpu_baseline"] = {
+            "value": n / t_cpu, "unit": "samples/s", "cores": r["threads"], "kind": "port",
+            "rtf": n / t_cpu / 22050, "loop_s": r["loop_s"], "pre_s": r["pre_s"], "post_s": r["post_s"],
+            "sample": f"PyTorch-CPU eager generate() of ONE 5 s utterance as the reference vocodes a list "
+                      f"(oracle/torch_cpu.py, {r['threads']} threads, the pruned weights as dense matrices): "
+                      f"{n} of {L4} loop steps + {n / L4:.3f} x the pre/post time"}
         n = min(cpu_steps, L5)
-        r = torch_cpu.timed_deepmind(state5, B5, syn.make_dm_noise(B5, n, dm.quantisation, 7), n, threads=threads)
+        r = torch_cpu.timed_deepmind(state5, UTT5_PER_RANK, syn.make_dm_noise(UTT5_PER_RANK, n, dm.quantisation, 7),
+                                     n, threads=threads)
         res["config5_deepmind_32utt"]["cpu_baseline"] = {
-            "value": n * B5 / r["loop_s"], "unit": "samples/s", "cores": r["threads"], "kind": "port",
-            "rtf": n * B5 / r["loop_s"] / 16000.0, "loop_s": r["loop_s"],
-            "sample": f"PyTorch-CPU eager deepmind loop (oracle/torch_cpu.deepmind_loop: the reference's per-step ops "
-                      f"for 32 rows at once, {r['threads']} threads), {n} of {L5} steps x 32 rows"}
+            "value": n * UTT5_PER_RANK / r["loop_s"], "unit": "samples/s", "cores": r["threads"], "kind": "port",
+            "rtf": n * UTT5_PER_RANK / r["loop_s"] / 16000.0, "loop_s": r["loop_s"],
+            "sample": f"PyTorch-CPU eager deepmind loop (oracle/torch_cpu.deepmind_loop: the reference's per-step "
+                      f"ops for 32 rows at once, {r['threads']} threads), {n} of {L5} steps x 32 rows"}
     return res
 
 
@@ -360,10 +453,12 @@ def stub_main(args, world, rank):
         return out.shape[0]
 
     elapsed, total = timed_steps(step, args.steps, args.warmup, world, dev)
+    sharded = sharded_configs(dev, world, rank, stub=True) if args.other_configs else {}
     if rank == 0:
         print(json.dumps({"metric": "stub", "value": total / elapsed, "unit": "samples/s", "n_gpus": world,
                           "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-                          "higher_is_better": True, "scaling": "weak", "data": "stub"}), flush=True)
+                          "higher_is_better": True, "scaling": "weak", "data": "stub",
+                          "other_configs": sharded}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -381,7 +476,8 @@ def main():
         args.steps, args.warmup, args.cpu_steps, args.fold_batched, args.pmc = 1, 0, 0, 0, 0
     # HBM traffic passes first, while this process has not touched the GPU (child processes)
     traffic, traffic_from = None, None
-    if args.pmc and world == 1 and not args.batched and args.mode == "MOL" and abs(args.seconds - 5.0) < 1e-9:
+    if args.pmc and rank == 0 and not args.batched and args.mode == "MOL" and abs(args.seconds - 5.0) < 1e-9:
+        # rank 0 only (its GPU = the children's cuda:0); the other ranks wait in the rendezvous
         live = pmc_live()
         if live is not None:
             traffic, traffic_from = live, "live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this run"
@@ -393,7 +489,9 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        # generous rendezvous timeout: rank 0 runs the PMC passes before it joins
+        from datetime import timedelta
+        dist.init_process_group("nccl", device_id=dev, timeout=timedelta(minutes=30))
 
     d = syn.DEFAULT_MOL if args.mode == "MOL" else syn.DEFAULT_RAW
     state = syn.make_fatchord_state(d, 0)
@@ -424,7 +522,15 @@ def main():
 
     if args.pmc_child:
         other_configs(dev, warm=False)
+        sharded_configs(dev, 1, 0, warm=False)
         return
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    # configs 4 / 5 as BASELINE states them: utterance batches sharded over all ranks (collective legs:
+    # every rank takes part; rank 0 gets the records, with their CPU baselines timed after the legs)
+    sharded = {}
+    if args.other_configs and args.mode == "MOL":
+        sharded = sharded_configs(dev, world, rank, cpu_steps=min(args.cpu_steps, 2000), threads=threads)
 
     if rank == 0:
         cond, _ = model.conditioning(mel, args.batched, target, overlap)
@@ -489,15 +595,16 @@ def main():
                         "hparams (10 folds in one launch) + conditioning-terms GEMM; rate over the whole "
                         "generate() wall time (upsample, loop, float64 post)",
             }
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
-        if args.other_configs and world == 1 and args.mode == "MOL":
+        if args.other_configs and args.mode == "MOL":
+            # single-GPU configs (1, 2 x 8 streams, 3) on rank 0's GPU, then the sharded legs' records
             rec["other_configs"] = other_configs(dev, cpu_steps=min(args.cpu_steps, 2000), threads=threads)
+            rec["other_configs"].update(sharded)
             for key, v in rec["other_configs"].items():
                 tr = (traffic or {}).get("other_configs", {}).get(key)
                 if tr is not None and "roofline" in v:
                     v["roofline"]["traffic_per_step"] = tr["bytes_per_step"]   # HBM bytes per loop step (PMC)
                     v["roofline"]["traffic_from"] = traffic_from
-        if args.cpu_steps > 0 and world == 1:
+        if args.cpu_steps > 0:
             # the reference's op sequence on this host's cores: PyTorch-CPU eager (oracle/torch_cpu.py),
             # whole pre/post + a bounded slice of the loop; and the C oracle on the same slice
             from oracle import oracle, torch_cpu

@@ -16,6 +16,9 @@ LONG_LOOP_CASES = ["loop_raw_1s", "loop_mol_1s"]
 SPARSE_LOOP_CASES = ["loop_mol_sparse896_b2", "loop_raw_sparse_b2"]
 DM_CASES = ["dm_b1", "dm_tiny_b1"]
 GEN_CASES = ["gen_mol_unbatched", "gen_raw_batched_mulaw", "gen_mol_batched", "gen_raw_tiny_unbatched"]
+# generate() at BASELINE sizes (configs 1, 2 unbatched and fold-batched, 3), written by the
+# reference itself; outputs stored strided / by row (make_golden.gen_case)
+GEN_BASELINE_CASES = ["gen_raw_1s_unbatched", "gen_mol_5s_unbatched", "gen_mol_5s_batched", "gen_mol_60s_batched"]
 
 # MoL parity tolerance per sample under noise injection: ~50-100x the
 # 5e-8..1.8e-7 the C restatement shows against the reference.

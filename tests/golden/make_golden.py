@@ -231,8 +231,15 @@ def dm_case(fv, name, d: syn.DeepmindDims, L: int, wseed=0, nseed=3):
 
 # ------------------------------------------------------------------------------ e2e cases
 def gen_case(fv, name, d: syn.FatchordDims, T: int, batched: bool, target: int, overlap: int,
-             mu_law: bool, wseed=0, mseed=1, nseed=3, cond_stride=25):
-    """Full reference generate(): pad → upsample → fold → loop → unfold/mu-law/fade."""
+             mu_law: bool, wseed=0, mseed=1, nseed=3, cond_stride=25, out_stride=1,
+             raw_rows=None, raw_stride=0):
+    """Full reference generate(): pad → upsample → fold → loop → unfold/mu-law/fade.
+
+    BASELINE-size cases keep the fixture small: `out_stride` stores every k-th output sample
+    (float64), `raw_rows` keeps the per-step loop outputs of those fold rows only, and
+    `raw_stride` > 0 additionally keeps every row at every raw_stride-th step.  Under MoL
+    feedback a divergence at one step changes every later sample of its row, so a strided
+    view still catches it."""
     state = syn.make_fatchord_state(d, wseed)
     mel = syn.make_mel(d.feat_dims, T, mseed)
     L = d.hop_length * T
@@ -261,13 +268,23 @@ def gen_case(fv, name, d: syn.FatchordDims, T: int, batched: bool, target: int, 
                mu_law=mu_law, B=B, Lf=Lf, wseed=wseed, mseed=mseed, nseed=nseed,
                dims=np.array(repr(d)), ref_seconds=dt, state_sha=syn.state_digest(state),
                mel_sha=syn.digest(mel), noise_sha=syn.digest(noise),
-               output=np.asarray(out, dtype=np.float64),
+               out_len=np.int64(len(out)), out_stride=np.int64(out_stride),
+               output=np.asarray(out, dtype=np.float64)[::out_stride].copy(),
+               out_sum=np.float64(np.asarray(out, dtype=np.float64).sum()),
                up_stride=cond_stride,
                up_mels=up_m[::cond_stride].copy(), up_aux=up_a[::cond_stride].copy(),
                up_mels_sum=np.float64(up_m.astype(np.float64).sum()),
                up_aux_sum=np.float64(up_a.astype(np.float64).sum()))
     raw = np.stack(inj.samples).T  # [B][Lf]
-    rec["raw"] = raw.astype(np.int16) if d.mode == "RAW" else raw.astype(np.float32)
+    raw = raw.astype(np.int16) if d.mode == "RAW" else raw.astype(np.float32)
+    if raw_rows is None:
+        rec["raw"] = raw
+    else:
+        rec["raw_rows"] = np.asarray(raw_rows, dtype=np.int64)
+        rec["raw"] = raw[list(raw_rows)].copy()
+        if raw_stride:
+            rec["raw_stride"] = np.int64(raw_stride)
+            rec["raw_strided"] = raw[:, ::raw_stride].copy()
     return rec
 
 
@@ -292,6 +309,17 @@ def cases():
         "gen_raw_batched_mulaw": ("gen", dict(d=R, T=30, batched=True, target=2000, overlap=200, mu_law=True)),
         "gen_mol_batched": ("gen", dict(d=M, T=30, batched=True, target=1500, overlap=300, mu_law=True)),
         "gen_raw_tiny_unbatched": ("gen", dict(d=syn.TINY_RAW, T=24, batched=False, target=1000, overlap=100, mu_law=False)),
+        # BASELINE sizes through the whole generate() (VERDICT r04 "do this" 1): config 1
+        # exactly (RAW 9-bit, 1 s, unbatched), config 2 unbatched (the headline) and in the
+        # reference's default fold-batched mode (hparams.py:58-60), config 3 (60 s, 115 folds)
+        "gen_raw_1s_unbatched": ("gen", dict(d=R, T=81, batched=False, target=11000, overlap=550, mu_law=True)),
+        "gen_mol_5s_unbatched": ("gen", dict(d=M, T=401, batched=False, target=11000, overlap=550,
+                                             mu_law=True, cond_stride=275, out_stride=4)),
+        "gen_mol_5s_batched": ("gen", dict(d=M, T=401, batched=True, target=11000, overlap=550,
+                                           mu_law=True, cond_stride=275, out_stride=4)),
+        "gen_mol_60s_batched": ("gen", dict(d=M, T=4811, batched=True, target=11000, overlap=550,
+                                            mu_law=True, cond_stride=2750, out_stride=32,
+                                            raw_rows=(0, 57, 114), raw_stride=50)),
         # deepmind_version dual softmax (config 5 model), batch 1 as the reference generates
         "dm_b1": ("dm", dict(d=syn.DEFAULT_DM, L=2000)),
         "dm_tiny_b1": ("dm", dict(d=syn.TINY_DM, L=3000)),

@@ -37,3 +37,21 @@ def test_bench_spawns_its_ranks(n):
 def test_bench_single_rank_default():
     rec = _run(["--steps", "2", "--warmup", "0", "--stub"])
     assert rec["n_gpus"] == 1
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_bench_sharded_legs(n):
+    """Configs 4 and 5 as BASELINE states them (utterances sharded over the ranks): at every N the
+    line carries both legs with the same keys; utterances = per-rank share x N, samples summed
+    over the ranks (gathered on rank 0) over the max-over-ranks time."""
+    rec = _run(["--gpus", str(n), "--steps", "1", "--warmup", "0", "--stub"])
+    oc = rec["other_configs"]
+    keys = {"samples_per_s", "rtf", "rtf_per_gpu", "utterances", "n_gpus", "rows_per_gpu", "loop_steps", "device_ms",
+            "wall_s", "us_per_loop_step", "loop_samples_per_s", "kernel_path", "roofline", "note"}
+    c4, c5 = oc["config4_sparse896_8utt"], oc["config5_deepmind_32utt"]
+    assert keys <= set(c4) and keys <= set(c5)
+    assert c4["utterances"] == 8 * n and c5["utterances"] == 32 * n and c4["n_gpus"] == c5["n_gpus"] == n
+    assert abs(c4["samples_per_s"] * c4["wall_s"] - 8 * n * 110000) <= 1e-6 * 8 * n * 110000
+    assert abs(c5["samples_per_s"] * c5["wall_s"] - 32 * n * 16000) <= 1e-6 * 32 * n * 16000
+    for c in (c4, c5):
+        assert set(c["roofline"]) >= {"bound", "achieved", "peak", "unit", "frac"}

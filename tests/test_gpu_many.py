@@ -3,9 +3,9 @@
 * `WaveRNN.generate_many(mels)` runs several utterances (or all their folds) as the rows of ONE
   loop launch; under Philox each utterance equals its own `generate(mel, row_offset=<first row>)`
   (row-keyed draws, the same kernel) within the MoL tolerance used between launches of different
-  shapes (2·MOL_TOL): the library GEMMs around the loop (MelResNet on MIOpen for equal-length
-  mels batched together, the rocBLAS terms GEMM over all rows) pick their tiling by shape, so the
-  conditioning terms may differ in the last bit; the deepmind rows (no conditioning) and RAW
+  shapes (2·MOL_TOL): the launch shape picks the loop kernel (one-row XCD kernel up to 8 MoL rows,
+  the many-row one from 9) and the rocBLAS terms GEMM over all utterances' frames picks its tiling
+  by shape, so the conditioning terms may differ in the last bit; the deepmind rows (no conditioning) and RAW
   labels are compared exactly.
 * Config 4's shape: 8 utterances of the rnn-896 block-sparse model in one launch of the sparse
   XCD kernel vs 8 separate calls.  Config 5's: 32 deepmind rows vs 32 single-row calls.

@@ -49,7 +49,7 @@ def _run(B, L, seed, monkeypatch, terms_mb=None):
     return err
 
 
-@pytest.mark.parametrize("B", [1, 2, 5, 8, 10, 13, 32, 33, 57, 115, 128])
+@pytest.mark.parametrize("B", [1, 2, 5, 8, 10, 13, 32, 33, 57, 80, 115, 128])
 def test_xcdm_vs_oracle(B, monkeypatch):
     err = _run(B, 240, 700 + B, monkeypatch)
     assert err.max() <= gf.MOL_TOL, f"max |Δ| {err.max()} at (row, step) {np.unravel_index(err.argmax(), err.shape)}"

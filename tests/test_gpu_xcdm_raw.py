@@ -51,7 +51,7 @@ def test_raw_xcdm_vs_reference_fixture(name, monkeypatch):
     _check(out, lab, x.astype(np.float32), labels)
 
 
-@pytest.mark.parametrize("B", [2, 8, 10, 33, 57, 128])
+@pytest.mark.parametrize("B", [2, 8, 10, 33, 57, 80, 128])
 def test_raw_xcdm_vs_oracle(B, monkeypatch):
     """One quad per XCD (B <= 32: every workgroup samples every row), the two-level sampler and
     the 16x16x4 form (B > 32), ragged XCDs."""

@@ -82,3 +82,34 @@ def test_long_oracle_fixtures_regenerate(name):
     np.testing.assert_array_equal(out, fx["out_full"][:, :n])
     sub = int(fx["sub"])
     np.testing.assert_array_equal(fx["out_sub"][rows, :n // sub], fx["out_full"][:, ::sub][:, :n // sub])
+
+
+@pytest.mark.parametrize("name", gf.GEN_BASELINE_CASES)
+def test_baseline_generate_fixture_pins_oracle(name):
+    """The BASELINE-size generate() fixtures (the reference run at configs 1, 2 and 3): their
+    inputs regenerate from the seeds (SHA-256 checked), the oracle's upsample matches the
+    reference's stored upsampled conditioning, and the oracle loop on that conditioning
+    reproduces the reference's first 300 steps of the stored rows (the GPU test then checks
+    the shipped entry over the whole length)."""
+    fx = gf.load(name)
+    d, state, mel, noise = gf.gen_inputs(fx)
+    mp = orc.pad_tensor(mel.T[None], d.pad)[0].T
+    m, a = orc.upsample(mp, state, d.upsample_factors, d.res_blocks, d.pad)
+    s = int(fx["up_stride"])
+    assert np.abs(m[::s] - fx["up_mels"]).max() < 1e-5
+    assert np.abs(a[::s] - fx["up_aux"]).max() < 1e-5
+    n = 300
+    batched, target, overlap = bool(fx["batched"]), int(fx["target"]), int(fx["overlap"])
+    if batched:
+        m = orc.fold_with_overlap(m[None], target, overlap)
+        a = orc.fold_with_overlap(a[None], target, overlap)
+    else:
+        m, a = m[None], a[None]
+    rows = fx["raw_rows"] if "raw_rows" in fx else np.arange(m.shape[0])
+    assert m.shape[0] == int(fx["B"]) and m.shape[1] == int(fx["Lf"])
+    out, labels = orc.fatchord_loop(state, d.mode, np.ascontiguousarray(m[rows, :n]),
+                                    np.ascontiguousarray(a[rows, :n]), np.ascontiguousarray(noise[:n][:, rows]))
+    if d.mode == "RAW":
+        np.testing.assert_array_equal(labels, fx["raw"][:, :n].astype(np.int32))
+    else:
+        assert np.abs(out - fx["raw"][:, :n]).max() <= gf.MOL_TOL

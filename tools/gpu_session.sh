@@ -1,5 +1,5 @@
 #!/bin/bash
-# One GPU session (round 4): parity suite, the headline bench exactly as the driver runs it (its
+# One GPU session: parity suite, the headline bench exactly as the driver runs it (its
 # own live PMC passes included), rocprofv3 kernel-trace summaries of the bench and of the headline
 # alone.  Stops at the first step that ends abnormally (fault / abort / timeout), per the pool rules.
 #   tools/gpu_r04.sh [pytest -k expression]

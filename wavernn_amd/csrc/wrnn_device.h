@@ -77,7 +77,10 @@ __device__ __forceinline__ int wave_argmax(float v, int i) {
 // index of lane l + 1, each lane's own candidates merged by am_merge in index order): the same
 // winner — largest value, ties to the smallest index — from a value-only max reduction and the
 // first lane holding it (ballot), instead of carrying the index through every DPP stage.
-// (No lane equals the max only when a NaN is present: then the general reduction decides.)
+// NaN: fmaxf drops NaN operands, so a NaN candidate never wins here — the winner is the argmax
+// over the non-NaN values (torch.argmax would return the NaN's index; the general (value, index)
+// reduction below is not NaN-faithful either).  NaN logits only come from NaN weights or inputs,
+// which are outside the parity contract.  The fallback runs only if every value is NaN.
 __device__ __forceinline__ int wave_argmax_ordered(float v, int i) {
     const float m = wave_max(v);
     const unsigned long long hit = __ballot(v == m);
@@ -86,8 +89,9 @@ __device__ __forceinline__ int wave_argmax_ordered(float v, int i) {
 }
 
 // wave_argmax for any layout: a value-only max reduction, then the lane holding it (ballot); only
-// when several lanes hold the maximum (an exact tie across lanes) or a NaN is present does the
-// (value, index) reduction decide.  Same winner as wave_argmax.
+// when several lanes hold the maximum (an exact tie across lanes) does the (value, index)
+// reduction decide.  Same winner as wave_argmax for finite values (NaN: as wave_argmax_ordered,
+// a NaN candidate is skipped unless every value is NaN).
 __device__ __forceinline__ int wave_argmax_fast(float v, int i) {
     const float m = wave_max(v);
     const unsigned long long hit = __ballot(v == m);

@@ -89,7 +89,7 @@ __device__ __forceinline__ float mol_sample_pairs(float la, float lb, float ua, 
         const unsigned long long hit = __ballot(v == m) & 0x1Full;
         if (hit != 0) {
             k = __builtin_amdgcn_readlane(i, (int)__builtin_ctzll(hit));
-        } else {   // a NaN among the logits: the general reduction
+        } else {   // every logit NaN (fmaxf skips NaN operands, so a single NaN never wins): fallback
             WRNN_AM_STAGE(0xB1) WRNN_AM_STAGE(0x4E) WRNN_AM_STAGE(0x141) WRNN_AM_STAGE(0x140)
             k = __builtin_amdgcn_readlane(i, 0);
         }

@@ -8,8 +8,11 @@ changes is where the sample loop runs: instead of the host-driven per-step loop
 HIP kernel through the C-ABI (`FatchordLoop`).  There is no CPU fallback: the model must
 live on a GPU and the HIP library must be built, otherwise generate() raises.
 
-Pre-processing: MelResNet as torch modules (MIOpen), then ONE HIP kernel for pad + the
-stretch/box-conv chain + crop + aux stretch + fold + time-major pack (`condition.upsample_pack`).
+Pre-processing: MelResNet as ONE fused HIP kernel (`wrnn_melresnet`, every BatchNorm folded on the
+host; the torch module only for channel counts the kernel does not cover), then the loop entry
+`wrnn_generate_frames`: pad + the stretch/box-conv chain + crop + aux stretch + fold are applied to
+the conditioning TERMS at frame rate on the XCD-resident paths (csrc/frame_terms.hip), or through
+the per-sample records of `condition.upsample_pack` on the others.
 Post-processing (mu-law, cross-fade/unfold, trim, fade-out) is one float64 HIP kernel
 (`condition.postprocess`) with the reference's operation order; only the finished waveform
 crosses to the host.

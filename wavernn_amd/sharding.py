@@ -4,8 +4,15 @@ The reference generates one utterance at a time on one device (gen_wavernn.py:11
 over the test set).  Utterances are independent, so the MI355X path shards them: rank r takes a
 contiguous block of the list (block sizes differ by at most one) and vocodes the whole block as
 the rows of ONE persistent-kernel launch (`WaveRNN.generate_many`; deepmind: `generate(batch=)`).
-Each loop row's sampler draws are keyed by its GLOBAL row id (Philox (seed, row)), so the audio
-does not depend on how many GPUs ran the job.  The only collective is the final gather of
+Each loop row's sampler draws are keyed by its GLOBAL row id (Philox (seed, row)), so every
+utterance sees the same random draws whatever the number of GPUs.  What the GPU count does change
+is the SHAPE of each rank's launch (its row count), and with it the kernel the C-ABI picks
+(`choose_path`, capi.cpp: MoL rnn 512 runs fatchord_xcd_kernel up to 8 rows and
+fatchord_xcdm_kernel from 9; RAW and deepmind one kernel at every row count) and the tiling the
+frame-rate terms GEMM gets.  So the promise is: deepmind outputs bit-identical across world sizes;
+RAW labels identical in every test so far (the terms are rounded differently, so a label exactly at
+a tie could flip); MoL samples equal within the MoL parity tolerance (2·MOL_TOL in
+tests/test_gpu_many.py), not bit for bit — the same contract as generate_many vs single calls.  The only collective is the final gather of
 finished audio to rank 0 (RCCL over xGMI under the "nccl" backend; gloo on CPU for tests) —
 there is no exchange inside the sample loop.
 """
@@ -16,6 +23,14 @@ from typing import Callable, Dict, List, Optional, Sequence
 import numpy as np
 import torch
 import torch.distributed as dist
+
+
+def world_rank(group=None):
+    """(world size, rank) of the group; (1, 0) without an initialised process group (a single
+    GPU runs the same entry points with no collective)."""
+    if not dist.is_available() or not dist.is_initialized():
+        return 1, 0
+    return dist.get_world_size(group), dist.get_rank(group)
 
 
 def shard_indices(n_items: int, rank: int, world: int) -> List[int]:
@@ -31,8 +46,12 @@ def gather_audio(local: Dict[int, np.ndarray], n_items: int, device: torch.devic
     tensor plus an int64 [n_slots, 2] (index, length) table; two all-gathers move them.  The
     audio travels as the float64 generate() returns (RCCL and gloo move float64 natively), so
     rank 0's list is bit-identical to what each rank's generate() produced."""
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
+    world, rank = world_rank(group)
+    if world == 1 and not dist.is_initialized():
+        out = [None] * n_items
+        for idx, audio in local.items():
+            out[idx] = np.asarray(audio, dtype=np.float64)
+        return out
     n_slots = (n_items + world - 1) // world
     lens = torch.tensor([max((len(v) for v in local.values()), default=0)], dtype=torch.int64, device=device)
     dist.all_reduce(lens, op=dist.ReduceOp.MAX, group=group)
@@ -72,9 +91,9 @@ def generate_sharded(model, mels: Sequence, batched: bool, target: int, overlap:
     A rank runs its block through ONE `generate_many` launch, seeded `base_seed` with its first
     loop row at the global row id of its first utterance (every rank knows every mel's row
     count from its length), so the result equals `model.generate_many(mels, seed=base_seed)` on
-    one GPU.  `generate_fn(indices, mels, row_offset)` replaces the generation (host tests)."""
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
+    one GPU — MoL within the parity tolerance, since a rank's launch shape (and so its kernel,
+    module docstring) depends on the world size.  `generate_fn(indices, mels, row_offset)` replaces the generation (host tests)."""
+    world, rank = world_rank(group)
     if device is None:
         device = next(model.parameters()).device
     idx = shard_indices(len(mels), rank, world)
@@ -94,8 +113,7 @@ def generate_sharded_deepmind(model, n_utterances: int, seq_len: int, base_seed:
     rows of one `generate(batch=...)` launch keyed by the global utterance index, rank 0 returns
     the int64 outputs (coarse·256 + fine − 2^15) in utterance order.  Outputs travel as float64
     (exact: |v| ≤ 2^15)."""
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
+    world, rank = world_rank(group)
     if device is None:
         device = next(model.parameters()).device
     idx = shard_indices(n_utterances, rank, world)
@@ -124,8 +142,7 @@ def generate_sharded_folds(model, mel, target: int, overlap: int, mu_law: bool, 
     fold_fn(fold_indices) -> [n][steps] and post_fn([folds][steps] float32) -> waveform replace the
     device work (host tests)."""
     from . import condition
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
+    world, rank = world_rank(group)
     if fold_fn is None:
         if device is None:
             device = next(model.parameters()).device
