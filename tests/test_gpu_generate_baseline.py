@@ -79,6 +79,7 @@ def test_dropin_generate_at_baseline_size(name, models):
         diff = np.abs(got - ref)
         assert diff.max() <= gf.MOL_TOL, f"output: max |Δ| {diff.max():.3g}, {_first_over(diff, gf.MOL_TOL)}"
         assert abs(out.sum() - float(fx["out_sum"])) <= gf.MOL_TOL * out.size
+        print(f"{name}: output max |Δ| {diff.max():.3g} (mean {diff.mean():.3g}) over {diff.size} samples")
 
     # the loop outputs of the same entry (frames -> wrnn_generate_frames), per step, vs the
     # reference's per-step sampler outputs
@@ -91,10 +92,14 @@ def test_dropin_generate_at_baseline_size(name, models):
         lab = lab.cpu().numpy()
         eq = lab[rows] == fx["raw"].astype(np.int32)
         assert eq.all(), f"RAW labels: {eq.mean():.6f} equal, first mismatch {tuple(np.argwhere(~eq)[0])}"
+        print(f"{name}: {eq.size} labels bit-exact; output max rel |Δ| "
+              f"{np.max(np.abs(got - ref) / np.maximum(np.abs(ref), 1e-300)):.3g}")
     else:
         y = y.cpu().numpy()
         diff = np.abs(y[rows] - fx["raw"])
         assert diff.max() <= gf.MOL_TOL, f"loop outputs: max |Δ| {diff.max():.3g}, {_first_over(diff, gf.MOL_TOL)}"
+        print(f"{name}: loop outputs of rows {list(rows)[:4]}{'…' if len(rows) > 4 else ''} max |Δ| {diff.max():.3g} "
+              f"over {diff.size} row-steps")
         if "raw_strided" in fx:
             st = int(fx["raw_stride"])
             diff = np.abs(y[:, ::st] - fx["raw_strided"])

@@ -74,15 +74,16 @@ __host__ __device__ inline XcdsLds xcds_lds_layout() {
     l.h1 = o;    o += kSR;
     l.h2 = o;    o += kSR;
     l.sg = o;    o += 4 * kSR;                // GRU1 terms of all units for the coming step
-    l.w3 = o;    o += kXFcRows * 32;          // fc3 columns of the own f2 rows (waves 4, 5)
-    l.f2x = o;   o += 32;                     // wave 5's fc3 partials, handed to wave 4
+    l.w3 = o;    o += kXFcRows * 32;          // fc3 columns of the own f2 rows (waves 0..3)
+    l.f2x = o;   o += 3 * 32;                 // waves 1..3's fc3 partials, handed to wave 0
     l.ring = o;  o += kXRing * kSTerms;
     l.nz = o;    o += kXRing * kXNoise;
     l.gh2 = o;   o += 88;                     // W_hh2·h2 of the own units (u·3 + q) for the next step
     l.cst = o;   o += kSCst;
     l.xs = o;    o += 4;                      // x, by step parity
     l.misc = o;  o += 8;                      // [0] abort, [1] member, flags (step + 1): [2] h2 gathered,
-                                              // [3] f2x ready, [4] y gathered, [5] f1 gathered
+                                              // [3], [6], [7] f2x of wave 1 / 2 / 3 ready, [4] y gathered,
+                                              // [5] f1 gathered
     l.whh1b = o; o += kSBR * kSNB * 16;
     l.whh1c = o; o += kSBR * kSNB;
     l.whh2b = o; o += kSBR * kSNB * 16;

@@ -15,13 +15,16 @@
 //   B2 → GRU2: wave ub (0..6), engine q (0..2) = gate q of block-row ub (W_ih2 blocks in VGPRs);
 //        permlane swaps bring the z and n sums to engine 0, whose lanes 0..3 finish units 4ub + l
 //        and publish y = x_I + h1 + h2                                             [hop Y]
-//   waves 6, 7 poll y (7 × 16 B per lane) → fc1 rows 8h.. in registers → relu      [hop F1]
-//   waves 4, 5 poll f1 → fc2 rows 8h.. → relu → fc3 partials; wave 5 → wave 4     [hop F2]
+//   waves 4..7 poll y (7 × 16 B per lane) → fc1 rows 4h.. (h = w − 4) in registers → relu [hop F1]
+//   waves 0..3 poll f1 → fc2 rows 4w.. → relu → fc3 partials; waves 1..3 → wave 0   [hop F2]
 //   wave 0 polls the 32 × 32 partials → Σ + b3 → MoL sample (redundant, bit-identical) → x_t
-// Off the critical path: W_hh1·h1 (LDS blocks; waves 0..5, one engine per gate block-row) → the
-// GRU1 terms of step t+1, published after "y gathered"; h2 likewise and gathered by wave 3 right
-// away; after "h2 gathered": W_hh2·h2 (LDS blocks; waves 0, 3, then 4, 5 after hop F2's publish,
-// 1, 2 after their S quarter); after "f1 gathered": S by waves 1, 2, 6, 7, then the ring (wave 7).  fp32, sums re-associated (tolerance-checked).
+// Four rows per fc wave (round 5; eight on two waves before: fc1's 8 × 7 weight pairs per lane
+// spilled 28 VGPRs).  Off the critical path, in each wave's idle windows: waves 0..3 (idle from
+// GRU2 until f1 arrives) W_hh1·h1 (LDS blocks, one engine per gate block-row, 21 = 16 + 5) → the
+// GRU1 terms of step t+1, published after "y gathered", and h2; waves 4..7 (idle from their f1
+// publish to the step's end) h2 out, after "f1 gathered": the h2 gather (wave 4), the four S
+// quarters, the ring (wave 7), then W_hh2·h2 (LDS blocks, 16 + 5 engines).  fp32, sums
+// re-associated (tolerance-checked).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -67,6 +70,36 @@ __device__ __forceinline__ void fc8_rows_k(const f2v *w, const f2v (&xk)[NK], fl
     }
 }
 
+// 4 rows of an (NK·128)-wide layer against a vector polled into registers by ONE wave (lane l:
+// pairs k at granules 2(l + 64k) + {0, 1}, weights of row r in w[r·NK + k]).  Packed FMAs, then a
+// reduce-scatter — permlane32 swap (row r vs r + 2), permlane16 swap (r vs r + 1), DPP sum over
+// the 16 lanes of a row — leaves the full sum of row l >> 4, identical bits in the 16 lanes of
+// DPP row l >> 4.
+template <int NK>
+__device__ __forceinline__ float fc4_rows_k(const f2v *w, const f2v (&xk)[NK]) {
+    float s[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        f2v a = __builtin_elementwise_fma(w[r * NK], xk[0], f2v{0.0f, 0.0f});
+        f2v b = __builtin_elementwise_fma(w[r * NK + 1], xk[1], f2v{0.0f, 0.0f});
+#pragma unroll
+        for (int k = 2; k < NK; k += 2) a = __builtin_elementwise_fma(w[r * NK + k], xk[k], a);
+#pragma unroll
+        for (int k = 3; k < NK; k += 2) b = __builtin_elementwise_fma(w[r * NK + k], xk[k], b);
+        const f2v t = a + b;
+        s[r] = t.x + t.y;
+    }
+    float h[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {   // lanes < 32 keep row j, lanes ≥ 32 row j + 2
+        const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(s[j]), __float_as_uint(s[j + 2]), false, false);
+        h[j] = __uint_as_float(q[0]) + __uint_as_float(q[1]);
+    }
+    // even DPP rows keep h[0], odd rows h[1]: DPP row g ends with row g
+    const auto q = __builtin_amdgcn_permlane16_swap(__float_as_uint(h[0]), __float_as_uint(h[1]), false, false);
+    return row_sum16(__uint_as_float(q[0]) + __uint_as_float(q[1]));
+}
+
 // One gate block-row on a 16-lane engine: Σ over its nonzero 4×4 blocks of W_blk · v[4j..4j+3];
 // this lane holds blocks wa (column block ja) and wb (jb), rows as float4.  The 4 row sums end
 // in g[0..3], identical in all 16 lanes of the engine.
@@ -106,7 +139,8 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
     float *whh1b = smem + ll.whh1b, *whh2b = smem + ll.whh2b;
     const int *whh1c = reinterpret_cast<const int *>(smem + ll.whh1c), *whh2c = reinterpret_cast<const int *>(smem + ll.whh2c);
     int *misc = reinterpret_cast<int *>(smem + ll.misc);
-    int *abort_flag = misc, *h2ready = misc + 2, *f2ready = misc + 3, *ygot = misc + 4, *f1got = misc + 5;
+    int *abort_flag = misc, *h2ready = misc + 2, *ygot = misc + 4, *f1got = misc + 5;
+    int *const f2ready[3] = {misc + 3, misc + 6, misc + 7};   // fc2 waves 1..3: partials in f2x
 
     // ---- membership: XCD k (row b0 + k) and index c within it
     if (tid == 0) {
@@ -137,10 +171,11 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
     // ---- register-resident weights
     //   wg (waves 0..6, engines 0..2): the two W_ih2 blocks of this lane in gate block-row
     //     (q = engine, ub = wave), columns ja / jb
-    //   wr (one register set, by role): waves 6, 7: fc1 rows 8h + r at the y granules this lane
-    //     polls (r·7 + k); waves 4, 5: fc2 rows (r·4 + k); wave 0: the F2 poll buffer
+    //   wr (one register set, by role): waves 4..7: fc1 rows 4h + r (h = w − 4) at the y granules
+    //     this lane polls (r·7 + k); waves 0..3: fc2 rows 4w + r (r·4 + k); wave 0: the F2 poll
+    //     buffer in wr[16..31]
     f4v wg[8];
-    f2v wr[56];
+    f2v wr[32];
     int ja = 0, jb = 0;
     {
         const bool gw = wave < kSUB && eng < 3;
@@ -157,23 +192,20 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
             jb = cc[li + 16];
         }
     }
-    if (wave >= 6) {
-        const float *W = S + a.s.w1 + (wave - 6) * 8 * R;
+    if (wave >= 4) {
+        const float *W = S + a.s.w1 + (wave - 4) * 4 * R;
 #pragma unroll
-        for (int r = 0; r < 8; ++r)
-#pragma unroll
-            for (int kk = 0; kk < kSPairs; ++kk)
-                wr[r * kSPairs + kk] = *reinterpret_cast<const f2v *>(W + r * R + 2 * (lane + 64 * kk));
-    } else if (wave >= 4) {
-        const float *W = S + a.s.w2 + (wave - 4) * 8 * 512;
-#pragma unroll
-        for (int i = 0; i < 56; ++i) {
-            const int r = i >> 2, kk = i & 3;
-            wr[i] = i < 32 ? *reinterpret_cast<const f2v *>(W + r * 512 + 2 * (lane + 64 * kk)) : f2v{0.0f, 0.0f};
+        for (int i = 0; i < 32; ++i) {
+            const int r = i / kSPairs, kk = i - r * kSPairs;
+            wr[i] = i < 4 * kSPairs ? *reinterpret_cast<const f2v *>(W + r * R + 2 * (lane + 64 * kk)) : f2v{0.0f, 0.0f};
         }
     } else {
+        const float *W = S + a.s.w2 + wave * 4 * 512;
 #pragma unroll
-        for (int i = 0; i < 56; ++i) wr[i] = f2v{0.0f, 0.0f};
+        for (int i = 0; i < 32; ++i) {
+            const int r = i >> 2, kk = i & 3;
+            wr[i] = i < 16 ? *reinterpret_cast<const f2v *>(W + r * 512 + 2 * (lane + 64 * kk)) : f2v{0.0f, 0.0f};
+        }
     }
     // GRU1 of units tid and tid + 512 (tid < 384): x-coefficients
     const bool two = tid + 512 < R;
@@ -216,32 +248,32 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
         }
         sp_block_row(wa4, wb4, wc[br * kSNB + li], wc[br * kSNB + li + 16], v, g);
     };
-    // W_hh1·h1 → GRU1 terms of step t+1: engines E = 4w + e < 21 of waves 0..5 (br = E)
-    const int gh1_br = 4 * wave + eng;
-    const bool gh1w = wave < 6 && gh1_br < kSBR;
-    auto gh1_dots = [&](float (&g)[4]) { lds_block_row(whh1b, whh1c, gh1w ? gh1_br : 0, h1s, g); };
-    auto publish_terms = [&](int t, const float (&g)[4]) {
-        if (gh1w && li < 4) {
-            const int q = gh1_br / kSUB, ub = gh1_br - q * kSUB;
+    // The 21 gate block-rows of W_hh1 / W_hh2 on a wave quad's 16 engines: pass 0 block-row 4·(w & 3) + e,
+    // pass 1 block-rows 16..20 on the first wave of the quad (engines 0..3) and the second (engine 0).
+    // W_hh1·h1 → GRU1 terms of step t+1 on waves 0..3, W_hh2·h2 → gh2s on waves 4..7.
+    const int wq = wave & 3;
+    const int br0 = 4 * wq + eng, br1 = wq == 0 ? 16 + eng : (wq == 1 && eng == 0) ? 20 : -1;
+    auto gh_dots = [&](const float *wbk, const int *wck, const float *v, int br, float (&g)[4]) {
+        lds_block_row(wbk, wck, br >= 0 ? br : 0, v, g);
+    };
+    auto publish_terms = [&](int t, int br, const float (&g)[4]) {
+        if (br >= 0 && li < 4) {
+            const int q = br / kSUB, ub = br - q * kSUB;
             publish_term(t, (4 * ub + li) * 3 + q, sel4(g, li));
         }
     };
-    // W_hh2·h2 → gh2s: engines E = 4·gidx + e < 21 of waves 0, 3, 4, 5, 1, 2
-    const int gidx = wave == 0 ? 0 : wave == 3 ? 1 : wave == 4 ? 2 : wave == 5 ? 3 : wave == 1 ? 4 : 5;
-    const int gh2_br = 4 * gidx + eng;
-    const bool gh2w = wave <= 5 && gh2_br < kSBR;
-    auto gh2_dots = [&]() {
+    auto gh2_dots = [&](int br) {
         float g[4];
-        lds_block_row(whh2b, whh2c, gh2w ? gh2_br : 0, h2s, g);
-        if (gh2w && li < 4) {
-            const int q = gh2_br / kSUB, ub = gh2_br - q * kSUB;
+        gh_dots(whh2b, whh2c, h2s, br, g);
+        if (br >= 0 && li < 4) {
+            const int q = br / kSUB, ub = br - q * kSUB;
             gh2s[(4 * ub + li) * 3 + q] = sel4(g, li);
         }
     };
-    // a quarter of step t's GRU1 terms (waves 1, 2, 6, 7: 896 granules each, one poll round)
+    // a quarter of step t's GRU1 terms (waves 4..7: 896 granules each, one poll round)
     auto gather_terms = [&](int t) {
         if (WRNN_XCDS_DIAG & 1) return;
-        const int qq = wave <= 2 ? wave - 1 : wave - 4;   // waves 1, 2, 6, 7
+        const int qq = wave - 4;
         xgather16<kSPairs>(XG(XH_S0 + (t & 1)) + qq * R, (uint32_t)t + 1u, a.ctl, a.timeout_ticks, t,
                            XH_S0 + (t & 1), abort_flag, lane, [&](int i, float v0, float v1) {
                                *reinterpret_cast<f2v *>(sg + qq * R + i) = f2v{v0, v1};
@@ -301,8 +333,11 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
     __syncthreads();
     if (!resume) {   // GRU1 terms of step 0 (GH1 = 0), published and gathered
         const float z4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        publish_terms(0, z4);
-        if (wave == 1 || wave == 2 || wave == 6 || wave == 7) {
+        if (wave < 4) {
+            publish_terms(0, br0, z4);
+            publish_terms(0, br1, z4);
+        }
+        if (wave >= 4) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             gather_terms(0);
         }
@@ -375,97 +410,142 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
         auto pub_h2 = [&]() {
             if (wave < kSUB && lane < 4) xpub_b(xgr, XGI(XH_H2) + c * kSU + ul, tag, h2own);
         };
-        // fc waves: lane l ends fc8_rows_k with row 8h + j + 2·(l >> 4) in o[j]; lanes with
-        // (l & 15) < 2 publish row 8h + (l & 1) + 2·(l >> 4)
-        const int jq = lane & 1, rho = jq + 2 * (lane >> 4);
-        if (wave == 0) {
+        // fc waves: lane l ends fc4_rows_k with row 4h + (l >> 4); lanes with (l & 15) == 0 publish it
+        const int rq = lane >> 4;
+        if (wave < 4) {
+            // ---- waves 0..3: W_hh1·h1 (GRU1 terms of step t+1) in hop Y's window, published after
+            // y gathered with h2; then hop F1 → fc2 (:220-221) rows 4w.. → relu → fc3 partial logits
+            // of those rows (:223); waves 1..3 hand theirs to wave 0 (LDS, flags), wave 0 publishes
+            // the workgroup's line (hop F2), polls all 32 lines and samples
             if (more) {
-                float g[4];
-                gh1_dots(g);
+                float g0[4], g1[4];
+                gh_dots(whh1b, whh1c, h1s, br0, g0);
+                if (wq < 2) gh_dots(whh1b, whh1c, h1s, br1, g1);
                 wait_flag(ygot, tag);
-                publish_terms(t + 1, g);
+                publish_terms(t + 1, br0, g0);
+                if (wq < 2) publish_terms(t + 1, br1, g1);
                 pub_h2();
-                wait_flag(h2ready, tag);
-                gh2_dots();
             }
-            // ---- hop F2: Σ of the 32 workgroups' partials + b3 → sample
-            const int jp = lane & 15, pg = lane >> 4;
-            const float ua = NZ(t)[jp < 5 ? 2 * jp : 0], ub = NZ(t)[jp < 5 ? 2 * jp + 1 : 0], u10 = NZ(t)[10];
-            const float b3a = cst[SC_B3 + 2 * jp], b3b = cst[SC_B3 + 2 * jp + 1];
+            const float v2 = tr[SX_V2 + 4 * wave + rq];
+            float w3c[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) w3c[r] = w3s[(4 * wave + r) * 32 + (lane & 31)];
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const __amdgpu_buffer_rsrc_t rf = hop_rsrc(XG(XH_F2));
-            const int goff = pg * 8 * kXF2Line * 8 + jp * 16;
-            const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
-            unsigned spins = 0;
-            float pa[8], pb[8];
-            for (;;) {
-                u4v *v = reinterpret_cast<u4v *>(&wr[0]);   // wave 0 holds no weights there
+            u4v v[4];
+            xpoll16<4>(XG(XH_F1), tag, a.ctl, a.timeout_ticks, t, XH_F1, abort_flag, lane, v);
+            if (wave == 1) set_flag(f1got, tag);
+            XSTAMPW(5, 1);
+            f2v fk[4];
 #pragma unroll
-                for (int m = 0; m < 8; ++m) v[m] = ld16_sc1(rf, goff + m * kXF2Line * 8);
-                bool ok = true;
+            for (int kk = 0; kk < 4; ++kk) fk[kk] = f2v{__uint_as_float(v[kk].x), __uint_as_float(v[kk].z)};
+            const float f = fc4_rows_k<4>(wr, fk) + v2;
+            const float f2 = f > 0.0f ? f : 0.0f;
+            float p = 0.0f;
 #pragma unroll
-                for (int m = 0; m < 8; ++m) ok &= (v[m].y == tag) & (v[m].w == tag);
-                if (ok) {
-#pragma unroll
-                    for (int m = 0; m < 8; ++m) {
-                        pa[m] = __uint_as_float(v[m].x);
-                        pb[m] = __uint_as_float(v[m].z);
-                    }
-                    break;
+            for (int g = 0; g < 4; ++g) p = fmaf(w3c[g], lane_bcast(f2, 16 * g), p);
+            if (wave != 0) {
+                if (lane < 32) f2x[(wave - 1) * 32 + lane] = p;
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                set_flag(f2ready[wave - 1], tag);
+            } else {
+                // waves 1..3 set their flags on every path (their polls are bounded); the abort word
+                // ends the wait too should that ever change
+                unsigned spin = 0;
+                while ((__hip_atomic_load(f2ready[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)tag) |
+                       (__hip_atomic_load(f2ready[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)tag) |
+                       (__hip_atomic_load(f2ready[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)tag)) {
+                    if ((++spin & 255u) == 0 &&
+                        __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+                        break;
                 }
-                if ((++spins & 63u) == 0) {
-                    const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - c0) > a.timeout_ticks;
-                    const bool other = __hip_atomic_load(&a.ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-                    if (late || other) {
-                        if (late) record_abort(a.ctl, -4, t, XH_F2, blockIdx.x);
-                        *abort_flag = 1;
+                asm volatile("" ::: "memory");
+                if (lane < kXF2Line)   // 30, 31: zero weights
+                    xpub_b(xgr, XGI(XH_F2) + c * kXF2Line + lane, tag, ((p + f2x[lane]) + f2x[32 + lane]) + f2x[64 + lane]);
+                XSTAMPW(6, 0);
+                // ---- hop F2: Σ of the 32 workgroups' partials + b3 → sample
+                const int jp = lane & 15, pg = lane >> 4;
+                const float ua = NZ(t)[jp < 5 ? 2 * jp : 0], ub = NZ(t)[jp < 5 ? 2 * jp + 1 : 0], u10 = NZ(t)[10];
+                const float b3a = cst[SC_B3 + 2 * jp], b3b = cst[SC_B3 + 2 * jp + 1];
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const __amdgpu_buffer_rsrc_t rf = hop_rsrc(XG(XH_F2));
+                const int goff = pg * 8 * kXF2Line * 8 + jp * 16;
+                const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
+                unsigned spins = 0;
+                float pa[8], pb[8];
+                for (;;) {
+                    u4v *vv = reinterpret_cast<u4v *>(&wr[16]);   // wave 0's fc2 weights are wr[0..15]
 #pragma unroll
-                        for (int m = 0; m < 8; ++m) pa[m] = pb[m] = 0.0f;
+                    for (int m = 0; m < 8; ++m) vv[m] = ld16_sc1(rf, goff + m * kXF2Line * 8);
+                    bool ok = true;
+#pragma unroll
+                    for (int m = 0; m < 8; ++m) ok &= (vv[m].y == tag) & (vv[m].w == tag);
+                    if (ok) {
+#pragma unroll
+                        for (int m = 0; m < 8; ++m) {
+                            pa[m] = __uint_as_float(vv[m].x);
+                            pb[m] = __uint_as_float(vv[m].z);
+                        }
                         break;
                     }
-                }
-            }
-            XSTAMP(7);
+                    if ((++spins & 63u) == 0) {
+                        const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - c0) > a.timeout_ticks;
+                        const bool other = __hip_atomic_load(&a.ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+                        if (late || other) {
+                            if (late) record_abort(a.ctl, -4, t, XH_F2, blockIdx.x);
+                            *abort_flag = 1;
 #pragma unroll
-            for (int n = 4; n >= 1; n /= 2)
-#pragma unroll
-                for (int m = 0; m < n; ++m) {
-                    pa[m] += pa[m + n];
-                    pb[m] += pb[m + n];
+                            for (int m = 0; m < 8; ++m) pa[m] = pb[m] = 0.0f;
+                            break;
+                        }
+                    }
                 }
-            const float la = cross_rows(pa[0]) + b3a, lb = cross_rows(pb[0]) + b3b;   // logits 2jp, 2jp+1
-            x = mol_sample_pairs(la, lb, ua, ub, u10, jp);
-            if (lane == 0) {
-                xs[t & 1] = x;
-                if (c == 0) a.out[(size_t)b * a.L + t] = x;
+                XSTAMP(7);
+#pragma unroll
+                for (int n = 4; n >= 1; n /= 2)
+#pragma unroll
+                    for (int m = 0; m < n; ++m) {
+                        pa[m] += pa[m + n];
+                        pb[m] += pb[m + n];
+                    }
+                const float la = cross_rows(pa[0]) + b3a, lb = cross_rows(pb[0]) + b3b;   // logits 2jp, 2jp+1
+                x = mol_sample_pairs(la, lb, ua, ub, u10, jp);
+                if (lane == 0) {
+                    xs[t & 1] = x;
+                    if (c == 0) a.out[(size_t)b * a.L + t] = x;
+                }
+                XSTAMP(8);
             }
-            XSTAMP(8);
-        } else if (wave >= 6) {
-            // ---- hop Y → fc1 (:216-218) rows 8h.. in registers → relu → hop F1
-            const int hf = wave - 6, rg = 8 * hf + rho;
+        } else {
+            // ---- waves 4..7: hop Y → fc1 (:216-218) rows 4h.. in registers → relu → hop F1
+            const int hf = wave - 4, rg = 4 * hf + rq;
             const float v1 = tr[SX_V1 + rg];
-            if (wave == 6) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (wave == 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             u4v v[kSPairs];
             xpoll16<kSPairs>(XG(XH_Y), tag, a.ctl, a.timeout_ticks, t, XH_Y, abort_flag, lane, v);
-            if (hf == 0) {
-                set_flag(ygot, tag);
-                if (more) pub_h2();   // before fc1: the early h2 gather (wave 3) waits for every h2
-            }
-            XSTAMPW(3, 6);
+            if (hf == 0) set_flag(ygot, tag);
+            XSTAMPW(3, 4);
             f2v yk[kSPairs];
 #pragma unroll
             for (int kk = 0; kk < kSPairs; ++kk) yk[kk] = f2v{__uint_as_float(v[kk].x), __uint_as_float(v[kk].z)};
-            float o[2];
-            fc8_rows_k<kSPairs>(wr, yk, o);
-            const float A = (jq == 0 ? o[0] : o[1]) + v1;
-            if ((lane & 15) < 2) xpub_b(xgr, XGI(XH_F1) + c * kXFcRows + rg, tag, A > 0.0f ? A : 0.0f);
-            XSTAMPW(4, 6);
+            const float A = fc4_rows_k<kSPairs>(wr, yk) + v1;
+            if ((lane & 15) == 0) xpub_b(xgr, XGI(XH_F1) + c * kXFcRows + rg, tag, A > 0.0f ? A : 0.0f);
+            XSTAMPW(4, 4);
             if (more) {
-                // after f1 gathered: a quarter of the next S; wave 7 then the ring entries of step
-                // t+3 from the registers loaded a step ago and the load for t+4 (lands during the
-                // next step, before this wave's next poll)
+                // h2 out (waves 4..6 hold GRU2 units); after f1 gathered: h2 (wave 4, then its flag),
+                // the four quarters of the next S, the ring (wave 7: step t+3's entries from the
+                // registers loaded a step ago, the load for t+4 lands during the next step); after
+                // h2 gathered: W_hh2·h2
+                pub_h2();
                 wait_flag(f1got, tag);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (wave == 4) {
+                    if (!(WRNN_XCDS_DIAG & 2))
+                        xgather16<kSPairs>(XG(XH_H2), tag, a.ctl, a.timeout_ticks, t, XH_H2, abort_flag, lane,
+                                           [&](int i, float v0, float v1) { *reinterpret_cast<f2v *>(h2s + i) = f2v{v0, v1}; });
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    set_flag(h2ready, tag);
+                    XSTAMPW(10, 4);
+                }
                 gather_terms(t + 1);
                 if (wave == 7) {
                     if (t + 3 <= t_terms && lane < kSTerms / 4) reinterpret_cast<f4v *>(RING(t + 3))[lane] = wg[0];
@@ -474,93 +554,11 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
                     stage_ring(t + 4);
                     XSTAMPW(12, 7);
                 }
+                wait_flag(h2ready, tag);
+                gh2_dots(br0);
+                if (wq < 2) gh2_dots(br1);
+                XSTAMPW(13, 5);
             }
-        } else if (wave >= 4) {
-            const int hf = wave - 4;
-            if (more) {   // W_hh1 block-rows; after y gathered their terms and h2 out
-                float g[4];
-                gh1_dots(g);
-                wait_flag(ygot, tag);
-                publish_terms(t + 1, g);
-                pub_h2();
-            }
-            // ---- hop F1 → fc2 (:220-221) rows 8h.. in registers → relu → fc3 partial logits of
-            // those rows (:223); wave 5 hands its partials to wave 4, wave 4 publishes (hop F2)
-            float v2[2], w3c[8];
-#pragma unroll
-            for (int j = 0; j < 2; ++j) v2[j] = tr[SX_V2 + 8 * hf + j + 2 * (lane >> 4)];
-#pragma unroll
-            for (int r = 0; r < 8; ++r) w3c[r] = w3s[(8 * hf + r) * 32 + (lane & 31)];
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            u4v v[4];
-            xpoll16<4>(XG(XH_F1), tag, a.ctl, a.timeout_ticks, t, XH_F1, abort_flag, lane, v);
-            if (hf == 0) set_flag(f1got, tag);
-            XSTAMPW(5, 4);
-            f2v fk[4];
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk) fk[kk] = f2v{__uint_as_float(v[kk].x), __uint_as_float(v[kk].z)};
-            float o[2];
-            fc8_rows_k<4>(wr, fk, o);
-            float p = 0.0f;
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const float f = o[j] + v2[j];
-                const float f2 = f > 0.0f ? f : 0.0f;
-#pragma unroll
-                for (int g = 0; g < 4; ++g) p = fmaf(w3c[j + 2 * g], lane_bcast(f2, 16 * g), p);
-            }
-            if (hf == 1) {
-                if (lane < 32) f2x[lane] = p;
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                set_flag(f2ready, tag);
-                if (more) {
-                    wait_flag(h2ready, tag);
-                    gh2_dots();
-                }
-            } else {
-                // wave 4 sets the flag on every path (its poll is bounded); the abort word ends the
-                // wait too should that ever change
-                unsigned spin = 0;
-                while (__hip_atomic_load(f2ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)tag) {
-                    if ((++spin & 255u) == 0 &&
-                        __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
-                        break;
-                }
-                asm volatile("" ::: "memory");
-                if (lane < kXF2Line) xpub_b(xgr, XGI(XH_F2) + c * kXF2Line + lane, tag, p + f2x[lane]);   // 30, 31: zero weights
-                XSTAMPW(6, 4);
-                if (more) {
-                    wait_flag(h2ready, tag);
-                    gh2_dots();
-                }
-            }
-        } else if (more) {
-            // ---- waves 1..3: W_hh1 block-rows → after y gathered their terms and h2 out; wave 3
-            // gathers h2; waves 1, 2 after f1 gathered S quarters; then W_hh2·h2
-            float g[4];
-            gh1_dots(g);
-            wait_flag(ygot, tag);
-            publish_terms(t + 1, g);
-            pub_h2();
-            XSTAMPW(9, 1);
-            if (wave == 3) {   // h2 right after y (every workgroup publishes it on "y gathered")
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (!(WRNN_XCDS_DIAG & 2))
-                    xgather16<kSPairs>(XG(XH_H2), tag, a.ctl, a.timeout_ticks, t, XH_H2, abort_flag, lane,
-                                       [&](int i, float v0, float v1) { *reinterpret_cast<f2v *>(h2s + i) = f2v{v0, v1}; });
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                set_flag(h2ready, tag);
-                XSTAMPW(10, 3);
-            }
-            if (wave != 3) {   // waves 1, 2: after f1 gathered a quarter of the next S
-                wait_flag(f1got, tag);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                gather_terms(t + 1);
-                XSTAMPW(11, 1);
-            }
-            wait_flag(h2ready, tag);
-            gh2_dots();
-            XSTAMPW(13, 1);
         }
         bar();
         // next step's x, GRU1 terms and the abort word: one LDS round trip

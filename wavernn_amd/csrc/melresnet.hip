@@ -19,6 +19,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 
 #include "wavernn_amd.h"
@@ -26,7 +27,9 @@
 namespace wrnn {
 
 constexpr int kMrThreads = 256;
-constexpr int kMrF = 16;          // frames per workgroup
+// frames per workgroup: 16 when the grid has enough tiles to fill the chip, else 4 (a single 5 s mel
+// is 26 tiles of 16 frames on 256 CUs; at 4 frames it is 102, each carrying a quarter of the work)
+constexpr int kMrFBig = 16, kMrFSmall = 4;
 
 constexpr int kMrKc = 128;        // weight rows (input channels) staged through LDS at a time
 
@@ -74,7 +77,7 @@ struct MrArgs {
     int U, T, in_dims, C, R, blocks, K;
 };
 
-template <int FPT_C, int FPT_R>
+template <int kMrF, int FPT_C, int FPT_R>
 __global__ __launch_bounds__(kMrThreads) void melresnet_kernel(MrArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int u = blockIdx.y, t0 = blockIdx.x * kMrF, tid = threadIdx.x;
@@ -134,7 +137,7 @@ __global__ __launch_bounds__(kMrThreads) void melresnet_kernel(MrArgs a) {
 }
 
 // frames per thread for Cout outputs over kMrF frames and 256 threads (0: unsupported)
-inline int mr_fpt(int cout) {
+inline int mr_fpt(int cout, int kMrF) {
     if (cout < 1 || cout > kMrThreads) return 0;
     const int out = cout * kMrF;
     if (out <= kMrThreads) return 1;
@@ -159,26 +162,39 @@ int wrnn_melresnet(const wrnn_melresnet_cfg *cfg, const float *packed, const flo
                    void *stream) {
     using namespace wrnn;
     if (wrnn_melresnet_floats(cfg) < 0 || !packed || !mel || !aux || U < 1 || T < 1) return WRNN_EINVAL;
-    const int fc = mr_fpt(cfg->compute_dims), fr = mr_fpt(cfg->res_out_dims);
     const int K = 2 * cfg->pad + 1;
-    const size_t lds = ((size_t)cfg->in_dims * (kMrF + K - 1) + 2 * (size_t)cfg->compute_dims * kMrF +
+    // small grids (fewer 16-frame tiles than CUs) take 4-frame tiles (WRNN_MR_FRAMES=16|4 forces one)
+    const char *fe = std::getenv("WRNN_MR_FRAMES");
+    int F = (long long)U * ((T + kMrFBig - 1) / kMrFBig) >= 256 ? kMrFBig : kMrFSmall;
+    if (fe && (std::atoi(fe) == kMrFBig || std::atoi(fe) == kMrFSmall)) F = std::atoi(fe);
+    int fc = mr_fpt(cfg->compute_dims, F), fr = mr_fpt(cfg->res_out_dims, F);
+    if ((!fc || !fr) && F == kMrFSmall) {   // channel counts only the 16-frame form covers
+        F = kMrFBig;
+        fc = mr_fpt(cfg->compute_dims, F);
+        fr = mr_fpt(cfg->res_out_dims, F);
+    }
+    const size_t lds = ((size_t)cfg->in_dims * (F + K - 1) + 2 * (size_t)cfg->compute_dims * F +
                         (size_t)kMrKc * std::max(cfg->compute_dims, cfg->res_out_dims)) * 4;
     if (!fc || !fr || lds > 160 * 1024) return WRNN_EUNSUPPORTED;
     MrArgs a{packed, mel, aux, U, T, cfg->in_dims, cfg->compute_dims, cfg->res_out_dims, cfg->res_blocks, K};
-    const dim3 grid((T + kMrF - 1) / kMrF, U);
+    const dim3 grid((T + F - 1) / F, U);
     hipStream_t st = (hipStream_t)stream;
-#define WRNN_MR_CASE(A, B)                                                                          \
-    if (fc == A && fr == B) {                                                                       \
+#define WRNN_MR_CASE(FF, A, B)                                                                      \
+    if (F == FF && fc == A && fr == B) {                                                            \
         if (lds > 64 * 1024 &&                                                                      \
-            hipFuncSetAttribute((const void *)melresnet_kernel<A, B>,                               \
+            hipFuncSetAttribute((const void *)melresnet_kernel<FF, A, B>,                           \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) \
             return WRNN_EHIP;                                                                       \
-        hipLaunchKernelGGL((melresnet_kernel<A, B>), grid, dim3(kMrThreads), lds, st, a);           \
+        hipLaunchKernelGGL((melresnet_kernel<FF, A, B>), grid, dim3(kMrThreads), lds, st, a);       \
         return hipGetLastError() == hipSuccess ? WRNN_OK : WRNN_EHIP;                              \
     }
-    WRNN_MR_CASE(8, 8) WRNN_MR_CASE(1, 1) WRNN_MR_CASE(2, 2) WRNN_MR_CASE(4, 4) WRNN_MR_CASE(16, 16)
-    WRNN_MR_CASE(8, 1) WRNN_MR_CASE(8, 2) WRNN_MR_CASE(8, 4) WRNN_MR_CASE(8, 16)
-    WRNN_MR_CASE(1, 8) WRNN_MR_CASE(2, 8) WRNN_MR_CASE(4, 8) WRNN_MR_CASE(16, 8)
+    WRNN_MR_CASE(16, 8, 8) WRNN_MR_CASE(16, 1, 1) WRNN_MR_CASE(16, 2, 2) WRNN_MR_CASE(16, 4, 4)
+    WRNN_MR_CASE(16, 16, 16) WRNN_MR_CASE(16, 8, 1) WRNN_MR_CASE(16, 8, 2) WRNN_MR_CASE(16, 8, 4)
+    WRNN_MR_CASE(16, 8, 16) WRNN_MR_CASE(16, 1, 8) WRNN_MR_CASE(16, 2, 8) WRNN_MR_CASE(16, 4, 8)
+    WRNN_MR_CASE(16, 16, 8)
+    WRNN_MR_CASE(4, 2, 2) WRNN_MR_CASE(4, 1, 1) WRNN_MR_CASE(4, 4, 4) WRNN_MR_CASE(4, 2, 1)
+    WRNN_MR_CASE(4, 1, 2) WRNN_MR_CASE(4, 4, 2) WRNN_MR_CASE(4, 2, 4) WRNN_MR_CASE(4, 4, 1)
+    WRNN_MR_CASE(4, 1, 4)
 #undef WRNN_MR_CASE
     return WRNN_EUNSUPPORTED;
 }
