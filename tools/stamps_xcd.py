@@ -14,9 +14,10 @@ from wavernn_amd import synthetic as syn  # noqa: E402
 from wavernn_amd.loop import FatchordLoop  # noqa: E402
 
 SPARSE_STAMPS = [(0, "start (after B1)"), (1, "GRU1 done (after B2)"), (2, "Y published (GRU2)"),
-                 (3, "w6: Y gathered"), (4, "w6: f1 published"), (5, "w4: F1 gathered"), (6, "w4: F2 published"),
-                 (7, "F2 gathered"), (8, "sample done"), (9, "w1: GH1 terms + h2 published"),
-                 (10, "w3: h2 gathered"), (13, "w1: GH2 done"), (11, "w1: S quarter gathered"), (12, "w7: ring done")]
+                 (3, "w4: Y gathered"), (4, "w4: f1 published"), (5, "w1: F1 gathered"),
+                 (6, "w0: F2 published (+3 hand-offs)"), (7, "F2 gathered"), (8, "sample done"),
+                 (9, "w1: GH1 terms + h2 published"), (10, "w4: h2 gathered"), (11, "w5: S quarter gathered"),
+                 (13, "w5: GH2 done"), (12, "w7: ring done")]
 STAMPS = [(0, "start (after B1)"), (1, "GRU1 done (after B2)"), (2, "Y published (GRU2)"), (3, "w1: Y gathered"),
           (4, "w1: f1 published"), (5, "w3: F1 gathered"), (6, "w3: F2 published"), (7, "F2 gathered"),
           (8, "sample done"), (9, "w3: GH1 terms published"), (10, "w6: h2 gathered"),

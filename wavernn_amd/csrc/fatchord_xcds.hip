@@ -425,6 +425,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
                 publish_terms(t + 1, br0, g0);
                 if (wq < 2) publish_terms(t + 1, br1, g1);
                 pub_h2();
+                XSTAMPW(9, 1);
             }
             const float v2 = tr[SX_V2 + 4 * wave + rq];
             float w3c[4];
@@ -523,6 +524,9 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
             u4v v[kSPairs];
             xpoll16<kSPairs>(XG(XH_Y), tag, a.ctl, a.timeout_ticks, t, XH_Y, abort_flag, lane, v);
             if (hf == 0) set_flag(ygot, tag);
+            // h2 out (waves 4..6 hold GRU2 units) before fc1: a store issued here lands in the fc1
+            // compute, not in hop F1's window
+            if (more) pub_h2();
             XSTAMPW(3, 4);
             f2v yk[kSPairs];
 #pragma unroll
@@ -531,11 +535,9 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
             if ((lane & 15) == 0) xpub_b(xgr, XGI(XH_F1) + c * kXFcRows + rg, tag, A > 0.0f ? A : 0.0f);
             XSTAMPW(4, 4);
             if (more) {
-                // h2 out (waves 4..6 hold GRU2 units); after f1 gathered: h2 (wave 4, then its flag),
-                // the four quarters of the next S, the ring (wave 7: step t+3's entries from the
-                // registers loaded a step ago, the load for t+4 lands during the next step); after
-                // h2 gathered: W_hh2·h2
-                pub_h2();
+                // after f1 gathered: h2 (wave 4, then its flag), the four quarters of the next S, the
+                // ring (wave 7: step t+3's entries from the registers loaded a step ago, the load for
+                // t+4 lands during the next step); after h2 gathered: W_hh2·h2
                 wait_flag(f1got, tag);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (wave == 4) {
@@ -547,6 +549,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
                     XSTAMPW(10, 4);
                 }
                 gather_terms(t + 1);
+                XSTAMPW(11, 5);
                 if (wave == 7) {
                     if (t + 3 <= t_terms && lane < kSTerms / 4) reinterpret_cast<f4v *>(RING(t + 3))[lane] = wg[0];
                     if (t + 3 < a.L && lane < 11)
