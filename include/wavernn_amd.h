@@ -185,6 +185,16 @@ int wrnn_generate_frames(wrnn_t *h, const wrnn_upsample_cfg *ucfg, const float *
                          int target, int overlap, const float *noise, uint64_t seed, int64_t row_offset, float *out,
                          int32_t *labels, void *stream);
 
+/* wrnn_generate_frames for the loop rows [row_begin, row_begin + row_count) of that launch only
+ * (round-5 addition, same ABI): e.g. a contiguous block of one long utterance's folds on one GPU
+ * of a node (wavernn_amd/sharding.py generate_sharded_folds).  The rows keep their
+ * place in the utterance (row r = fold r % nf of utterance r / nf); noise [steps][row_count][K],
+ * out / labels [row_count][steps]; row_offset keys the Philox draws of launch row j as
+ * row_offset + j (pass the global row id of row_begin). */
+int wrnn_generate_frames_rows(wrnn_t *h, const wrnn_upsample_cfg *ucfg, const float *mel, const float *aux, int U,
+                              int T, int target, int overlap, int row_begin, int row_count, const float *noise,
+                              uint64_t seed, int64_t row_offset, float *out, int32_t *labels, void *stream);
+
 /* The frame weights wrnn_generate_frames uses (host, stateless): mel_up(p) = Σ_k coef[φ][k] ·
  * mel[f + k + jlo] for p = f·hop + φ, 0 <= k < nJ — the Stretch2d/Conv2d cascade's response to
  * one frame, float64 rounded to fp32.  coef (nullable) [hop][nJ], coef_cap floats.

@@ -18,7 +18,7 @@ STATUS = {0: "WRNN_OK", -1: "WRNN_EINVAL", -2: "WRNN_EHIP", -3: "WRNN_ENOWEIGHTS
 # Every symbol include/wavernn_amd.h declares (tests check the .so exports all of them).
 EXPORTS = ("wrnn_create", "wrnn_set_weights", "wrnn_generate", "wrnn_check", "wrnn_elapsed_ms",
            "wrnn_query", "wrnn_last_error", "wrnn_destroy", "wrnn_cond_shape", "wrnn_upsample_pack",
-           "wrnn_postprocess", "wrnn_cond_last_error", "wrnn_generate_frames",
+           "wrnn_postprocess", "wrnn_cond_last_error", "wrnn_generate_frames", "wrnn_generate_frames_rows",
            "wrnn_frame_weights", "wrnn_melresnet_floats", "wrnn_melresnet")
 
 
@@ -94,6 +94,9 @@ def lib() -> ctypes.CDLL:
     L.wrnn_generate_frames.argtypes = [vp, ctypes.POINTER(UpsampleCfg), vp, vp, i32, i32, i32, i32, vp, u64, i64, vp,
                                        vp, vp]
     L.wrnn_generate_frames.restype = i32
+    L.wrnn_generate_frames_rows.argtypes = [vp, ctypes.POINTER(UpsampleCfg), vp, vp, i32, i32, i32, i32, i32, i32, vp,
+                                            u64, i64, vp, vp, vp]
+    L.wrnn_generate_frames_rows.restype = i32
     L.wrnn_frame_weights.argtypes = [ctypes.POINTER(UpsampleCfg), pi, pi, pi, vp, i32]
     L.wrnn_frame_weights.restype = i32
     L.wrnn_melresnet_floats.argtypes = [ctypes.POINTER(MelResNetCfg)]

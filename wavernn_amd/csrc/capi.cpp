@@ -1674,6 +1674,7 @@ int generate_split(wrnn_t *h, const float *cond, int B, int L, const float *nois
 struct FrameSrc {
     const float *mel = nullptr, *aux = nullptr;   // [U][feat][NF], [U][4·aux][NF] (device)
     int U = 0, NF = 0, nf = 1, stride = 0;
+    int rb = 0;                                   // launch row j is row rb + j of the U·nf (wrnn_generate_frames_rows)
     int hop = 1, nJ = 1, jlo = 0;
     const float *coef = nullptr;                  // [hop][nJ] (device)
 };
@@ -1805,7 +1806,7 @@ int generate_xcd_rows(wrnn_t *h, const float *cond, const FrameSrc *fs, int B, i
             const int rows = std::min(Lc + 1, L - t0);     // terms rows: steps [t0, t0 + rows)
             if (fs) {
                 HIP_TRY(h, launch_terms_interp(h->d_FT, h->d_AT, fs->coef, h->d_T, N, fs->U, fs->NF, fs->NF + fs->nJ - 1,
-                                               fs->hop, fs->nJ, fs->nf, fs->stride, b0, nb, t0, rows, st));
+                                               fs->hop, fs->nJ, fs->nf, fs->stride, fs->rb + b0, nb, t0, rows, st));
             } else {
                 HIP_TRY(h, launch_pack_cond_input(cond, h->CD, B, b0, nb, t0, rows, h->KXc, h->d_X, st));
                 if (rocblas_sgemm(h->blas, rocblas_operation_transpose, rocblas_operation_none, N, rows * nb, h->KXc,
@@ -1913,7 +1914,7 @@ int generate_xcdm(wrnn_t *h, const float *cond, const FrameSrc *fs, int B, int L
                 return fail(h, WRNN_EINVAL, "xcdm: terms workspace too small");
             if (fs) {
                 HIP_TRY(h, launch_terms_interp(h->d_FT, h->d_AT, fs->coef, h->d_T, N, fs->U, fs->NF, fs->NF + fs->nJ - 1,
-                                               fs->hop, fs->nJ, fs->nf, fs->stride, b0, nb, t0, Lc, st));
+                                               fs->hop, fs->nJ, fs->nf, fs->stride, fs->rb + b0, nb, t0, Lc, st));
             } else {
                 HIP_TRY(h, launch_pack_cond_input(cond, h->CD, B, b0, nb, t0, Lc, h->KXc, h->d_X, st,
                                                   h->cfg.feat_dims + h->cfg.aux_dims));
@@ -2462,6 +2463,14 @@ int wrnn_frame_weights(const wrnn_upsample_cfg *ucfg, int *hop, int *nJ, int *jl
 int wrnn_generate_frames(wrnn_t *h, const wrnn_upsample_cfg *ucfg, const float *mel, const float *aux, int U, int T,
                          int target, int overlap, const float *noise, uint64_t seed, int64_t row_offset, float *out,
                          int32_t *labels, void *stream) {
+    return wrnn_generate_frames_rows(h, ucfg, mel, aux, U, T, target, overlap, 0, -1, noise, seed, row_offset, out,
+                                     labels, stream);
+}
+
+// row_count < 0: every row of the launch (wrnn_generate_frames)
+int wrnn_generate_frames_rows(wrnn_t *h, const wrnn_upsample_cfg *ucfg, const float *mel, const float *aux, int U,
+                              int T, int target, int overlap, int row_begin, int row_count, const float *noise,
+                              uint64_t seed, int64_t row_offset, float *out, int32_t *labels, void *stream) {
     if (!h) return WRNN_EINVAL;
     if (!h->ready) return fail(h, WRNN_ENOWEIGHTS, "weights not (fully) set");
     if (h->dm) return fail(h, WRNN_EINVAL, "deepmind handles take no conditioning (wrnn_generate)");
@@ -2470,9 +2479,16 @@ int wrnn_generate_frames(wrnn_t *h, const wrnn_upsample_cfg *ucfg, const float *
     if (ucfg->feat_dims != h->cfg.feat_dims || ucfg->res_out_dims != h->CD - h->cfg.feat_dims)
         return fail(h, WRNN_EINVAL, "upsample config does not match the handle's feat / aux dims");
     if (ucfg->res_out_dims > 0 && !aux) return fail(h, WRNN_EINVAL, "need aux (MelResNet output)");
-    int L = 0, B = 0;
-    if (int rc = wrnn_cond_shape(ucfg, U, T, target, overlap, &L, &B))
+    int L = 0, Ball = 0;
+    if (int rc = wrnn_cond_shape(ucfg, U, T, target, overlap, &L, &Ball))
         return fail(h, rc, std::string("conditioning shape: ") + wrnn_cond_last_error());
+    if (row_count < 0) {
+        row_begin = 0;
+        row_count = Ball;
+    }
+    if (row_begin < 0 || row_count < 1 || row_begin + row_count > Ball)
+        return fail(h, WRNN_EINVAL, "rows [row_begin, row_begin + row_count) outside the launch's " + std::to_string(Ball));
+    const int B = row_count;
     HIP_TRY(h, hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
     const LoopPath path = choose_path(h, B);
@@ -2485,10 +2501,18 @@ int wrnn_generate_frames(wrnn_t *h, const wrnn_upsample_cfg *ucfg, const float *
         frames = N % 4 == 0;
     }
     if (!frames) {   // the per-sample conditioning (wrnn_upsample_pack) into a handle workspace
-        if (grow(h, h->d_cond, h->cond_cap, (size_t)L * B * h->CD)) return WRNN_EHIP;
+        const size_t rec = (size_t)h->CD * sizeof(float);
+        if (grow(h, h->d_cond, h->cond_cap, (size_t)L * (Ball + (B < Ball ? B : 0)) * h->CD)) return WRNN_EHIP;
         if (int rc = wrnn_upsample_pack(ucfg, mel, aux, U, T, target, overlap, h->d_cond, stream))
             return fail(h, rc, std::string("upsample_pack: ") + wrnn_cond_last_error());
-        return run_loop(h, path, h->d_cond, nullptr, B, L, noise, seed, row_offset, out, labels, st);
+        const float *cond = h->d_cond;
+        if (B < Ball) {   // the rows' records, compacted after the launch's [L][Ball] block
+            float *sub = h->d_cond + (size_t)L * Ball * h->CD;
+            HIP_TRY(h, hipMemcpy2DAsync(sub, B * rec, h->d_cond + (size_t)row_begin * h->CD, Ball * rec, B * rec, L,
+                                        hipMemcpyDeviceToDevice, st));
+            cond = sub;
+        }
+        return run_loop(h, path, cond, nullptr, B, L, noise, seed, row_offset, out, labels, st);
     }
     if (coef != h->coef_host) {
         if (grow(h, h->d_coef, h->coef_cap, coef.size())) return WRNN_EHIP;
@@ -2500,7 +2524,8 @@ int wrnn_generate_frames(wrnn_t *h, const wrnn_upsample_cfg *ucfg, const float *
     fs.aux = aux;
     fs.U = U;
     fs.NF = T;
-    fs.nf = B / U;
+    fs.nf = Ball / U;
+    fs.rb = row_begin;
     fs.stride = target > 0 ? target + overlap : 0;
     fs.coef = h->d_coef;
     return run_loop(h, path, nullptr, &fs, B, L, noise, seed, row_offset, out, labels, st);

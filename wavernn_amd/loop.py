@@ -180,12 +180,14 @@ class FatchordLoop:
 
     def generate_frames(self, spec, mel: torch.Tensor, aux: torch.Tensor, target: int = 0, overlap: int = 0,
                         noise: Optional[torch.Tensor] = None, seed: int = 0, row_offset: int = 0,
-                        want_labels: bool = False, stream=None,
-                        check: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+                        want_labels: bool = False, stream=None, check: bool = True,
+                        rows: Optional[Tuple[int, int]] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
         """The loop from the generate() inputs at frame rate (C-ABI wrnn_generate_frames):
         mel [U][feat][T], aux [U][4·aux][T] (MelResNet of the padded mel) fp32 on this GPU, with
         `spec` the UpsampleNetwork's condition.UpsampleSpec → samples [rows][steps] (+ labels),
-        rows / steps as condition.upsample_pack would lay them out (target <= 0: unbatched)."""
+        rows / steps as condition.upsample_pack would lay them out (target <= 0: unbatched).
+        `rows=(begin, count)`: only those rows of the launch (wrnn_generate_frames_rows; e.g. a
+        block of one utterance's folds), keyed row_offset + j."""
         for name, t in (("mel", mel), ("aux", aux)):
             if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.dim() == 3):
                 raise ValueError(f"{name} must be a contiguous fp32 CUDA tensor [U][C][T]")
@@ -199,7 +201,10 @@ class FatchordLoop:
                 ap[:, j * Ap:j * Ap + A] = aux[:, j * A:(j + 1) * A]
             aux = ap
             spec = spec.with_res_out(4 * Ap)
-        steps, rows = spec.shape(U, T, target, overlap)
+        steps, n_rows = spec.shape(U, T, target, overlap)
+        r0, rows = (0, n_rows) if rows is None else (int(rows[0]), int(rows[1]))
+        if r0 < 0 or rows < 1 or r0 + rows > n_rows:
+            raise ValueError(f"rows [{r0}, {r0 + rows}) outside the launch's {n_rows}")
         if noise is not None:
             if not (noise.is_cuda and noise.dtype == torch.float32 and noise.is_contiguous()):
                 raise ValueError("noise must be a contiguous fp32 CUDA tensor [L][B][K]")
@@ -211,10 +216,11 @@ class FatchordLoop:
             labels = torch.empty(rows, steps, dtype=torch.int32, device=mel.device)
         if stream is None:
             stream = torch.cuda.current_stream(mel.device).cuda_stream
-        rc = nat.lib().wrnn_generate_frames(self._h, ctypes.byref(spec.cfg), mel.data_ptr(), aux.data_ptr(), U, T,
-                                            target, overlap, noise.data_ptr() if noise is not None else None,
-                                            ctypes.c_uint64(seed & (2 ** 64 - 1)), row_offset, out.data_ptr(),
-                                            labels.data_ptr() if labels is not None else None, stream)
+        rc = nat.lib().wrnn_generate_frames_rows(self._h, ctypes.byref(spec.cfg), mel.data_ptr(), aux.data_ptr(), U,
+                                                 T, target, overlap, r0, rows,
+                                                 noise.data_ptr() if noise is not None else None,
+                                                 ctypes.c_uint64(seed & (2 ** 64 - 1)), row_offset, out.data_ptr(),
+                                                 labels.data_ptr() if labels is not None else None, stream)
         nat.check(self._h, rc)
         if check:
             self.check(stream)

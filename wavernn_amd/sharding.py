@@ -146,13 +146,17 @@ def generate_sharded_folds(model, mel, target: int, overlap: int, mu_law: bool, 
     if fold_fn is None:
         if device is None:
             device = next(model.parameters()).device
-        cond, wave_len = model.conditioning(mel, True, target, overlap)
-        n_folds = cond.shape[1]
+        # the frame-rate inputs only (mel + MelResNet output: kilobytes), then the loop entry for
+        # this rank's folds — the same conditioning-terms route as generate(batched=True), never
+        # the whole utterance's per-sample records on every rank
+        mel_f, aux, wave_len = model.frames(mel)
+        spec = model._upsample_spec()
+        n_folds = model.rows_of(np.shape(mel)[-1], True, target, overlap)
         mu = mu_law if model.mode == 'RAW' else False
 
         def fold_fn(ii):
-            y, _ = model.loop_handle().generate(cond[:, ii[0]:ii[-1] + 1].contiguous(), seed=base_seed,
-                                                row_offset=ii[0])
+            y, _ = model.loop_handle().generate_frames(spec, mel_f, aux, target, overlap, seed=base_seed,
+                                                       row_offset=ii[0], rows=(ii[0], len(ii)))
             return y.cpu().numpy()
 
         def post_fn(y_all):
