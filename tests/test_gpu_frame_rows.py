@@ -1,9 +1,10 @@
 """wrnn_generate_frames_rows: a block of a launch's rows (one utterance's folds on one GPU of a
 node, sharding.generate_sharded_folds) equals those rows of the whole launch, keyed by their
 global row id.  RAW labels exactly (the many-row kernel at every row count); MoL within the
-parity tolerance (a different row count can pick the other XCD kernel); the per-sample fallback
-(WRNN_NO_FRAME_TERMS=1: the launch's records compacted to the block's rows) bit for bit when the
-kernel is the same."""
+parity tolerance — a different row count can pick the other XCD kernel, and the rocBLAS terms
+GEMM over the block's records (the per-sample fallback, WRNN_NO_FRAME_TERMS=1: the launch's
+records compacted to the block's rows) tiles by its row count (observed: not bit-identical at
+15 of 16 rows on the same kernel)."""
 import numpy as np
 import pytest
 import torch
@@ -37,15 +38,12 @@ def test_frame_rows_block_equals_whole_launch(mode, frames, monkeypatch):
     full, lab_full = loop.generate_frames(spec, mel_f, aux, target, overlap, seed=11, want_labels=mode == "RAW")
     n = full.shape[0]
     assert n >= 12
-    path_full = loop.info["last_path"]
     for r0, cnt in ((0, n), (2, 5), (n - 3, 3), (1, n - 1)):
         y, lab = loop.generate_frames(spec, mel_f, aux, target, overlap, seed=11, row_offset=r0,
                                       want_labels=mode == "RAW", rows=(r0, cnt))
         assert y.shape == (cnt, full.shape[1])
         if mode == "RAW":
             assert torch.equal(lab, lab_full[r0:r0 + cnt]), (r0, cnt)
-        elif loop.info["last_path"] == path_full and not frames:
-            assert torch.equal(y, full[r0:r0 + cnt]), (r0, cnt)
         else:
             assert (y - full[r0:r0 + cnt]).abs().max().item() <= gf.MOL_TOL, (r0, cnt)
     with pytest.raises(ValueError):
