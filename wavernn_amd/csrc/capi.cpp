@@ -1446,8 +1446,11 @@ int generate_rows(wrnn_t *h, const float *cond, int B, int L, const float *noise
 
 // deepmind_version: B rows (utterances) in row groups of <= kRowsMax, one launch each
 // deepmind rows through the XCD-resident kernel: up to kDxRowsMax rows per launch (launch row r
-// on XCD r % 8); Philox draws precomputed per time chunk (≤ WRNN_DM_NOISE_MB, default 64 MiB, so a
-// chunk's draws stay in the Infinity Cache); the recurrent state carried per workgroup in d_dxstate.
+// on XCD r % 8); Philox draws precomputed per time chunk (≤ WRNN_DM_NOISE_MB, default 2 GiB: config
+// 5's 32 rows × 16 000 steps are 1 GiB of draws, one fill and ONE persistent launch — with 64 MiB
+// chunks the call was 16 launches, ≈ 0.24 µs per step of relaunch, prologue and fill; the draws of
+// a step are read once per XCD, ≈ 10 GB/s from HBM, so they need not stay in the Infinity Cache);
+// the recurrent state carried per workgroup in d_dxstate.
 int generate_dx(wrnn_t *h, int B, int L, const float *noise, uint64_t seed, int64_t row_offset, float *out,
                 int32_t *labels, hipStream_t st) {
     const size_t xg_words = (size_t)kXcds * kDxXcdStride;
@@ -1455,7 +1458,7 @@ int generate_dx(wrnn_t *h, int B, int L, const float *noise, uint64_t seed, int6
     if (!h->d_dxxg) HIP_TRY(h, hipMalloc(&h->d_dxxg, xg_words * 8));
     if (!h->d_dxstate) HIP_TRY(h, hipMalloc(&h->d_dxstate, (size_t)kXcds * kXcdWgs * kDxStateW * sizeof(float)));
     const char *mb_env = std::getenv("WRNN_DM_NOISE_MB");
-    const double budget = (mb_env ? std::atof(mb_env) : 64.0) * (1 << 20) / 4.0;   // floats
+    const double budget = (mb_env ? std::atof(mb_env) : 2048.0) * (1 << 20) / 4.0;   // floats
     const char *dbg_env = std::getenv("WRNN_DEBUG_STAMPS");
     const int dbg_steps = (dbg_env && std::atoi(dbg_env) > 0 && L >= kDxDbgSkip + kDxDbgSteps) ? kDxDbgSteps : 0;
     const size_t dbg_n = (size_t)kXcds * kXcdWgs * kDxWaves * dbg_steps * kDxStamps;
