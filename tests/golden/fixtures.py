@@ -77,3 +77,18 @@ def dm_inputs(fx: dict):
     assert syn.state_digest(state) == str(fx["state_sha"]), "synthetic weight generator drifted"
     assert syn.digest(noise) == str(fx["noise_sha"]), "synthetic noise drifted"
     return d, state, noise
+
+TRAIN_CASES = ["train_mol", "train_raw"]
+
+
+def train_inputs(fx: dict):
+    """(dims, state, mel [B][feat][T + 2·pad], x [B][T·hop]) of a training-forward fixture."""
+    d = dims_of(fx)
+    state = syn.make_fatchord_state(d, int(fx["wseed"]))
+    g = np.random.default_rng(int(fx["xseed"]))
+    B, T = int(fx["B"]), int(fx["T"])
+    mel = g.uniform(0, 1, (B, d.feat_dims, T + 2 * d.pad)).astype(np.float32)
+    x = g.uniform(-1, 1, (B, T * d.hop_length)).astype(np.float32)
+    assert syn.state_digest(state) == str(fx["state_sha"]), "synthetic weight generator drifted"
+    assert syn.digest(mel, x) == str(fx["x_sha"]), "synthetic training inputs drifted"
+    return d, state, mel, x

@@ -288,6 +288,43 @@ def gen_case(fv, name, d: syn.FatchordDims, T: int, batched: bool, target: int, 
     return rec
 
 
+# ---------------------------------------------------------------------- training forward
+def train_case(fv, name, d: syn.FatchordDims, B=2, T=4, wseed=5, xseed=3, out_stride=1, n_grad=256):
+    """The reference's teacher-forced forward (fatchord_version.py:131-167) and the backward of
+    mean(y²) (§8(f)4): eval-mode output (BatchNorm running statistics), train-mode output (batch
+    statistics), and per parameter the L2 norm and the first n_grad values of its gradient."""
+    state = syn.make_fatchord_state(d, wseed)
+    g = np.random.default_rng(xseed)
+    mel = g.uniform(0, 1, (B, d.feat_dims, T + 2 * d.pad)).astype(np.float32)
+    x = g.uniform(-1, 1, (B, T * d.hop_length)).astype(np.float32)
+    model = build_ref_model(fv, d, state)
+    t0 = time.time()
+    model.eval()
+    with torch.no_grad():
+        y_eval = model(torch.from_numpy(x), torch.from_numpy(mel)).numpy()
+    model.train()
+    y = model(torch.from_numpy(x), torch.from_numpy(mel))
+    loss = y.square().mean()
+    loss.backward()
+    dt = time.time() - t0
+    rec = dict(kind="train", mode=d.mode, B=B, T=T, wseed=wseed, xseed=xseed, dims=np.array(repr(d)),
+               ref_seconds=dt, state_sha=syn.state_digest(state), x_sha=syn.digest(mel, x),
+               out_stride=np.int64(out_stride), y_eval=y_eval[:, ::out_stride].copy(),
+               y_train=y.detach().numpy()[:, ::out_stride].copy(), loss=np.float64(loss.item()))
+    names, norms, heads = [], [], []
+    for n, p in model.named_parameters():
+        if p.grad is None:
+            continue
+        gr = p.grad.detach().numpy().astype(np.float64).ravel()
+        names.append(n)
+        norms.append(np.sqrt((gr * gr).sum()))
+        heads.append(np.pad(gr[:n_grad], (0, max(0, n_grad - gr.size))))
+    rec["grad_names"] = np.array(names)
+    rec["grad_norms"] = np.array(norms)
+    rec["grad_heads"] = np.stack(heads).astype(np.float32)
+    return rec
+
+
 def cases():
     M, R = syn.DEFAULT_MOL, syn.DEFAULT_RAW
     return {
@@ -320,6 +357,9 @@ def cases():
         "gen_mol_60s_batched": ("gen", dict(d=M, T=4811, batched=True, target=11000, overlap=550,
                                             mu_law=True, cond_stride=2750, out_stride=32,
                                             raw_rows=(0, 57, 114), raw_stride=50)),
+        # the training-side teacher-forced forward + backward (§8(f)4)
+        "train_mol": ("train", dict(d=M, out_stride=2)),
+        "train_raw": ("train", dict(d=R, out_stride=16)),
         # deepmind_version dual softmax (config 5 model), batch 1 as the reference generates
         "dm_b1": ("dm", dict(d=syn.DEFAULT_DM, L=2000)),
         "dm_tiny_b1": ("dm", dict(d=syn.TINY_DM, L=3000)),
@@ -334,7 +374,7 @@ def main(argv):
     names = argv or list(todo)
     for name in names:
         kind, kw = todo[name]
-        fn = {"loop": loop_case, "gen": gen_case, "dm": dm_case}[kind]
+        fn = {"loop": loop_case, "gen": gen_case, "dm": dm_case, "train": train_case}[kind]
         rec = fn(fv, name, **kw)
         path = os.path.join(HERE, name + ".npz")
         np.savez_compressed(path, **{k: np.asarray(v) for k, v in rec.items()})

@@ -103,3 +103,17 @@ def test_deepmind_training_forward_on_gpu():
     outg = gpu(prev_y.to(DEV), prev_hidden.to(DEV), current_coarse.to(DEV))
     for a, b in zip(outc, outg):
         assert (b.detach().cpu() - a.detach()).abs().max().item() <= 1e-5
+
+
+@pytest.mark.parametrize("name", ["train_mol", "train_raw"])
+def test_training_forward_backward_on_miopen_vs_reference(name, deterministic):
+    """The same forward + backward on the MI355X (MIOpen GRU, deterministic algorithms) against the
+    REFERENCE's own CPU outputs and gradients (tests/golden train_* fixtures): eval and train
+    outputs within 1e-4, the loss within 1e-4 relative, each gradient's first values and norm
+    within 1.5e-3 of its largest |value| / its norm (the bound of the CPU-module test above)."""
+    from tests.golden import fixtures as gf
+    from tests.test_train_golden import check, run
+    fx = gf.load(name)
+    y_eval, y_train, loss, grads = run(fx, device=DEV)
+    worst = check(fx, y_eval, y_train, loss, grads, out_tol=1e-4, loss_rtol=1e-4, grad_rtol=1.5e-3)
+    print(f"\n{name}: largest relative gradient error vs the reference {worst:.2e}")
