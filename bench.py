@@ -466,6 +466,10 @@ def stub_main(args, world, rank):
 def main():
     args = parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one rank per GPU: two ranks' persistent launches cannot share a GPU (each needs every CU
+        # co-resident), so refuse rather than time out (device_count() does not initialise the GPU)
+        if not args.stub and torch.cuda.device_count() < args.gpus:
+            sys.exit(f"bench.py --gpus {args.gpus}: only {torch.cuda.device_count()} GPU(s) visible")
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
