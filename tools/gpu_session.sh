@@ -2,7 +2,7 @@
 # One GPU session: parity suite, the headline bench exactly as the driver runs it (its
 # own live PMC passes included), rocprofv3 kernel-trace summaries of the bench and of the headline
 # alone.  Stops at the first step that ends abnormally (fault / abort / timeout), per the pool rules.
-#   tools/gpu_r04.sh [pytest -k expression]
+#   tools/gpu_session.sh [pytest -k expression]   (SKIP_TESTS / SKIP_BENCH / SKIP_PMC / SKIP_PROF=1 skip a step)
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 R=$(pwd)
 mkdir -p gpurun_out
@@ -19,6 +19,15 @@ if [ -z "$SKIP_BENCH" ]; then
   rc=$?; echo "bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
   tail -1 gpurun_out/bench.log > gpurun_out/bench.json
   cut -c1-400 gpurun_out/bench.json
+fi
+if [ -z "$SKIP_PMC" ]; then
+  # the HBM traffic passes on their own (one counter per pass), summarised like bench.py's live ones
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 300 rocprofv3 --pmc $c -d "$R/gpurun_out/pmc_$c" -o pmc --output-format csv -- \
+        python "$R/bench.py" --pmc-child > gpurun_out/pmc_$c.log 2>&1
+    rc=$?; echo "pmc $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  done
+  python tools/pmc_summary.py gpurun_out gpurun_out/pmc_traffic.json > /dev/null && echo "pmc summary ok"
 fi
 if [ -z "$SKIP_PROF" ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o bench --output-format csv -- \
