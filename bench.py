@@ -162,7 +162,8 @@ def other_configs(dev, warm: bool = True, cpu_steps: int = 0, threads: int = 1) 
     post-processing included), synthetic inputs, random weights of each architecture:
       1: RAW 9-bit generate(), 1 s unbatched and 5 s fold-batched;
       3: MoL fold-batched generate() of one 60 s utterance (115 folds x 12 100 steps);
-    plus the headline architecture serving 8 utterances at once (generate_many, one per XCD).
+    plus the headline architecture serving 8 utterances at once (generate_many, one per XCD) and
+    32 at once (the many-row kernel, 4 per XCD: aggregate serving throughput).
     Configs 4 and 5 are utterance batches sharded over the ranks: `sharded_configs`.
     `warm` = an untimed first call per config (the PMC child runs each config once)."""
     res = {}
@@ -187,6 +188,22 @@ def other_configs(dev, warm: bool = True, cpu_steps: int = 0, threads: int = 1) 
                                 "note": "8 independent 5 s utterances, unbatched, WaveRNN.generate_many (ONE launch of "
                                         "fatchord_xcd_kernel, one utterance per XCD); rate over the whole call "
                                         "(upsample, loop, float64 post)"}
+    # serving throughput: 32 concurrent unbatched utterances (4 per XCD on the many-row MFMA kernel) —
+    # per-stream latency traded for aggregate rate
+    mels = [torch.from_numpy(syn.make_mel(d.feat_dims, T5, 140 + i))[None] for i in range(32)]
+    if warm:
+        model.generate_many(mels, None, False, 11000, 550, True, seed=1)
+    outs, dt = _timed(lambda: model.generate_many(mels, None, False, 11000, 550, True, seed=2))
+    ms = model.loop_handle().elapsed_ms()
+    n = sum(o.shape[0] for o in outs)
+    res["config2_32_streams"] = {"samples_per_s": n / dt, "rtf_per_gpu": n / dt / sr, "rtf_per_stream": n / 32 / dt / sr,
+                                 "rows": 32, "loop_steps": L2, "device_ms": ms, "wall_s": dt,
+                                 "us_per_loop_step": ms * 1e3 / L2, "kernel_path": model.loop_handle().info["last_path"],
+                                 "roofline": hbm_roofline(loop_weight_bytes(d) + 32 * COND_BYTES_PER_ROW_STEP,
+                                                          ms * 1e3 / L2, "as config2_8_streams"),
+                                 "note": "32 independent 5 s utterances, unbatched (batch-1 streams), one "
+                                         "WaveRNN.generate_many launch of fatchord_xcdm_kernel (4 rows per XCD): "
+                                         "aggregate serving rate over the whole call"}
     del model
     # config 1's model (RAW 9-bit, rnn 512) on the GPU through the drop-in generate(): 1 s unbatched
     # (the reference runs it on the CPU) and a 5 s utterance fold-batched

@@ -34,6 +34,7 @@ def test_summary_picks_the_headline_dispatch_and_sums_the_configs(tmp_path):
             ("void wrnn::fatchord_xcdm_kernel<1, false, true>(wrnn::XcdmArgs)", 7.0 * scale, 100),   # RAW
             ("void wrnn::fatchord_xcdm_kernel<4, false, false>(wrnn::XcdmArgs)", 40.0 * scale, 50),
             ("void wrnn::fatchord_xcdm_kernel<4, false, false>(wrnn::XcdmArgs)", 60.0 * scale, 50),
+            ("void wrnn::fatchord_xcdm_kernel<1, false, false>(wrnn::XcdmArgs)", 20.0 * scale, 70),  # 32 streams
             ("void wrnn::fatchord_xcds_kernel<false>(wrnn::XcdsArgs)", 11.0 * scale, 50),
             ("void wrnn::deepmind_xcd_kernel<false>(wrnn::DxArgs)", 13.0 * scale, 50),
         ])
@@ -43,5 +44,7 @@ def test_summary_picks_the_headline_dispatch_and_sums_the_configs(tmp_path):
     cfg = out["other_configs"]
     assert cfg["config2_8_streams"]["bytes_per_step"] == 1024.0 * (2 * 900.0 + 450.0) / 110275
     assert cfg["config3_mol_fold_60s"]["bytes_per_step"] == 1024.0 * (2 * 100.0 + 50.0) / 12100
+    assert cfg["config2_32_streams"]["bytes_per_step"] == 1024.0 * (2 * 20.0 + 10.0) / 110275
+    assert cfg["config3_mol_fold_60s"]["kernel"] == "fatchord_xcdm_kernel"
     assert cfg["config4_sparse896_8utt"]["fetch_kib"] == 11.0
     assert cfg["config5_deepmind_32utt"]["write_kib"] == 6.5

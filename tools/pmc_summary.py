@@ -24,7 +24,8 @@ HEADLINE = ("fatchord_xcd_kernel", "fatchord_split_kernel", "fatchord_loop_kerne
 # bench.py --pmc-child run: every config generated ONCE, no warm-up calls, no fold-batched line).
 # The headline is the FIRST headline-kernel dispatch; later fatchord_xcd_kernel dispatches are the
 # 8-utterance line (config2_8_streams).
-OTHER = {"fatchord_xcdm_kernel": ("config3_mol_fold_60s", 12100),
+OTHER = {"fatchord_xcdm_kernel<4,": ("config3_mol_fold_60s", 12100),       # 115 rows: 4 quads per XCD
+         "fatchord_xcdm_kernel<1,": ("config2_32_streams", 110275),        # 32 rows: 1 quad per XCD
          "fatchord_xcds_kernel": ("config4_sparse896_8utt", 110275),
          "deepmind_rows_kernel": ("config5_deepmind_32utt", 16000),
          "deepmind_xcd_kernel": ("config5_deepmind_32utt", 16000),
@@ -80,7 +81,7 @@ def summarise(src):
         if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
             key, steps = OTHER[k]
             b = 1024.0 * (2.0 * v["FETCH_SIZE"] + v["WRITE_SIZE"])
-            cfg[key] = {"kernel": k, "fetch_kib": v["FETCH_SIZE"], "write_kib": v["WRITE_SIZE"], "loop_steps": steps,
+            cfg[key] = {"kernel": k.rstrip("<,"), "fetch_kib": v["FETCH_SIZE"], "write_kib": v["WRITE_SIZE"], "loop_steps": steps,
                         "bytes_per_step": b / steps}
     return {
         "workload": "MOL rnn512 B=1 5 s (110275 steps), one persistent launch",
