@@ -81,7 +81,7 @@ def summarise(src):
         if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
             key, steps = OTHER[k]
             b = 1024.0 * (2.0 * v["FETCH_SIZE"] + v["WRITE_SIZE"])
-            cfg[key] = {"kernel": k.rstrip("<,"), "fetch_kib": v["FETCH_SIZE"], "write_kib": v["WRITE_SIZE"], "loop_steps": steps,
+            cfg[key] = {"kernel": k.split("<")[0], "fetch_kib": v["FETCH_SIZE"], "write_kib": v["WRITE_SIZE"], "loop_steps": steps,
                         "bytes_per_step": b / steps}
     return {
         "workload": "MOL rnn512 B=1 5 s (110275 steps), one persistent launch",
