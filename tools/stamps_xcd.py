@@ -10,7 +10,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+from wavernn_amd import _native  # noqa: E402
 from wavernn_amd import synthetic as syn  # noqa: E402
+
+if os.environ.get("TIME_DM_LIB"):   # a diagnostic build (tools/build_alt.py)
+    _native.LIB_PATH = os.environ["TIME_DM_LIB"]
 from wavernn_amd.loop import FatchordLoop  # noqa: E402
 
 SPARSE_STAMPS = [(0, "start (after B1)"), (1, "GRU1 done (after B2)"), (2, "Y published (GRU2)"),
@@ -26,6 +30,9 @@ STAMPS = [(0, "start (after B1)"), (1, "GRU1 done (after B2)"), (2, "Y published
 
 
 def main(L=3000, sparse=0):
+    labels = dict(SPARSE_STAMPS if sparse else STAMPS)
+    if os.environ.get("GRU2_STAMPS"):   # the WRNN_XCDS_GRU2_STAMPS build: slots 12..14 inside GRU2
+        labels.update({12: "w0: GRU2 block-row dots", 13: "w0: GRU2 z/n exchanged", 14: "w0: GRU2 gate math"})
     os.makedirs("gpurun_out", exist_ok=True)
     path = "gpurun_out/stamps_xcd.bin"
     os.environ["WRNN_DEBUG_STAMPS"] = str(L)
@@ -51,7 +58,7 @@ def main(L=3000, sparse=0):
     print(f"xcd kernel L={L}: step period median {np.median(period):.3f} us (stamped build), "
           f"shader clock {np.median(clk):.3f} GHz (s_memtime / s_memrealtime)")
     print("-- median over steps of (min / median / max over the 32 workgroups), us")
-    for k, lab in (SPARSE_STAMPS if sparse else STAMPS):
+    for k, lab in sorted(labels.items(), key=lambda kv: (kv[0] > 8, kv[0])):
         x = rel[:, :, k]
         print(f"   {lab:28s} {np.median(x.min(0)):6.2f} {np.median(np.median(x, 0)):6.2f} {np.median(x.max(0)):6.2f}")
 

@@ -38,6 +38,9 @@ namespace wrnn {
 #ifndef WRNN_XCDS_DIAG
 #define WRNN_XCDS_DIAG 0   // timing diagnostics (wrong results): 1 skip the S gathers, 2 skip the h2 gather
 #endif
+#ifndef WRNN_XCDS_GRU2_STAMPS
+#define WRNN_XCDS_GRU2_STAMPS 0   // diagnostics: stamps 12..14 inside GRU2 (wave 0) instead of the ring / GH2 ones
+#endif
 
 // 8 rows of an (NK·128)-wide layer against a vector polled into registers by ONE wave: lane l
 // holds the pairs k = 0..NK-1 at granules 2(l + 64k) + {0, 1} (xk[k]) and the matching weights
@@ -117,8 +120,12 @@ __device__ __forceinline__ void sp_block_row(const f4v (&wa)[4], const f4v (&wb)
     }
 }
 
+// g[i] for a per-lane i in 0..3 as three v_cndmask (the nested ?: form compiled into exec-mask
+// branches: ≈ 30 scalar / branch instructions per call in the GRU2 epilogue)
 __device__ __forceinline__ float sel4(const float (&g)[4], int i) {
-    return i == 0 ? g[0] : i == 1 ? g[1] : i == 2 ? g[2] : g[3];
+    const float a = (i & 1) ? g[1] : g[0];
+    const float b = (i & 1) ? g[3] : g[2];
+    return (i & 2) ? b : a;
 }
 
 #define XSTAMPW(kk, w)                                                                                        \
@@ -385,23 +392,33 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
         XSTAMP(1);
         // ---- GRU2 (:212-214): engine q of wave ub → gate q of units 4ub..4ub+3 (W_ih2[:, :R]·h1)
         if (wave < kSUB) {
+            const float h1j = h1s[c * kSU + ul];   // (read before the dots: its latency off the chain)
             float g[4];
             sp_block_row(*reinterpret_cast<const f4v(*)[4]>(&wg[0]), *reinterpret_cast<const f4v(*)[4]>(&wg[4]), ja, jb,
                          h1s, g);
-            // engine 0 collects z (engine 1, permlane16 swap) and n (engine 2, permlane32 swap)
-            float gz[4], gn[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const auto s16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(g[r]), __float_as_uint(g[r]), false, false);
-                const auto s32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(g[r]), __float_as_uint(g[r]), false, false);
-                gz[r] = __uint_as_float(s16[1]);
-                gn[r] = __uint_as_float(s32[1]);
+            if (WRNN_XCDS_GRU2_STAMPS) {
+                asm volatile("" ::"v"(g[0]), "v"(g[1]), "v"(g[2]), "v"(g[3]));
+                XSTAMP(12);
             }
+            // every lane keeps its row (lane & 3) of its engine's gate; engine 0 collects z (engine 1,
+            // one permlane16 swap) and n (engine 2, one permlane32 swap) — lane l < 4 then holds
+            // r, z, n of unit 4ub + l (two swaps instead of one per row and gate)
             const int r4 = lane & 3;
-            const float h1j = h1s[c * kSU + ul];
-            const float hn = gru_gate_math(sel4(g, r4) + p2q[0], sel4(gz, r4) + p2q[1], sel4(gn, r4) + p2q[2], ghv[0],
-                                           ghv[1], ghv[2], h2own);
+            const float gs = sel4(g, r4);
+            const float gz = __uint_as_float(
+                __builtin_amdgcn_permlane16_swap(__float_as_uint(gs), __float_as_uint(gs), false, false)[1]);
+            const float gn = __uint_as_float(
+                __builtin_amdgcn_permlane32_swap(__float_as_uint(gs), __float_as_uint(gs), false, false)[1]);
+            if (WRNN_XCDS_GRU2_STAMPS) {
+                asm volatile("" ::"v"(gz), "v"(gn));
+                XSTAMP(13);
+            }
+            const float hn = gru_gate_math(gs + p2q[0], gz + p2q[1], gn + p2q[2], ghv[0], ghv[1], ghv[2], h2own);
             h2own = hn;
+            if (WRNN_XCDS_GRU2_STAMPS) {
+                asm volatile("" ::"v"(hn));
+                XSTAMP(14);
+            }
             // y = (x_I + h1) + h2 (:212, :216)
             const float y = (xi + h1j) + hn;
             if (lane < 4) xpub_b(xgr, XGI(XH_Y) + c * kSU + ul, tag, y);
@@ -555,12 +572,12 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
                     if (t + 3 < a.L && lane < 11)
                         NZ(t + 3)[lane] = mol_noise_term(a.noise ? wg[1].x : philox_noise(a.seed, prow, (uint32_t)(t + 3), (uint32_t)lane, 1), lane);
                     stage_ring(t + 4);
-                    XSTAMPW(12, 7);
+                    if (!WRNN_XCDS_GRU2_STAMPS) XSTAMPW(12, 7);
                 }
                 wait_flag(h2ready, tag);
                 gh2_dots(br0);
                 if (wq < 2) gh2_dots(br1);
-                XSTAMPW(13, 5);
+                if (!WRNN_XCDS_GRU2_STAMPS) XSTAMPW(13, 5);
             }
         }
         bar();
