@@ -67,7 +67,9 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int R = 512, TW = kXcdWgs * kXTerms;
     const XcdLds ll = xcd_lds_layout();
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 31, eng = lane >> 5;
+    const int tid = threadIdx.x, lane = tid & 63, li = lane & 31, eng = lane >> 5;
+    // the wave index wave-uniform (SGPR): its role branches become scalar, its offsets scalar operands
+    const int wave = WRNN_XCD_UNIFORM_WAVE ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
     float *whh1 = smem + ll.whh1, *whh2l = smem + ll.whh2, *f2x = smem + ll.f2x, *h1s = smem + ll.h1, *h2s = smem + ll.h2, *sg = smem + ll.sg, *w3s = smem + ll.w3;
     float *ring = smem + ll.ring, *nzr = smem + ll.nz, *gh2s = smem + ll.gh2, *cst = smem + ll.cst, *xs = smem + ll.xs;
     int *misc = reinterpret_cast<int *>(smem + ll.misc);

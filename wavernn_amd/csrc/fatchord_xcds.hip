@@ -140,7 +140,9 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int R = kSR, TW = kXcdWgs * kSTerms;
     const XcdsLds ll = xcds_lds_layout();
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, eng = lane >> 4;
+    const int tid = threadIdx.x, lane = tid & 63, li = lane & 15, eng = lane >> 4;
+    // the wave index wave-uniform (SGPR): its role branches become scalar, its offsets scalar operands
+    const int wave = WRNN_XCD_UNIFORM_WAVE ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
     float *h1s = smem + ll.h1, *h2s = smem + ll.h2, *sg = smem + ll.sg, *w3s = smem + ll.w3, *f2x = smem + ll.f2x;
     float *ring = smem + ll.ring, *nzr = smem + ll.nz, *gh2s = smem + ll.gh2, *cst = smem + ll.cst, *xs = smem + ll.xs;
     float *whh1b = smem + ll.whh1b, *whh2b = smem + ll.whh2b;

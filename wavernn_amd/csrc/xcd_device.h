@@ -12,6 +12,9 @@ namespace wrnn {
 #ifndef WRNN_XCD_ORDERED_ARGMAX
 #define WRNN_XCD_ORDERED_ARGMAX 1   // MoL argmax: value-only max over lanes 0..7 + ballot (0: index through DPP)
 #endif
+#ifndef WRNN_XCD_UNIFORM_WAVE
+#define WRNN_XCD_UNIFORM_WAVE 1   // the XCD kernels' wave index through readfirstlane (0: per-lane, A/B)
+#endif
 #ifndef WRNN_XCD_FAST_EXP
 #define WRNN_XCD_FAST_EXP 1     // sampler scale e^s by v_exp_f32 (A/B vs libm expf: 3.92 -> 3.88 us/step, parity unchanged)
 #endif
