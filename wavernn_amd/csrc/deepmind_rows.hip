@@ -230,7 +230,7 @@ __global__ __launch_bounds__(kDmThreads) void deepmind_rows_kernel(DmArgs a, DmG
     auto gates = [&](int h2, int par, int dhop, float *dst, const float *xcur, int t) {
         for (int i = tid; i < B * Uv; i += kCompute) {
             const int b = i / Uv, u = i - b * Uv, j = w * U + u;
-            const float x0 = pcv[b] / 127.5f - 1.0f, x1 = pfv[b] / 127.5f - 1.0f;   // (:106-108)
+            const float x0 = label_x(pcv[b]), x1 = label_x(pfv[b]);   // (:106-108)
             float *sb = st + b * SW;
             float I[3];
 #pragma unroll
@@ -240,7 +240,7 @@ __global__ __launch_bounds__(kDmThreads) void deepmind_rows_kernel(DmArgs a, DmG
                     I[g] = __fadd_rn(__fmul_rn(wi[0], x0), __fmul_rn(wi[1], x1));
                 } else {
                     const float *wi = W + s.if_ + (g * U + u) * 3;
-                    const float x2 = xcur[b] / 127.5f - 1.0f;                           // (:135-136)
+                    const float x2 = label_x(xcur[b]);                                    // (:135-136)
                     I[g] = __fadd_rn(__fadd_rn(__fmul_rn(wi[0], x0), __fmul_rn(wi[1], x1)), __fmul_rn(wi[2], x2));
                 }
             }

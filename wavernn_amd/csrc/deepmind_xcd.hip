@@ -37,6 +37,9 @@
 #include "wrnn_device.h"
 #include "xcd_device.h"
 
+#ifndef WRNN_DX_GATE_WAVE
+#define WRNN_DX_GATE_WAVE 0   // the wave whose lanes run the coarse / fine gates (3: A/B, slower)
+#endif
 #ifndef WRNN_DX_ORDERED_ARGMAX
 #define WRNN_DX_ORDERED_ARGMAX 1   // samplers: lane l holds classes 4l..4l+3, value-only max + ballot
 #endif
@@ -365,8 +368,11 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
     }
 
     // roles: gate threads (unit u, row n), 56 of them; O1/O3 epilogue (row r < 14, n); O2/O4 (r < 8, n)
-    const bool gate = tid < 4 * kDxU;
-    const int gu = tid % kDxU, gn = tid / kDxU;
+    // the gate threads are lanes 0..55 of wave WRNN_DX_GATE_WAVE (wave 3 instead of 0, so that
+    // wave 0's row-group-B share would not follow the gates: 6.63 → 6.68 µs/step at 32 rows,
+    // profiles/r05_ab_dx_gate_wave.log)
+    const bool gate = (tid >> 6) == WRNN_DX_GATE_WAVE && (tid & 63) < 4 * kDxU;
+    const int gu = (tid & 63) % kDxU, gn = (tid & 63) / kDxU;
     const int t_end = a.t0 + a.Lc;
     float *st = a.state + (size_t)(k * kXcdWgs + c) * kDxStateW;
     auto noise_src = [&](int t, int n) {
@@ -414,7 +420,7 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
     for (int t = a.t0; t < t_end; ++t) {
         int tid = threadIdx.x;   // opaque per step (see fatchord_xcdm.hip)
         asm volatile("" : "+v"(tid));
-        const int lane = tid & 63, gu = tid % kDxU, gn = tid / kDxU;
+        const int lane = tid & 63, gu = lane % kDxU, gn = lane / kDxU;
         const uint32_t tag = (uint32_t)t + 1u;
         const bool more = t + 1 < t_end;
         DST(0);
@@ -423,7 +429,7 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
                 (unsigned)__builtin_amdgcn_s_memrealtime();
         // ---- coarse gates (:106-125): R·h_{t-1} (partials of the previous step), I_coarse(prev)
         if (gate) {
-            const float x0 = lab[gn] / 127.5f - 1.0f, x1 = lab[4 + gn] / 127.5f - 1.0f;
+            const float x0 = label_x(lab[gn]), x1 = label_x(lab[4 + gn]);
             float I[3], Rg[3];
 #pragma unroll
             for (int g = 0; g < 3; ++g) {   // separately rounded products (:111)
@@ -440,8 +446,9 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             DSTR(22);   // (s_memrealtime: the h_c hop measured across workgroups, tools/stamps_dx.py)
         }
         // row group B (WG-local rows 48..83: fine gate rows only) of R·h_{t-1}, both halves from the
-        // still-staged h_c(t-1) / h_f(t-1) slices: waves 1..3 while wave 0 runs the coarse gates,
-        // wave 0 in its h_c hop wait; partials → LDS (summed in this step's O2 epilogue window)
+        // still-staged h_c(t-1) / h_f(t-1) slices: the other waves while the gate wave runs the
+        // coarse gates, the gate wave in its h_c hop wait; partials → LDS (summed in this step's O2
+        // epilogue window)
         if (t > a.t0) r_group_b();
         DST(1);
         // ---- h_c slice → O1 → relu → o1
@@ -563,8 +570,8 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         DST(9);
         // ---- fine gates (:135-145): I_fine(prev, c_t)
         if (gate) {
-            const float x0 = lab[gn] / 127.5f - 1.0f, x1 = lab[4 + gn] / 127.5f - 1.0f;
-            const float x2 = lab[8 + gn] / 127.5f - 1.0f;
+            const float x0 = label_x(lab[gn]), x1 = label_x(lab[4 + gn]);
+            const float x2 = label_x(lab[8 + gn]);
             float I[3], Rg[3];
 #pragma unroll
             for (int g = 0; g < 3; ++g) {   // (:137)

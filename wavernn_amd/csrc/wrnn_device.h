@@ -126,6 +126,16 @@ __device__ __forceinline__ void dots(const float *__restrict__ w0, int wstride, 
 // ≈1e-7 absolute error, inside the parity tolerance (the reference's SLEEF/MKL paths are not
 // correctly rounded either).  Samplers keep the accurate libm functions.
 __device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+// The deepmind input x = c / 127.5 − 1 of a label c ∈ {0, …, 255} (deepmind_version.py:106-108,
+// :135-136) with the IEEE quotient: one FMA correction of c·fl(1/127.5) rounds correctly for every
+// label (checked exhaustively, tests/test_label_x.py), 4 instructions instead of the division
+// sequence (v_div_scale / rcp / 5 FMAs / div_fmas / div_fixup) on the gates' critical path.
+__device__ __forceinline__ float label_x(float c) {
+    constexpr float r = 1.0f / 127.5f;
+    const float q0 = c * r;
+    const float e = __builtin_fmaf(-q0, 127.5f, c);   // exact residual
+    return __builtin_fmaf(e, r, q0) - 1.0f;
+}
 __device__ __forceinline__ float sigmoid_(float x) { return __builtin_amdgcn_rcpf(1.0f + fast_exp(-x)); }
 __device__ __forceinline__ float tanh_(float x) {
     const float e = fast_exp(-2.0f * fabsf(x));            // in (0, 1]: no overflow
