@@ -57,7 +57,10 @@ def _worker(rank, world, port, n_items, batched, q):
 
         out = sharding.generate_sharded(_RowsModel(), mels, batched, 0, 0, False, device=torch.device("cpu"),
                                         generate_fn=gen)
-        assert len(calls) <= 1
+        # the rank's launch carries exactly its contiguous block: the launch's row count (and so the
+        # loop kernel choose_path picks, sharding.py docstring) is a function of (n, rank, world)
+        block = sharding.shard_indices(n_items, rank, world)
+        assert calls == ([len(block)] if block else [])
         dm = sharding.generate_sharded_deepmind(None, n_items, 5, device=torch.device("cpu"),
                                                 generate_fn=lambda ii, r0: [np.arange(5) * 1000 - 32768 + i
                                                                             for i in ii])
