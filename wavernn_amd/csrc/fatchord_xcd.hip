@@ -93,6 +93,11 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
     const int t_terms = min(t_end, a.L - 1);
     unsigned long long *xg = a.xg + (size_t)k * kXXcdStride;
     auto XG = [&](int hop) { return xg + (size_t)hop * kXHopStride; };
+    // publishes through one wave-uniform buffer descriptor + a 32-bit granule index (the 64-bit
+    // per-lane pointers of each hop stayed live across the loop and were spilled: the F2 publish
+    // reloaded its address from scratch and waited vmcnt(0) on the critical path)
+    const __amdgpu_buffer_rsrc_t xgr = __builtin_amdgcn_make_buffer_rsrc(xg, 0, 0x7fffffff, 0x00020000);
+    auto XGI = [&](int hop) { return hop * (int)kXHopStride; };
     auto RING = [&](int t) { return ring + (t & (kXRing - 1)) * kXTerms; };
     auto NZ = [&](int t) { return nzr + (t & (kXRing - 1)) * kXNoise; };
     auto TERMS = [&](int t) { return a.terms + ((size_t)(t - a.t0) * a.nb + k) * TW + (size_t)c * kXTerms; };
@@ -152,13 +157,13 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
     auto publish_term = [&](int t, int rr, float gh) {
         const int u = rr / 3, q = rr - 3 * u;
         const float p1 = RING(t)[XT_P1 + rr], bh = cst[XC_BHH1 + rr], bi = cst[XC_BIH1 + rr];
-        unsigned long long *g = XG(XH_S0 + (t & 1)) + (size_t)(c * kXUnits + u) * 4;
+        const int g = XGI(XH_S0 + (t & 1)) + (c * kXUnits + u) * 4;
         const uint32_t tag = (uint32_t)t + 1u;
         if (q < 2) {
-            xpub(g + q, tag, (gh + bh) + (p1 + bi));
+            xpub_b(xgr, g + q, tag, (gh + bh) + (p1 + bi));
         } else {
-            xpub(g + 3, tag, gh + bh);
-            xpub(g + 2, tag, p1 + bi);
+            xpub_b(xgr, g + 3, tag, gh + bh);
+            xpub_b(xgr, g + 2, tag, p1 + bi);
         }
     };
     // the GRU1 terms of this wave's W_hh1 rows (gh[p]: row gh0 + 2p + e), lanes li < 5
@@ -288,13 +293,16 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
         {
             f4v hx[4];
             e32x(h1s, li, hx);
-            const float h1j = h1s[c * kXUnits + ui];
+            // x_I + h1 of the engine's unit (:212) formed before the dots and pinned there: hipcc
+            // otherwise sinks the h1 LDS read into the publishing lane's branch after the gate math
+            float yb = xi + h1s[c * kXUnits + ui];
+            asm volatile("" : "+v"(yb));
             const float g_r = e32dot(wih2[0], hx), g_z = e32dot(wih2[1], hx), g_n = e32dot(wih2[2], hx);
             const float hn = gru_gate_math(g_r + p2q[0], g_z + p2q[1], g_n + p2q[2], ghv[0], ghv[1], ghv[2], h2own);
             h2own = hn;
             // y = (x_I + h1) + h2 (:212, :216)
-            const float y = (xi + h1j) + hn;
-            if (li == 0) xpub(XG(XH_Y) + c * kXUnits + ui, tag, y);   // h2: after hop Y (pub_h2)
+            const float y = yb + hn;
+            if (li == 0) xpub_b(xgr, XGI(XH_Y) + c * kXUnits + ui, tag, y);   // h2: after hop Y (pub_h2)
         }
         XSTAMP(2);
         // Off-critical memory traffic (GRU1-term and h2 publishes, the S / h2 gathers, the ring)
@@ -305,7 +313,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
         //   after f1 gathered : gather h2 (wave 6), S (waves 1, 2, 5, 6), the ring (wave 7)
         //   after h2 gathered : W_hh2·h2 (waves 0, 1, 2, 5, 6, 7)
         auto pub_h2 = [&]() {
-            if (li == 0) xpub(XG(XH_H2) + c * kXUnits + ui, tag, h2own);
+            if (li == 0) xpub_b(xgr, XGI(XH_H2) + c * kXUnits + ui, tag, h2own);
         };
         // fc waves: lane l ends fc8_rows with row 8h + j + 2·(l >> 4) in o[j]; lanes with
         // (l & 15) < 2 publish row 8h + (l & 1) + 2·(l >> 4)
@@ -395,7 +403,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
             float o[2];
             fc8_rows(wr, yk, o);
             const float A = (jq == 0 ? o[0] : o[1]) + v1;
-            if ((lane & 15) < 2) xpub(XG(XH_F1) + c * kXFcRows + rg, tag, A > 0.0f ? A : 0.0f);
+            if ((lane & 15) < 2) xpub_b(xgr, XGI(XH_F1) + c * kXFcRows + rg, tag, A > 0.0f ? A : 0.0f);
             XSTAMPW(4, 1);
             if (more && !WRNN_XCD_SKIP_RECUR) {   // h2 out; after f1 gathered: a quarter of the next S; W_hh2 LDS rows 28 + 10h + 2p + e
                 pub_h2();
@@ -467,7 +475,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
                         break;
                 }
                 asm volatile("" ::: "memory");
-                if (lane < kXF2Line) xpub(XG(XH_F2) + c * kXF2Line + lane, tag, p + f2x[lane]);   // 30, 31: zero weights
+                if (lane < kXF2Line) xpub_b(xgr, XGI(XH_F2) + c * kXF2Line + lane, tag, p + f2x[lane]);   // 30, 31: zero weights
                 XSTAMPW(6, 3);
             }
         } else if (more) {

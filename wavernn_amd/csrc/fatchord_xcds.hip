@@ -394,7 +394,10 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
         XSTAMP(1);
         // ---- GRU2 (:212-214): engine q of wave ub → gate q of units 4ub..4ub+3 (W_ih2[:, :R]·h1)
         if (wave < kSUB) {
-            const float h1j = h1s[c * kSU + ul];   // (read before the dots: its latency off the chain)
+            // x_I + h1 of unit 4ub + (lane & 3) (:212) before the dots, pinned there (hipcc sinks the
+            // h1 LDS read into the publishing lanes' branch after the gate math otherwise)
+            float yb = xi + h1s[c * kSU + ul];
+            asm volatile("" : "+v"(yb));
             float g[4];
             sp_block_row(*reinterpret_cast<const f4v(*)[4]>(&wg[0]), *reinterpret_cast<const f4v(*)[4]>(&wg[4]), ja, jb,
                          h1s, g);
@@ -422,7 +425,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
                 XSTAMP(14);
             }
             // y = (x_I + h1) + h2 (:212, :216)
-            const float y = (xi + h1j) + hn;
+            const float y = yb + hn;
             if (lane < 4) xpub_b(xgr, XGI(XH_Y) + c * kSU + ul, tag, y);
         }
         XSTAMP(2);
