@@ -352,7 +352,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
                 bool ok = true;
 #pragma unroll
                 for (int m = 0; m < 8; ++m) ok &= (v[m].y == tag) & (v[m].w == tag);
-                if (ok) {
+                if (__ballot(!ok) == 0) {   // wave-uniform exit: no exec-mask branches, no copies
 #pragma unroll
                     for (int m = 0; m < 8; ++m) {
                         pa[m] = __uint_as_float(v[m].x);

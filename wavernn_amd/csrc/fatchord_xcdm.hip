@@ -105,7 +105,7 @@ __device__ __forceinline__ void mpoll(const float *vec, int w, int *ctl, long lo
         bool ok = true;
 #pragma unroll
         for (int i = 0; i < kMPP * NQ; ++i) ok &= pfull(v[i]);
-        if (ok) return;
+        if (__ballot(!ok) == 0) return;   // wave-uniform exit
         if ((++spins & 63u) == 0) {
             const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - c0) > timeout;
             const bool other = __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
@@ -406,7 +406,7 @@ __device__ __forceinline__ float msample(const unsigned long long *f2, int n, ui
         bool ok = true;
 #pragma unroll
         for (int m = 0; m < 8; ++m) ok &= (v[m].y == tag) & (v[m].w == tag);
-        if (ok) {
+        if (__ballot(!ok) == 0) {   // wave-uniform exit
 #pragma unroll
             for (int m = 0; m < 8; ++m) {
                 pa[m] = __uint_as_float(v[m].x);

@@ -502,7 +502,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
                     bool ok = true;
 #pragma unroll
                     for (int m = 0; m < 8; ++m) ok &= (vv[m].y == tag) & (vv[m].w == tag);
-                    if (ok) {
+                    if (__ballot(!ok) == 0) {   // wave-uniform exit
 #pragma unroll
                         for (int m = 0; m < 8; ++m) {
                             pa[m] = __uint_as_float(vv[m].x);

@@ -143,7 +143,7 @@ __device__ __forceinline__ void xgather(const unsigned long long *g, uint32_t ta
         bool ok = true;
 #pragma unroll
         for (int k = 0; k < NG; ++k) ok &= (uint32_t)(v[k] >> 32) == tag;
-        if (ok) {
+        if (__ballot(!ok) == 0) {   // wave-uniform exit (a per-lane exit builds exec-mask branches)
 #pragma unroll
             for (int k = 0; k < NG; ++k) store(lid + 64 * k, __uint_as_float((uint32_t)v[k]));
             return;
@@ -187,7 +187,7 @@ __device__ __forceinline__ void xgather16(const unsigned long long *g, uint32_t 
         bool ok = true;
 #pragma unroll
         for (int k = 0; k < NP; ++k) ok &= (v[k].y == tag) & (v[k].w == tag);
-        if (ok) {
+        if (__ballot(!ok) == 0) {
 #pragma unroll
             for (int k = 0; k < NP; ++k) store2(2 * (lid + 64 * k), __uint_as_float(v[k].x), __uint_as_float(v[k].z));
             return;
@@ -218,7 +218,7 @@ __device__ __forceinline__ void xpoll16(const unsigned long long *g, uint32_t ta
         bool ok = true;
 #pragma unroll
         for (int k = 0; k < NP; ++k) ok &= (v[k].y == tag) & (v[k].w == tag);
-        if (ok) return;
+        if (__ballot(!ok) == 0) return;
         if ((++spins & 63u) == 0) {
             const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - t0) > timeout;
             const bool other = __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
