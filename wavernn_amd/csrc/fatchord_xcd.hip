@@ -232,6 +232,10 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
     float *st = a.state + ((size_t)k * kXcdWgs + c) * kXStateW;
     float h1v = resume ? st[tid] : 0.0f;              // h1 of unit tid (recurrent, this thread)
     float h2own = resume ? st[512 + 2048 + 48 + ui] : 0.0f;   // h2 of this engine's unit
+    // consume the carried-state loads here (an empty asm use: the wait lands before the loop);
+    // left pending into the loop, their first use inside it is an s_waitcnt vmcnt(0) in EVERY
+    // step (GRU1's h1 update), draining all the wave's in-flight publishes and loads there
+    asm volatile("" : "+v"(h1v), "+v"(h2own));
     if (resume) {
         for (int i = tid; i < 4 * R; i += kXThreads) sg[i] = st[512 + i];
         if (tid < 48) gh2s[tid] = st[512 + 2048 + tid];
