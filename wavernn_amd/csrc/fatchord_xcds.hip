@@ -38,6 +38,9 @@ namespace wrnn {
 #ifndef WRNN_XCDS_DIAG
 #define WRNN_XCDS_DIAG 0   // timing diagnostics (wrong results): 1 skip the S gathers, 2 skip the h2 gather
 #endif
+#ifndef WRNN_XCDS_RS
+#define WRNN_XCDS_RS 1   // block-row sums reduce-scattered over the engine (0: four row sums + select, A/B)
+#endif
 #ifndef WRNN_XCDS_GRU2_STAMPS
 #define WRNN_XCDS_GRU2_STAMPS 0   // diagnostics: stamps 12..14 inside GRU2 (wave 0) instead of the ring / GH2 ones
 #endif
@@ -103,29 +106,50 @@ __device__ __forceinline__ float fc4_rows_k(const f2v *w, const f2v (&xk)[NK]) {
     return row_sum16(__uint_as_float(q[0]) + __uint_as_float(q[1]));
 }
 
-// One gate block-row on a 16-lane engine: Σ over its nonzero 4×4 blocks of W_blk · v[4j..4j+3];
-// this lane holds blocks wa (column block ja) and wb (jb), rows as float4.  The 4 row sums end
-// in g[0..3], identical in all 16 lanes of the engine.
-__device__ __forceinline__ void sp_block_row(const f4v (&wa)[4], const f4v (&wb)[4], int ja, int jb,
-                                             const float *v, float (&g)[4]) {
-    const f4v xa = lds4(v + 4 * ja), xb = lds4(v + 4 * jb);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        f2v acc = __builtin_elementwise_fma(wa[r].xy, xa.xy, f2v{0.0f, 0.0f});
-        f2v acc2 = __builtin_elementwise_fma(wa[r].zw, xa.zw, f2v{0.0f, 0.0f});
-        acc = __builtin_elementwise_fma(wb[r].xy, xb.xy, acc);
-        acc2 = __builtin_elementwise_fma(wb[r].zw, xb.zw, acc2);
-        const f2v t = acc + acc2;
-        g[r] = row_sum16(t.x + t.y);
-    }
-}
-
 // g[i] for a per-lane i in 0..3 as three v_cndmask (the nested ?: form compiled into exec-mask
 // branches: ≈ 30 scalar / branch instructions per call in the GRU2 epilogue)
 __device__ __forceinline__ float sel4(const float (&g)[4], int i) {
     const float a = (i & 1) ? g[1] : g[0];
     const float b = (i & 1) ? g[3] : g[2];
     return (i & 2) ? b : a;
+}
+
+// One gate block-row on a 16-lane engine: Σ over its nonzero 4×4 blocks of W_blk · v[4j..4j+3];
+// this lane holds blocks wa (column block ja) and wb (jb), rows as float4.  Returns, in lane l,
+// the full sum of row l & 3 (every consumer takes that row: the GRU2 epilogue, the term and
+// W_hh2·h2 stores of lanes li < 4).
+__device__ __forceinline__ float sp_block_row(const f4v (&wa)[4], const f4v (&wb)[4], int ja, int jb,
+                                              const float *v, int lane) {
+    const f4v xa = lds4(v + 4 * ja), xb = lds4(v + 4 * jb);
+    float t[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        f2v acc = __builtin_elementwise_fma(wa[r].xy, xa.xy, f2v{0.0f, 0.0f});
+        f2v acc2 = __builtin_elementwise_fma(wa[r].zw, xa.zw, f2v{0.0f, 0.0f});
+        acc = __builtin_elementwise_fma(wb[r].xy, xb.xy, acc);
+        acc2 = __builtin_elementwise_fma(wb[r].zw, xb.zw, acc2);
+        const f2v tt = acc + acc2;
+        t[r] = tt.x + tt.y;
+    }
+#if WRNN_XCDS_RS
+    // reduce-scatter over the engine's 16 lanes: lane l keeps rows of its parity (l & 1) against
+    // lane l ^ 1, then row l & 3 against l ^ 2, then sums the four lanes of its residue class
+    // (row_ror 4, 8): 5 DPP adds and 6 selects on a 4-deep chain instead of four 4-deep row sums
+    const bool odd = (lane & 1) != 0, hi = (lane & 2) != 0;
+    const float u0 = odd ? t[1] : t[0], v0 = odd ? t[0] : t[1];
+    const float u1 = odd ? t[3] : t[2], v1 = odd ? t[2] : t[3];
+    const float a0 = u0 + WRNN_DPP(v0, 0xB1), a1 = u1 + WRNN_DPP(v1, 0xB1);   // quad_perm [1,0,3,2]
+    const float keep = hi ? a1 : a0, send = hi ? a0 : a1;
+    float b = keep + WRNN_DPP(send, 0x4E);                                     // quad_perm [2,3,0,1]
+    b += WRNN_DPP(b, 0x124);                                                   // row_ror:4
+    b += WRNN_DPP(b, 0x128);                                                   // row_ror:8
+    return b;
+#else
+    float g[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) g[r] = row_sum16(t[r]);
+    return sel4(g, lane & 3);
+#endif
 }
 
 #define XSTAMPW(kk, w)                                                                                        \
@@ -247,7 +271,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
         }
     };
     // a gate block-row of W_hh1 / W_hh2 from LDS (block-row br of this engine)
-    auto lds_block_row = [&](const float *wb, const int *wc, int br, const float *v, float (&g)[4]) {
+    auto lds_block_row = [&](const float *wb, const int *wc, int br, const float *v) -> float {
         const float *p = wb + ((size_t)br * kSNB + li) * 16;
         f4v wa4[4], wb4[4];
 #pragma unroll
@@ -255,28 +279,27 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
             wa4[i] = lds4(p + 4 * i);
             wb4[i] = lds4(p + 16 * 16 + 4 * i);
         }
-        sp_block_row(wa4, wb4, wc[br * kSNB + li], wc[br * kSNB + li + 16], v, g);
+        return sp_block_row(wa4, wb4, wc[br * kSNB + li], wc[br * kSNB + li + 16], v, lane);
     };
     // The 21 gate block-rows of W_hh1 / W_hh2 on a wave quad's 16 engines: pass 0 block-row 4·(w & 3) + e,
     // pass 1 block-rows 16..20 on the first wave of the quad (engines 0..3) and the second (engine 0).
     // W_hh1·h1 → GRU1 terms of step t+1 on waves 0..3, W_hh2·h2 → gh2s on waves 4..7.
     const int wq = wave & 3;
     const int br0 = 4 * wq + eng, br1 = wq == 0 ? 16 + eng : (wq == 1 && eng == 0) ? 20 : -1;
-    auto gh_dots = [&](const float *wbk, const int *wck, const float *v, int br, float (&g)[4]) {
-        lds_block_row(wbk, wck, br >= 0 ? br : 0, v, g);
+    auto gh_dots = [&](const float *wbk, const int *wck, const float *v, int br) -> float {
+        return lds_block_row(wbk, wck, br >= 0 ? br : 0, v);
     };
-    auto publish_terms = [&](int t, int br, const float (&g)[4]) {
+    auto publish_terms = [&](int t, int br, float g) {   // g: row li & 3 of block-row br
         if (br >= 0 && li < 4) {
             const int q = br / kSUB, ub = br - q * kSUB;
-            publish_term(t, (4 * ub + li) * 3 + q, sel4(g, li));
+            publish_term(t, (4 * ub + li) * 3 + q, g);
         }
     };
     auto gh2_dots = [&](int br) {
-        float g[4];
-        gh_dots(whh2b, whh2c, h2s, br, g);
+        const float g = gh_dots(whh2b, whh2c, h2s, br);
         if (br >= 0 && li < 4) {
             const int q = br / kSUB, ub = br - q * kSUB;
-            gh2s[(4 * ub + li) * 3 + q] = sel4(g, li);
+            gh2s[(4 * ub + li) * 3 + q] = g;
         }
     };
     // a quarter of step t's GRU1 terms (waves 4..7: 896 granules each, one poll round)
@@ -341,10 +364,9 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
     }
     __syncthreads();
     if (!resume) {   // GRU1 terms of step 0 (GH1 = 0), published and gathered
-        const float z4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
         if (wave < 4) {
-            publish_terms(0, br0, z4);
-            publish_terms(0, br1, z4);
+            publish_terms(0, br0, 0.0f);
+            publish_terms(0, br1, 0.0f);
         }
         if (wave >= 4) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -398,18 +420,15 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
             // h1 LDS read into the publishing lanes' branch after the gate math otherwise)
             float yb = xi + h1s[c * kSU + ul];
             asm volatile("" : "+v"(yb));
-            float g[4];
-            sp_block_row(*reinterpret_cast<const f4v(*)[4]>(&wg[0]), *reinterpret_cast<const f4v(*)[4]>(&wg[4]), ja, jb,
-                         h1s, g);
+            const float gs = sp_block_row(*reinterpret_cast<const f4v(*)[4]>(&wg[0]),
+                                          *reinterpret_cast<const f4v(*)[4]>(&wg[4]), ja, jb, h1s, lane);
             if (WRNN_XCDS_GRU2_STAMPS) {
-                asm volatile("" ::"v"(g[0]), "v"(g[1]), "v"(g[2]), "v"(g[3]));
+                asm volatile("" ::"v"(gs));
                 XSTAMP(12);
             }
             // every lane keeps its row (lane & 3) of its engine's gate; engine 0 collects z (engine 1,
             // one permlane16 swap) and n (engine 2, one permlane32 swap) — lane l < 4 then holds
             // r, z, n of unit 4ub + l (two swaps instead of one per row and gate)
-            const int r4 = lane & 3;
-            const float gs = sel4(g, r4);
             const float gz = __uint_as_float(
                 __builtin_amdgcn_permlane16_swap(__float_as_uint(gs), __float_as_uint(gs), false, false)[1]);
             const float gn = __uint_as_float(
@@ -440,9 +459,8 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
             // of those rows (:223); waves 1..3 hand theirs to wave 0 (LDS, flags), wave 0 publishes
             // the workgroup's line (hop F2), polls all 32 lines and samples
             if (more) {
-                float g0[4], g1[4];
-                gh_dots(whh1b, whh1c, h1s, br0, g0);
-                if (wq < 2) gh_dots(whh1b, whh1c, h1s, br1, g1);
+                const float g0 = gh_dots(whh1b, whh1c, h1s, br0);
+                const float g1 = wq < 2 ? gh_dots(whh1b, whh1c, h1s, br1) : 0.0f;
                 wait_flag(ygot, tag);
                 publish_terms(t + 1, br0, g0);
                 if (wq < 2) publish_terms(t + 1, br1, g1);
