@@ -52,6 +52,9 @@ namespace wrnn {
 #define WRNN_XCD_SKIP_RECUR 0
 #endif
 #ifndef WRNN_XCD_PRIO
+#ifndef WRNN_XCD_RS
+#define WRNN_XCD_RS 1           // GRU2's three engine dots reduce-scattered (e32dot3_rs; 0: three e32dot, A/B)
+#endif
 #define WRNN_XCD_PRIO 0         // s_setprio of wave 0 (the poller / sampler)
 #endif
 
@@ -301,7 +304,14 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
             // otherwise sinks the h1 LDS read into the publishing lane's branch after the gate math
             float yb = xi + h1s[c * kXUnits + ui];
             asm volatile("" : "+v"(yb));
-            const float g_r = e32dot(wih2[0], hx), g_z = e32dot(wih2[1], hx), g_n = e32dot(wih2[2], hx);
+            float g_r, g_z, g_n;   // valid in lanes li == 0 (the publishing lane)
+            if (WRNN_XCD_RS) {
+                e32dot3_rs(wih2[0], wih2[1], wih2[2], hx, lane, g_r, g_z, g_n);
+            } else {
+                g_r = e32dot(wih2[0], hx);
+                g_z = e32dot(wih2[1], hx);
+                g_n = e32dot(wih2[2], hx);
+            }
             const float hn = gru_gate_math(g_r + p2q[0], g_z + p2q[1], g_n + p2q[2], ghv[0], ghv[1], ghv[2], h2own);
             h2own = hn;
             // y = (x_I + h1) + h2 (:212, :216)

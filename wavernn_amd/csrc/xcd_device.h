@@ -121,6 +121,41 @@ __device__ __forceinline__ float e32dot(const f4v (&w)[4], const f4v (&x)[4]) {
     return perm_sum16(row_sum16(s.x + s.y));
 }
 
+// The in-lane part of e32dot (no cross-lane sum)
+__device__ __forceinline__ float e32part(const f4v (&w)[4], const f4v (&x)[4]) {
+    f2v a = __builtin_elementwise_fma(w[0].xy, x[0].xy, f2v{0.0f, 0.0f});
+    f2v b = __builtin_elementwise_fma(w[1].xy, x[1].xy, f2v{0.0f, 0.0f});
+    a = __builtin_elementwise_fma(w[0].zw, x[0].zw, a);
+    b = __builtin_elementwise_fma(w[1].zw, x[1].zw, b);
+    a = __builtin_elementwise_fma(w[2].xy, x[2].xy, a);
+    b = __builtin_elementwise_fma(w[3].xy, x[3].xy, b);
+    a = __builtin_elementwise_fma(w[2].zw, x[2].zw, a);
+    b = __builtin_elementwise_fma(w[3].zw, x[3].zw, b);
+    const f2v s = a + b;
+    return s.x + s.y;
+}
+
+// Three e32dot rows of an engine (the r, z, n gate rows of its unit) reduce-scattered over its 32
+// lanes: lane l keeps row l & 3 (a zero fourth row) against l ^ 1, then l ^ 2, then sums the
+// lanes of its residue class (row_ror 4 and 8, the paired DPP row); lanes 1 and 2 hand z and n
+// to lane 0.  8 cross-lane operations on one chain instead of 3 × 5.  Valid in lanes li == 0.
+__device__ __forceinline__ void e32dot3_rs(const f4v (&w0)[4], const f4v (&w1)[4], const f4v (&w2)[4],
+                                           const f4v (&x)[4], int lane, float &gr, float &gz, float &gn) {
+    const float t0 = e32part(w0, x), t1 = e32part(w1, x), t2 = e32part(w2, x);
+    const bool odd = (lane & 1) != 0, hi = (lane & 2) != 0;
+    const float u0 = odd ? t1 : t0, v0 = odd ? t0 : t1;
+    const float u1 = odd ? 0.0f : t2, v1 = odd ? t2 : 0.0f;
+    const float a0 = u0 + WRNN_DPP(v0, 0xB1), a1 = u1 + WRNN_DPP(v1, 0xB1);   // quad_perm [1,0,3,2]
+    const float keep = hi ? a1 : a0, send = hi ? a0 : a1;
+    float b = keep + WRNN_DPP(send, 0x4E);                                     // quad_perm [2,3,0,1]
+    b += WRNN_DPP(b, 0x124);                                                   // row_ror:4
+    b += WRNN_DPP(b, 0x128);                                                   // row_ror:8
+    b = perm_sum16(b);
+    gr = b;
+    gz = WRNN_DPP(b, 0x55);   // quad_perm [1,1,1,1]
+    gn = WRNN_DPP(b, 0xAA);   // quad_perm [2,2,2,2]
+}
+
 __device__ __forceinline__ f4v lds4(const float *p) { return *reinterpret_cast<const f4v *>(p); }
 
 // x chunks of an engine lane (li = lane & 31) from a 512-float LDS vector
