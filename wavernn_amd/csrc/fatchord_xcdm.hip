@@ -563,7 +563,10 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         for (int j = 0; j < kMJ; ++j) A[s][j] = S[a.s.a + ((wave * kMSets + s) * kMJ + j) * 64 + lane];
 
     // roles: (unit / fc row u, batch row n) for the layer epilogues; (logit j, row n) for fc3
-    const bool gru = tid < 16 * NR;
+    // (16·NR = 64·NQ threads = waves 0..NQ-1: tested on the SGPR wave index, so the epilogue role
+    // branches are scalar instead of exec-mask branches)
+    static_assert(16 * NR == 64 * NQ, "epilogue threads are whole waves");
+    const bool gru = wave < NQ;
     // the off-critical recurrent sums (Σ W_hh·h of the next step; 16 partials each in the 4x4x1
     // form) are taken by the waves that do not sample, while the samplers run J: waves ≥ aux_w0
     // (none when every wave samples: then the epilogue threads take them in F and I)
