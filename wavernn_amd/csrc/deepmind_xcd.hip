@@ -519,27 +519,28 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         // ---- sample c_t (:129-131): wave n samples row n
         auto sample_row = [&](int hop, int half) -> int {
             const __amdgpu_buffer_rsrc_t rl = hop_rsrc(xg + kDxHopOff[hop]);
-            f4v lv = {0.0f, 0.0f, 0.0f, 0.0f};
             const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
             unsigned spins = 0;
+            bool dead = false;
+            u4v v0, v1;   // polled in place: the exit path is one uniform branch, no copies
             for (;;) {
-                const u4v v0 = ld16_sc1(rl, (wave * kDxQ + (WRNN_DX_ORDERED_ARGMAX ? 4 * lane : 2 * lane)) * 8);
-                const u4v v1 = ld16_sc1(rl, (wave * kDxQ + (WRNN_DX_ORDERED_ARGMAX ? 4 * lane + 2 : 2 * lane + 128)) * 8);
+                v0 = ld16_sc1(rl, (wave * kDxQ + (WRNN_DX_ORDERED_ARGMAX ? 4 * lane : 2 * lane)) * 8);
+                v1 = ld16_sc1(rl, (wave * kDxQ + (WRNN_DX_ORDERED_ARGMAX ? 4 * lane + 2 : 2 * lane + 128)) * 8);
                 const bool ok = (v0.y == tag) & (v0.w == tag) & (v1.y == tag) & (v1.w == tag);
-                if (__ballot(!ok) == 0) {
-                    lv = f4v{__uint_as_float(v0.x), __uint_as_float(v0.z), __uint_as_float(v1.x), __uint_as_float(v1.z)};
-                    break;
-                }
+                if (__ballot(!ok) == 0) break;
                 if ((++spins & 63u) == 0) {
                     const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - c0) > a.timeout_ticks;
                     const bool other = __hip_atomic_load(&a.ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
                     if (late || other) {
                         if (late) record_abort(a.ctl, -4, t, hop, blockIdx.x);
                         *abort_flag = 1;
-                        return 0;
+                        dead = true;
+                        break;
                     }
                 }
             }
+            if (dead) return 0;
+            const f4v lv = {__uint_as_float(v0.x), __uint_as_float(v0.z), __uint_as_float(v1.x), __uint_as_float(v1.z)};
             // argmax_c l_c − log q_c ≡ argmax_c p_c / q_c (softmax, Categorical renormalisation and
             // the draw's scale cancel): lane l holds classes 4l .. 4l + 3, so the winner is the first
             // lane holding the wave's max (wave_argmax_ordered: no index through the DPP stages)
