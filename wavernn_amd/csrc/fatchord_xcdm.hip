@@ -398,33 +398,29 @@ __device__ __forceinline__ float msample(const unsigned long long *f2, int n, ui
     const int goff = ((n * kXcdWgs + 8 * pg) * 32 + 2 * jp) * 8;
     const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
     unsigned spins = 0;
-    float pa[8], pb[8];
-    for (;;) {
-        u4v v[8];
+    u4v v[8];
+    for (;;) {   // one wave-uniform exit; the values taken after the loop
 #pragma unroll
         for (int m = 0; m < 8; ++m) v[m] = ld16_sc1(rf, goff + m * 32 * 8);
         bool ok = true;
 #pragma unroll
         for (int m = 0; m < 8; ++m) ok &= (v[m].y == tag) & (v[m].w == tag);
-        if (__ballot(!ok) == 0) {   // wave-uniform exit
-#pragma unroll
-            for (int m = 0; m < 8; ++m) {
-                pa[m] = __uint_as_float(v[m].x);
-                pb[m] = __uint_as_float(v[m].z);
-            }
-            break;
-        }
+        if (__ballot(!ok) == 0) break;
         if ((++spins & 63u) == 0) {
             const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - c0) > timeout;
             const bool other = __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
             if (late || other) {
                 if (late) record_abort(ctl, -4, step, MH_F2, blockIdx.x);
                 *lds_abort = 1;
-#pragma unroll
-                for (int m = 0; m < 8; ++m) pa[m] = pb[m] = 0.0f;
                 break;
             }
         }
+    }
+    float pa[8], pb[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        pa[m] = __uint_as_float(v[m].x);
+        pb[m] = __uint_as_float(v[m].z);
     }
 #pragma unroll
     for (int w = 4; w >= 1; w /= 2)
@@ -449,31 +445,32 @@ __device__ __forceinline__ int rsample(const unsigned long long *lg, int n, uint
     const int goff = (n * kMRawNC + 2 * lane) * 8;
     const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
     unsigned spins = 0;
-    float e[8];
-    for (;;) {
-        u4v v[4];
+    u4v v[4];
+    bool dead = false;
+    for (;;) {   // one wave-uniform exit; the values taken after the loop
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = ld16_sc1(rf, goff + i * 128 * 8);
         bool ok = true;
 #pragma unroll
         for (int i = 0; i < 4; ++i) ok &= (v[i].y == tag) & (v[i].w == tag);
-        if (__ballot(!ok) == 0) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                e[2 * i] = __uint_as_float(v[i].x);
-                e[2 * i + 1] = __uint_as_float(v[i].z);
-            }
-            break;
-        }
+        if (__ballot(!ok) == 0) break;
         if ((++spins & 63u) == 0) {
             const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - c0) > timeout;
             const bool other = __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
             if (late || other) {
                 if (late) record_abort(ctl, -4, step, MH_LG, blockIdx.x);
                 *lds_abort = 1;
-                return 0;
+                dead = true;
+                break;
             }
         }
+    }
+    if (dead) return 0;
+    float e[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        e[2 * i] = __uint_as_float(v[i].x);
+        e[2 * i + 1] = __uint_as_float(v[i].z);
     }
     float m = -INFINITY;
 #pragma unroll

@@ -512,33 +512,29 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
                 const int goff = pg * 8 * kXF2Line * 8 + jp * 16;
                 const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
                 unsigned spins = 0;
-                float pa[8], pb[8];
-                for (;;) {
-                    u4v *vv = reinterpret_cast<u4v *>(&wr[16]);   // wave 0's fc2 weights are wr[0..15]
+                u4v *vv = reinterpret_cast<u4v *>(&wr[16]);   // wave 0's fc2 weights are wr[0..15]
+                for (;;) {   // one wave-uniform exit; the values taken after the loop
 #pragma unroll
                     for (int m = 0; m < 8; ++m) vv[m] = ld16_sc1(rf, goff + m * kXF2Line * 8);
                     bool ok = true;
 #pragma unroll
                     for (int m = 0; m < 8; ++m) ok &= (vv[m].y == tag) & (vv[m].w == tag);
-                    if (__ballot(!ok) == 0) {   // wave-uniform exit
-#pragma unroll
-                        for (int m = 0; m < 8; ++m) {
-                            pa[m] = __uint_as_float(vv[m].x);
-                            pb[m] = __uint_as_float(vv[m].z);
-                        }
-                        break;
-                    }
+                    if (__ballot(!ok) == 0) break;
                     if ((++spins & 63u) == 0) {
                         const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - c0) > a.timeout_ticks;
                         const bool other = __hip_atomic_load(&a.ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
                         if (late || other) {
                             if (late) record_abort(a.ctl, -4, t, XH_F2, blockIdx.x);
                             *abort_flag = 1;
-#pragma unroll
-                            for (int m = 0; m < 8; ++m) pa[m] = pb[m] = 0.0f;
                             break;
                         }
                     }
+                }
+                float pa[8], pb[8];
+#pragma unroll
+                for (int m = 0; m < 8; ++m) {
+                    pa[m] = __uint_as_float(vv[m].x);
+                    pb[m] = __uint_as_float(vv[m].z);
                 }
                 XSTAMP(7);
 #pragma unroll
