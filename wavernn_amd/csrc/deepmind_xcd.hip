@@ -284,23 +284,31 @@ __device__ __forceinline__ float dx_rsum(const float *PR, const float *PRQ, int 
 }
 
 // Σ of an O1 / O3 output (row r < 16, n) and of an O2 / O4 output (row r < 8, n)
+// (all partial loads issued before the first add — a scheduling barrier between them: hipcc
+// otherwise interleaves reads and adds two loads at a time, one LDS round trip per pair)
 __device__ __forceinline__ float dx_o13sum(const float *P, int r, int n) {
+    f4v u[kDxWaves];
+#pragma unroll
+    for (int w = 0; w < kDxWaves; ++w) u[w] = lds4(P + (w * 16 + r) * 20 + 4 * n);
+    __builtin_amdgcn_sched_barrier(0);
     float t[kDxWaves];
 #pragma unroll
-    for (int w = 0; w < kDxWaves; ++w) {
-        const f4v u = lds4(P + (w * 16 + r) * 20 + 4 * n);
-        t[w] = (u.x + u.y) + (u.z + u.w);
-    }
+    for (int w = 0; w < kDxWaves; ++w) t[w] = (u[w].x + u[w].y) + (u[w].z + u[w].w);
     return (t[0] + t[1]) + (t[2] + t[3]);
 }
 __device__ __forceinline__ float dx_o24sum(const float *P, int r, int n) {
-    float t[kDxWaves];
+    f4v u0[kDxWaves], u1[kDxWaves];
 #pragma unroll
     for (int w = 0; w < kDxWaves; ++w) {
         const float *p = P + ((w * 8 + r) * 4 + n) * 8;
-        const f4v u0 = lds4(p), u1 = lds4(p + 4);
-        t[w] = ((u0.x + u0.y) + (u0.z + u0.w)) + ((u1.x + u1.y) + (u1.z + u1.w));
+        u0[w] = lds4(p);
+        u1[w] = lds4(p + 4);
     }
+    __builtin_amdgcn_sched_barrier(0);
+    float t[kDxWaves];
+#pragma unroll
+    for (int w = 0; w < kDxWaves; ++w)
+        t[w] = ((u0[w].x + u0[w].y) + (u0[w].z + u0[w].w)) + ((u1[w].x + u1[w].y) + (u1[w].z + u1[w].w));
     return (t[0] + t[1]) + (t[2] + t[3]);
 }
 
@@ -475,12 +483,15 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             }
         }
         DST(2);
+        // epilogue biases read before the layer (pinned: off the post-barrier LDS chain)
+        float bo1 = cst[DC_B1 + tid % kDxU], bo2 = cst[DC_B2 + tid % kDxUO2];
+        asm volatile("" : "+v"(bo1), "+v"(bo2));
         dx_o13<true>(AO1, stg_of(2), po1, lane, wave);
         bar();
         DST(3);
         if (tid < 4 * kDxU) {
             const int r = tid % kDxU, n = tid / kDxU;
-            const float o = dx_o13sum(po1, r, n) + cst[DC_B1 + r];
+            const float o = dx_o13sum(po1, r, n) + bo1;
             xpub(xg + kDxHopOff[DX_O1] + n * kDxS + kDxU * c + r, tag, o > 0.0f ? o : 0.0f);
         } else if (more && lt >= 0) {   // log q of step t + 1 → ring slot (t + 1) & 1
             float *slot = nzr + ((t + 1) & 1) * 4 * 2 * kDxQ;
@@ -511,7 +522,7 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         DST(7);
         if (tid < 4 * kDxUO2) {
             const int r = tid % kDxUO2, n = tid / kDxUO2;
-            xpub(xg + kDxHopOff[DX_LC] + n * kDxQ + kDxUO2 * c + r, tag, dx_o24sum(po2, r, n) + cst[DC_B2 + r]);
+            xpub(xg + kDxHopOff[DX_LC] + n * kDxQ + kDxUO2 * c + r, tag, dx_o24sum(po2, r, n) + bo2);
         } else if (tid >= 64 && t > a.t0) {
             r_sums(tid - 64, kDxThreads - 64, 48, 84);   // group B of R·h_{t-1} (partials from this step's start)
         }
@@ -594,12 +605,14 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             dx_stage(stg_of(0), lane, v);
         }
         DST(11);
+        float bo3 = cst[DC_B3 + tid % kDxU], bo4 = cst[DC_B4 + tid % kDxUO2];
+        asm volatile("" : "+v"(bo3), "+v"(bo4));
         dx_o13<false>(AO3, stg_of(0), po3, lane, wave);
         bar();
         DST(12);
         if (tid < 4 * kDxU) {
             const int r = tid % kDxU, n = tid / kDxU;
-            const float o = dx_o13sum(po3, r, n) + cst[DC_B3 + r];
+            const float o = dx_o13sum(po3, r, n) + bo3;
             xpub(xg + kDxHopOff[DX_O3] + n * kDxS + kDxU * c + r, tag, o > 0.0f ? o : 0.0f);
         }
         DST(13);
@@ -620,7 +633,7 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         DST(16);
         if (tid < 4 * kDxUO2) {
             const int r = tid % kDxUO2, n = tid / kDxUO2;
-            xpub(xg + kDxHopOff[DX_LF] + n * kDxQ + kDxUO2 * c + r, tag, dx_o24sum(po4, r, n) + cst[DC_B4 + r]);
+            xpub(xg + kDxHopOff[DX_LF] + n * kDxQ + kDxUO2 * c + r, tag, dx_o24sum(po4, r, n) + bo4);
         } else if (tid >= 64) {
             r_sums(tid - 64, kDxThreads - 64, 0, 48);   // group A of R·h_t (complete since the barrier)
         }
