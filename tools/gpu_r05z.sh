@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5 A/B: deepmind O1-O4 epilogues: all partial loads before the sums, biases read before the layers (in-tree) vs HEAD.
+# Round 5 A/B: deepmind gates: all LDS operands issued at once, carried h consumed before the loop; sampler log q read before the poll (in-tree) vs HEAD.
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"; export TMPDIR=/tmp; mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests/test_gpu_dx.py tests/test_gpu_deepmind.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r05z_pytest.log 2>&1
 rc=$?; tail -3 gpurun_out/r05z_pytest.log; [ $rc -eq 0 ] || exit $rc

@@ -402,6 +402,9 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         hc = st[gn * 2 * kDxU + gu];
         hf = st[gn * 2 * kDxU + kDxU + gu];
     }
+    // consume the carried-state loads here: left pending into the loop, the gates' first use of
+    // hc waits on vmcnt inside every step (behind the wave's in-flight publishes)
+    asm volatile("" : "+v"(hc), "+v"(hf));
     for (int i = tid; i < RX * 2 * kDxQ / 4; i += kDxThreads) {
         const int n = i / (2 * kDxQ / 4), f = i - n * (2 * kDxQ / 4);
         *reinterpret_cast<f4v *>(nzr + ((a.t0 & 1) * 4 + n) * 2 * kDxQ + 4 * f) =
@@ -437,17 +440,26 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
                 (unsigned)__builtin_amdgcn_s_memrealtime();
         // ---- coarse gates (:106-125): R·h_{t-1} (partials of the previous step), I_coarse(prev)
         if (gate) {
-            const float x0 = label_x(lab[gn]), x1 = label_x(lab[4 + gn]);
-            float I[3], Rg[3];
+            // every LDS operand of the gate chain issued at once (one round trip: hipcc otherwise
+            // waits on the labels before issuing the weight / sum / bias reads)
+            const float l0 = lab[gn], l1 = lab[4 + gn];
+            float w0[3], w1[3], Rg[3];
 #pragma unroll
-            for (int g = 0; g < 3; ++g) {   // separately rounded products (:111)
+            for (int g = 0; g < 3; ++g) {
                 const float *wi = cst + DC_IC + (g * kDxU + gu) * 2;
-                I[g] = __fadd_rn(__fmul_rn(wi[0], x0), __fmul_rn(wi[1], x1));
+                w0[g] = wi[0];
+                w1[g] = wi[1];
                 Rg[g] = rs[(g * kDxU + gu) * 4 + gn];
             }
-            const float uu = sigmoid_((Rg[0] + I[0]) + cst[DC_BU + gu]);
-            const float rr = sigmoid_((Rg[1] + I[1]) + cst[DC_BR + gu]);
-            const float ee = tanh_((rr * Rg[2] + I[2]) + cst[DC_BE + gu]);
+            const float bu = cst[DC_BU + gu], br = cst[DC_BR + gu], be = cst[DC_BE + gu];
+            __builtin_amdgcn_sched_barrier(0);
+            const float x0 = label_x(l0), x1 = label_x(l1);
+            float I[3];
+#pragma unroll
+            for (int g = 0; g < 3; ++g) I[g] = __fadd_rn(__fmul_rn(w0[g], x0), __fmul_rn(w1[g], x1));   // separately rounded products (:111)
+            const float uu = sigmoid_((Rg[0] + I[0]) + bu);
+            const float rr = sigmoid_((Rg[1] + I[1]) + br);
+            const float ee = tanh_((rr * Rg[2] + I[2]) + be);
             hc = uu * hc + (1.0f - uu) * ee;
             xpub(xg + kDxHopOff[DX_HC] + gn * kDxS + kDxU * c + gu, tag, hc);
             DST(19);
@@ -530,6 +542,11 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         // ---- sample c_t (:129-131): wave n samples row n
         auto sample_row = [&](int hop, int half) -> int {
             const __amdgpu_buffer_rsrc_t rl = hop_rsrc(xg + kDxHopOff[hop]);
+            // log q of this row's draws (written a step ahead) read before the logits poll: its
+            // LDS round trip off the chain that follows the poll
+            const float *lq = nzr + ((t & 1) * 4 + wave) * 2 * kDxQ + half * kDxQ;
+            f4v q = lds4(lq + 4 * lane);
+            asm volatile("" : "+v"(q));
             const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
             unsigned spins = 0;
             bool dead = false;
@@ -555,9 +572,7 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             // argmax_c l_c − log q_c ≡ argmax_c p_c / q_c (softmax, Categorical renormalisation and
             // the draw's scale cancel): lane l holds classes 4l .. 4l + 3, so the winner is the first
             // lane holding the wave's max (wave_argmax_ordered: no index through the DPP stages)
-            const float *lq = nzr + ((t & 1) * 4 + wave) * 2 * kDxQ + half * kDxQ;
             if constexpr (WRNN_DX_ORDERED_ARGMAX) {
-                const f4v q = lds4(lq + 4 * lane);
                 float bv = lv.x - q.x;
                 int bi = 4 * lane;
                 am_merge(bv, bi, lv.y - q.y, 4 * lane + 1);
@@ -582,18 +597,26 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         DST(9);
         // ---- fine gates (:135-145): I_fine(prev, c_t)
         if (gate) {
-            const float x0 = label_x(lab[gn]), x1 = label_x(lab[4 + gn]);
-            const float x2 = label_x(lab[8 + gn]);
-            float I[3], Rg[3];
+            const float l0 = lab[gn], l1 = lab[4 + gn], l2 = lab[8 + gn];   // (all reads at once, as above)
+            float w0[3], w1[3], w2[3], Rg[3];
 #pragma unroll
-            for (int g = 0; g < 3; ++g) {   // (:137)
+            for (int g = 0; g < 3; ++g) {
                 const float *wi = cst + DC_IF + (g * kDxU + gu) * 3;
-                I[g] = __fadd_rn(__fadd_rn(__fmul_rn(wi[0], x0), __fmul_rn(wi[1], x1)), __fmul_rn(wi[2], x2));
+                w0[g] = wi[0];
+                w1[g] = wi[1];
+                w2[g] = wi[2];
                 Rg[g] = rs[((3 + g) * kDxU + gu) * 4 + gn];
             }
-            const float uu = sigmoid_((Rg[0] + I[0]) + cst[DC_BU + kDxU + gu]);
-            const float rr = sigmoid_((Rg[1] + I[1]) + cst[DC_BR + kDxU + gu]);
-            const float ee = tanh_((rr * Rg[2] + I[2]) + cst[DC_BE + kDxU + gu]);
+            const float bu = cst[DC_BU + kDxU + gu], br = cst[DC_BR + kDxU + gu], be = cst[DC_BE + kDxU + gu];
+            __builtin_amdgcn_sched_barrier(0);
+            const float x0 = label_x(l0), x1 = label_x(l1), x2 = label_x(l2);
+            float I[3];
+#pragma unroll
+            for (int g = 0; g < 3; ++g)   // (:137)
+                I[g] = __fadd_rn(__fadd_rn(__fmul_rn(w0[g], x0), __fmul_rn(w1[g], x1)), __fmul_rn(w2[g], x2));
+            const float uu = sigmoid_((Rg[0] + I[0]) + bu);
+            const float rr = sigmoid_((Rg[1] + I[1]) + br);
+            const float ee = tanh_((rr * Rg[2] + I[2]) + be);
             hf = uu * hf + (1.0f - uu) * ee;
             xpub(xg + kDxHopOff[DX_HF] + gn * kDxS + kDxU * c + gu, tag, hf);
         }
