@@ -50,6 +50,9 @@ namespace wrnn {
 // fc3 partials wave-local (no barrier) from this many quads per XCD on: at B = 115 (4 quads)
 // 12.97 → 12.87 µs/step; at 1 quad (B ≤ 32) the barrier form is faster (5.29 vs 5.35 at B = 10,
 // 6.00 vs 6.12 at B = 32), at 2 quads neutral (profiles/r04_ab_xcdm_fc3_local.log)
+#ifndef WRNN_XCDM_PART_BATCH
+#define WRNN_XCDM_PART_BATCH 1   // GRU2 epilogue: operands hoisted above the barrier, the three gate partials' loads issued together (0: A/B)
+#endif
 #ifndef WRNN_XCDM_FC3_LOCAL_MINQ
 #define WRNN_XCDM_FC3_LOCAL_MINQ 3
 #endif
@@ -223,6 +226,39 @@ __device__ __forceinline__ float mpart(const float *P, int i, int n) {
 #pragma unroll
         for (int w = 0; w < kMWaves; ++w) t[w] = (u[w].x + u[w].y) + (u[w].z + u[w].w);
         return (t[0] + t[1]) + (t[2] + t[3]);
+    }
+}
+
+// mpart of rows i0, i0 + 16, i0 + 32 (the r, z, n gate rows of a unit) with every load issued
+// before the first add (a scheduling barrier between: hipcc pairs loads with their adds, one LDS
+// round trip per pair)
+template <int NQ>
+__device__ __forceinline__ void mpart3(const float *P, int i0, int n, float (&out)[3]) {
+    if constexpr (xcdm_big(NQ)) {
+        static_assert(kMWaves == 4, "one float4 of wave partials per output");
+        f4v u[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) u[q] = lds4(P + ((i0 + 16 * q) * (4 * NQ) + n) * kMWaves);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) out[q] = (u[q].x + u[q].y) + (u[q].z + u[q].w);
+    } else {
+        constexpr int S = xcdm_pstride_row(NQ);
+        f4v u[3][kMWaves];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const int i = i0 + 16 * q, ss = i >> 4, r = i & 15;
+#pragma unroll
+            for (int w = 0; w < kMWaves; ++w) u[q][w] = lds4(P + ((ss * kMWaves + w) * 16 + r) * S + 4 * n);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            float t[kMWaves];
+#pragma unroll
+            for (int w = 0; w < kMWaves; ++w) t[w] = (u[q][w].x + u[q][w].y) + (u[q][w].z + u[q][w].w);
+            out[q] = (t[0] + t[1]) + (t[2] + t[3]);
+        }
     }
 }
 
@@ -675,20 +711,48 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
             mlayer_any<NQ, MS_IH2, 3>(A, stg_h1, pbig, lane, wave);
             MST(3);
         }
+        // C's operands that the layer does not produce, read above the barrier (in registers
+        // across it: only the partials' loads remain after it)
+        // (not for the 4-quad RAW head: 4 more VGPRs than it has)
+        constexpr bool kHoistC = WRNN_XCDM_PART_BATCH && !(kRaw && NQ == 4);
+        float c_pi[3], c_gh[3], c_xi = 0.0f;
+        if (kHoistC && gru) {
+            const float *tr = rg + gn * kMRing;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const int i = q * 16 + gu;
+                c_pi[q] = fmaf(x, cst[MC_Q2 + i], tr[MT_P2 + gu * 3 + q]) + cst[MC_BIH2 + i];
+                c_gh[q] = gh2[i * NR + gn] + cst[MC_BHH2 + i];
+            }
+            c_xi = fmaf(cst[MC_WI0 + gu], x, tr[MT_CI + gu]);
+            asm volatile("" : "+v"(c_pi[0]), "+v"(c_pi[1]), "+v"(c_pi[2]), "+v"(c_gh[0]), "+v"(c_gh[1]), "+v"(c_gh[2]),
+                         "+v"(c_xi));
+        }
         bar();
         MST(4);
         // ---- C: GRU2 (:212-214) gate math → h2; y = (x_I + h1) + h2 (:212, :216)
         if (gru) {
             const float *tr = rg + gn * kMRing;
-            float gi[3], gh[3];
+            float gi[3], gh[3], xi;
+            if constexpr (kHoistC) {
+                float pp[3];
+                mpart3<NQ>(pbig, gu, gn, pp);
 #pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                const int i = q * 16 + gu;
-                gi[q] = mpart<NQ>(pbig, i, gn) + (fmaf(x, cst[MC_Q2 + i], tr[MT_P2 + gu * 3 + q]) + cst[MC_BIH2 + i]);
-                gh[q] = gh2[i * NR + gn] + cst[MC_BHH2 + i];
+                for (int q = 0; q < 3; ++q) {
+                    gi[q] = pp[q] + c_pi[q];
+                    gh[q] = c_gh[q];
+                }
+                xi = c_xi;
+            } else {
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    const int i = q * 16 + gu;
+                    gi[q] = mpart<NQ>(pbig, i, gn) + (fmaf(x, cst[MC_Q2 + i], tr[MT_P2 + gu * 3 + q]) + cst[MC_BIH2 + i]);
+                    gh[q] = gh2[i * NR + gn] + cst[MC_BHH2 + i];
+                }
+                xi = fmaf(cst[MC_WI0 + gu], x, tr[MT_CI + gu]);
             }
             h2v = gru_gate_math(gi[0], gi[1], gi[2], gh[0], gh[1], gh[2], h2v);
-            const float xi = fmaf(cst[MC_WI0 + gu], x, tr[MT_CI + gu]);
             const float y = (xi + h1v) + h2v;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the slot clears of B first
             ppub(pvec(xg, MH_Y, t) + gn * 512 + 16 * c + gu, y);
