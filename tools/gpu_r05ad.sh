@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round 5 A/B: next step's GRU1 terms pinned before the step-end abort branch (one LDS round trip
-# after the barrier) in the dense and sparse XCD kernels (in-tree) vs HEAD.
+# Round 5 A/B: fc3 partial hand-off as tagged 8-byte LDS pairs polled by the consumer (one LDS round trip
+# less) in the dense and sparse XCD kernels (in-tree) vs HEAD.
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"; export TMPDIR=/tmp; mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest tests/test_gpu_xcd.py tests/test_gpu_xcds.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r05ad_pytest.log 2>&1
 rc=$?; tail -3 gpurun_out/r05ad_pytest.log; [ $rc -eq 0 ] || exit $rc

@@ -86,14 +86,14 @@ __host__ __device__ inline XcdLds xcd_lds_layout() {
     l.h2 = o;    o += 512;
     l.sg = o;    o += 4 * 512;                // GRU1 terms of all units for the coming step
     l.w3 = o;    o += kXFcRows * 32;          // fc3 columns of the own f2 rows (waves 3, 4)
-    l.f2x = o;   o += 32;                     // wave 4's fc3 partials, handed to wave 3
+    l.f2x = o;   o += 64;                     // wave 4's fc3 partials, handed to wave 3: (value, tag) pairs
     l.ring = o;  o += kXRing * kXTerms;
     l.nz = o;    o += kXRing * kXNoise;
     l.gh2 = o;   o += 48;                     // W_hh2·h2 of the own units for the next step
     l.cst = o;   o += kXCst;
     l.xs = o;    o += 4;                      // x, by step parity
     l.misc = o;  o += 8;                      // [0] abort flag, [1] member index, step flags (step + 1):
-                                              // [2] h2 gathered, [3] f2x ready, [4] y gathered, [5] f1 gathered
+                                              // [2] h2 gathered, [3] (unused), [4] y gathered, [5] f1 gathered
     l.whh1 = o;  o += 48 * 512;
     l.whh2 = o;  o += (48 - kXH2RegRows) * 512;
     l.total = o;

@@ -87,6 +87,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
         misc[0] = 0;
         for (int i = 2; i < 8; ++i) misc[i] = 0;
     }
+    if (tid < 64) f2x[tid] = 0.0f;   // the fc3 hand-off pairs: tag 0, which no step carries
     __syncthreads();
     const int mem = __builtin_amdgcn_readfirstlane(misc[1]);   // wave-uniform: hop addresses in SGPRs
     if (mem < 0) return;
@@ -475,21 +476,27 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
 #pragma unroll
                 for (int g = 0; g < 4; ++g) p = fmaf(w3c[j + 2 * g], lane_bcast(f2, 16 * g), p);
             }
+            // wave 4 → wave 3: 8-byte (value, tag) pairs in LDS, polled by the consumer lanes
+            // themselves (one LDS round trip less than data + flag + a flag poll)
+            unsigned long long *f2p = reinterpret_cast<unsigned long long *>(f2x);
             if (hf == 1) {
-                if (lane < 32) f2x[lane] = p;
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                set_flag(f2ready, tag);
+                if (lane < 32)
+                    __hip_atomic_store(f2p + lane, ((unsigned long long)tag << 32) | __float_as_uint(p), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
             } else {
-                // wave 4 sets the flag on every path (its poll is bounded); the abort word ends the
-                // wait too should that ever change
+                // wave 4 stores on every path (its poll is bounded); the abort word ends the wait
+                // too should that ever change
                 unsigned spin = 0;
-                while (__hip_atomic_load(f2ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)tag) {
+                unsigned long long pv = (unsigned long long)tag << 32;
+                for (;;) {
+                    if (lane < 32) pv = __hip_atomic_load(f2p + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (__ballot((uint32_t)(pv >> 32) != tag) == 0) break;
                     if ((++spin & 255u) == 0 &&
                         __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
                         break;
                 }
-                asm volatile("" ::: "memory");
-                if (lane < kXF2Line) xpub_b(xgr, XGI(XH_F2) + c * kXF2Line + lane, tag, p + f2x[lane]);   // 30, 31: zero weights
+                if (lane < kXF2Line)   // 30, 31: zero weights
+                    xpub_b(xgr, XGI(XH_F2) + c * kXF2Line + lane, tag, p + __uint_as_float((uint32_t)pv));
                 XSTAMPW(6, 3);
             }
         } else if (more) {

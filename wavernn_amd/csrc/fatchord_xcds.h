@@ -75,7 +75,7 @@ __host__ __device__ inline XcdsLds xcds_lds_layout() {
     l.h2 = o;    o += kSR;
     l.sg = o;    o += 4 * kSR;                // GRU1 terms of all units for the coming step
     l.w3 = o;    o += kXFcRows * 32;          // fc3 columns of the own f2 rows (waves 0..3)
-    l.f2x = o;   o += 3 * 32;                 // waves 1..3's fc3 partials, handed to wave 0
+    l.f2x = o;   o += 3 * 64;                 // waves 1..3's fc3 partials, handed to wave 0: (value, tag) pairs
     l.ring = o;  o += kXRing * kSTerms;
     l.nz = o;    o += kXRing * kXNoise;
     l.gh2 = o;   o += 88;                     // W_hh2·h2 of the own units (u·3 + q) for the next step

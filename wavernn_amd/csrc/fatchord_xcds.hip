@@ -184,6 +184,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
         misc[0] = 0;
         for (int i = 2; i < 8; ++i) misc[i] = 0;
     }
+    if (tid < 3 * 64) f2x[tid] = 0.0f;   // the fc3 hand-off pairs: tag 0, which no step carries
     __syncthreads();
     const int mem = __builtin_amdgcn_readfirstlane(misc[1]);   // wave-uniform: hop addresses in SGPRs
     if (mem < 0) return;
@@ -484,24 +485,36 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
             float p = 0.0f;
 #pragma unroll
             for (int g = 0; g < 4; ++g) p = fmaf(w3c[g], lane_bcast(f2, 16 * g), p);
+            // waves 1..3 → wave 0: 8-byte (value, tag) pairs in LDS, polled by wave 0's lanes
+            // themselves (one LDS round trip less than data + flags + a flag poll)
+            unsigned long long *f2p = reinterpret_cast<unsigned long long *>(f2x);
             if (wave != 0) {
-                if (lane < 32) f2x[(wave - 1) * 32 + lane] = p;
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                set_flag(f2ready[wave - 1], tag);
+                if (lane < 32)
+                    __hip_atomic_store(f2p + (wave - 1) * 32 + lane, ((unsigned long long)tag << 32) | __float_as_uint(p),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             } else {
-                // waves 1..3 set their flags on every path (their polls are bounded); the abort word
-                // ends the wait too should that ever change
+                // waves 1..3 store on every path (their polls are bounded); the abort word ends the
+                // wait too should that ever change
                 unsigned spin = 0;
-                while ((__hip_atomic_load(f2ready[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)tag) |
-                       (__hip_atomic_load(f2ready[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)tag) |
-                       (__hip_atomic_load(f2ready[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)tag)) {
+                unsigned long long pv[3] = {(unsigned long long)tag << 32, (unsigned long long)tag << 32,
+                                            (unsigned long long)tag << 32};
+                for (;;) {
+                    if (lane < 32) {
+#pragma unroll
+                        for (int w = 0; w < 3; ++w)
+                            pv[w] = __hip_atomic_load(f2p + w * 32 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                    const bool ok = ((uint32_t)(pv[0] >> 32) == tag) & ((uint32_t)(pv[1] >> 32) == tag) &
+                                    ((uint32_t)(pv[2] >> 32) == tag);
+                    if (__ballot(!ok) == 0) break;
                     if ((++spin & 255u) == 0 &&
                         __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
                         break;
                 }
-                asm volatile("" ::: "memory");
                 if (lane < kXF2Line)   // 30, 31: zero weights
-                    xpub_b(xgr, XGI(XH_F2) + c * kXF2Line + lane, tag, ((p + f2x[lane]) + f2x[32 + lane]) + f2x[64 + lane]);
+                    xpub_b(xgr, XGI(XH_F2) + c * kXF2Line + lane, tag,
+                           ((p + __uint_as_float((uint32_t)pv[0])) + __uint_as_float((uint32_t)pv[1])) +
+                               __uint_as_float((uint32_t)pv[2]));
                 XSTAMPW(6, 0);
                 // ---- hop F2: Σ of the 32 workgroups' partials + b3 → sample
                 const int jp = lane & 15, pg = lane >> 4;
