@@ -65,9 +65,17 @@ __host__ __device__ inline DxSlab dx_slab_layout() {
 
 // Hand-off vectors of one XCD, row n (0..3) = launch row k + 8n; granules {tag = step + 1, value}
 enum DxHop { DX_HC = 0, DX_O1 = 1, DX_LC = 2, DX_HF = 3, DX_O3 = 4, DX_LF = 5, kDxHops = 6 };
-constexpr long long kDxHopOff[kDxHops] = {0, 4 * kDxS, 8 * kDxS, 8 * kDxS + 4 * kDxQ, 12 * kDxS + 4 * kDxQ,
-                                          16 * kDxS + 4 * kDxQ};
-constexpr long long kDxXcdStride = 16 * kDxS + 8 * kDxQ + 64;   // granules per XCD
+#ifndef WRNN_DX_PAD
+#define WRNN_DX_PAD 1   // 448-wide hop rows padded to 16 granules per workgroup (one 128-B line each)
+#endif
+// row stride (granules) of the 448-wide hop vectors (h_c, o1, h_f, o3): with WRNN_DX_PAD each
+// workgroup's 14 granules start a 128-byte line of their own (16 granules, the last two written
+// as pads with the tag) instead of sharing lines with the neighbouring workgroups
+constexpr int kDxSP = WRNN_DX_PAD ? 16 * kXcdWgs : kDxS;
+constexpr int kDxUP = kDxSP / kXcdWgs;   // granules per workgroup and row (16 or 14)
+constexpr long long kDxHopOff[kDxHops] = {0, 4 * kDxSP, 8 * kDxSP, 8 * kDxSP + 4 * kDxQ, 12 * kDxSP + 4 * kDxQ,
+                                          16 * kDxSP + 4 * kDxQ};
+constexpr long long kDxXcdStride = 16 * kDxSP + 8 * kDxQ + 64;   // granules per XCD
 
 // Carried state per workgroup (time-chunked launches): h of the own units [4 rows][28], the R·h
 // partials (LDS image of ll.pr / ll.prq), previous labels [2][4]

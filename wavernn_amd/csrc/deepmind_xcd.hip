@@ -54,14 +54,21 @@ __device__ __forceinline__ f2v lds2(const float *p) { return *reinterpret_cast<c
 __device__ __forceinline__ float fast_log(float q) { return __builtin_amdgcn_logf(q) * 0.693147180559945309f; }
 __device__ __forceinline__ f4v log4(f4v q) { return f4v{fast_log(q.x), fast_log(q.y), fast_log(q.z), fast_log(q.w)}; }
 
-// wave w's slice of a 448-wide hop vector, 4 rows: 224 granule pairs, pair p = min(lane + 64i,
-// 223) (i < 4; lanes 32..63 of i = 3 repeat pairs 192..223): row p / 56, columns
-// 112w + 2(p % 56) + {0, 1}
+// wave w's slice of a 448-wide hop vector, 4 rows: columns 112w .. 112w + 111 = the 14 units of
+// workgroups 8w .. 8w + 7.  Padded rows (WRNN_DX_PAD): 256 granule pairs, pair p = lane + 64i:
+// row p / 64, workgroup 8w + (p % 64) / 8, units 2((p % 64) % 8) + {0, 1} (pair 7 of a workgroup
+// = its two pads).  Unpadded: 224 pairs, p = min(lane + 64i, 223) (lanes 32..63 of i = 3 repeat
+// pairs 192..223): row p / 56, columns 112w + 2(p % 56) + {0, 1}.
 __device__ __forceinline__ int dx_pair(int lane, int i) {
     const int p = lane + 64 * i;
+    if constexpr (WRNN_DX_PAD) return p;
     return p < 224 ? p : p - 32;
 }
 __device__ __forceinline__ int dx_poll_off(int w, int p) {   // bytes
+    if constexpr (WRNN_DX_PAD) {
+        const int n = p >> 6, q = p & 63;
+        return (n * kDxSP + kDxUP * 8 * w + 2 * q) * 8;
+    }
     const int n = p / 56, cp = p - 56 * n;
     return (n * kDxS + kDxKW * w + 2 * cp) * 8;
 }
@@ -90,12 +97,23 @@ __device__ __forceinline__ void dx_poll(__amdgpu_buffer_rsrc_t r, int w, uint32_
     }
 }
 
-// polled pairs → the wave's staging rows [n][kDxST]
+// polled pairs → the wave's staging rows [n][kDxST] (column 2·pair within the row's 112; the
+// padded form skips each workgroup's pad pair)
 __device__ __forceinline__ void dx_stage(float *stg, int lane, const u4v (&v)[4]) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int p = dx_pair(lane, i), n = p / 56, cp = p - 56 * n;
-        *reinterpret_cast<f2v *>(stg + n * kDxST + 2 * cp) = f2v{__uint_as_float(v[i].x), __uint_as_float(v[i].z)};
+        const int p = dx_pair(lane, i);
+        int n, col;
+        if constexpr (WRNN_DX_PAD) {
+            const int q = p & 63;
+            n = p >> 6;
+            col = 14 * (q >> 3) + 2 * (q & 7);
+            if ((q & 7) == 7) continue;   // pads
+        } else {
+            n = p / 56;
+            col = 2 * (p - 56 * n);
+        }
+        *reinterpret_cast<f2v *>(stg + n * kDxST + col) = f2v{__uint_as_float(v[i].x), __uint_as_float(v[i].z)};
     }
 }
 
@@ -438,6 +456,17 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         if (kDbg && lane == 0 && (unsigned)(t - a.t0 - kDxDbgSkip) < (unsigned)kDxDbgSteps)
             dbgs[((t - a.t0 - kDxDbgSkip) * kDxWaves + wave) * kDxStamps + kDxStamps - 1] =
                 (unsigned)__builtin_amdgcn_s_memrealtime();
+        // the pads of this step's 448-wide hop rows (lanes 56..63 of wave 0: 4 rows × 2 per hop),
+        // tagged like the data: every workgroup has finished polling step t − 1's vectors before
+        // any workgroup starts step t (its logits came after those polls)
+        if (WRNN_DX_PAD && wave == 0 && lane >= 4 * kDxU) {
+            const int pl = lane - 4 * kDxU;
+            unsigned long long *pad = xg + (pl >> 1) * kDxSP + kDxUP * c + kDxU + (pl & 1);
+            xpub(pad + kDxHopOff[DX_HC], tag, 0.0f);
+            xpub(pad + kDxHopOff[DX_O1], tag, 0.0f);
+            xpub(pad + kDxHopOff[DX_HF], tag, 0.0f);
+            xpub(pad + kDxHopOff[DX_O3], tag, 0.0f);
+        }
         // ---- coarse gates (:106-125): R·h_{t-1} (partials of the previous step), I_coarse(prev)
         if (gate) {
             // every LDS operand of the gate chain issued at once (one round trip: hipcc otherwise
@@ -461,7 +490,7 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             const float rr = sigmoid_((Rg[1] + I[1]) + br);
             const float ee = tanh_((rr * Rg[2] + I[2]) + be);
             hc = uu * hc + (1.0f - uu) * ee;
-            xpub(xg + kDxHopOff[DX_HC] + gn * kDxS + kDxU * c + gu, tag, hc);
+            xpub(xg + kDxHopOff[DX_HC] + gn * kDxSP + kDxUP * c + gu, tag, hc);
             DST(19);
             DSTR(22);   // (s_memrealtime: the h_c hop measured across workgroups, tools/stamps_dx.py)
         }
@@ -504,7 +533,7 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         if (tid < 4 * kDxU) {
             const int r = tid % kDxU, n = tid / kDxU;
             const float o = dx_o13sum(po1, r, n) + bo1;
-            xpub(xg + kDxHopOff[DX_O1] + n * kDxS + kDxU * c + r, tag, o > 0.0f ? o : 0.0f);
+            xpub(xg + kDxHopOff[DX_O1] + n * kDxSP + kDxUP * c + r, tag, o > 0.0f ? o : 0.0f);
         } else if (more && lt >= 0) {   // log q of step t + 1 → ring slot (t + 1) & 1
             float *slot = nzr + ((t + 1) & 1) * 4 * 2 * kDxQ;
 #pragma unroll
@@ -618,7 +647,7 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             const float rr = sigmoid_((Rg[1] + I[1]) + br);
             const float ee = tanh_((rr * Rg[2] + I[2]) + be);
             hf = uu * hf + (1.0f - uu) * ee;
-            xpub(xg + kDxHopOff[DX_HF] + gn * kDxS + kDxU * c + gu, tag, hf);
+            xpub(xg + kDxHopOff[DX_HF] + gn * kDxSP + kDxUP * c + gu, tag, hf);
         }
         DST(10);
         // ---- h_f slice → O3 → relu → o3
@@ -636,7 +665,7 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         if (tid < 4 * kDxU) {
             const int r = tid % kDxU, n = tid / kDxU;
             const float o = dx_o13sum(po3, r, n) + bo3;
-            xpub(xg + kDxHopOff[DX_O3] + n * kDxS + kDxU * c + r, tag, o > 0.0f ? o : 0.0f);
+            xpub(xg + kDxHopOff[DX_O3] + n * kDxSP + kDxUP * c + r, tag, o > 0.0f ? o : 0.0f);
         }
         DST(13);
         // ---- R[rows 0..47, S:]·h_f finishes group A of R·h_t (the gates above have read R·h_{t-1})
