@@ -2,7 +2,7 @@
 # A/B of library builds on the GPU box: a parity run on the in-tree build, then one timing
 # command per build, each in its own process (TIME_DM_LIB), the in-tree build first and the list
 # repeated (box drift).  Builds: python tools/build_alt.py <name> <source.hip> -DFLAG=V → tools/_alt/<name>.so
-#   tools/ab.sh "<pytest files>" "<timing command>" <name>...
+#   tools/ab.sh "<pytest files>" "<timing commands (bash -c)>" <name>...
 #   e.g. tools/ab.sh tests/test_gpu_dx.py "python -u tools/time_dm.py 8 32" ride0
 #        tools/ab.sh tests/test_gpu_xcd.py "python -u tools/time_any.py --mode MOL --L 20000 --B 1,8 --paths xcd" packf2_0
 # (round 5's one-off drivers, tools/gpu_r05*.sh in git history, were this with fixed arguments;
@@ -18,6 +18,6 @@ for n in "$@"; do libs+=("tools/_alt/$n.so"); done
 for rep in 1 2 3; do
   for lib in "${libs[@]}"; do
     echo "== $lib"
-    TIME_DM_LIB=$PWD/$lib timeout -k 10 120 $cmd 2>&1 | grep us/step || exit 1
+    TIME_DM_LIB=$PWD/$lib timeout -k 10 300 bash -c "$cmd" 2>&1 | grep us/step || exit 1
   done
 done

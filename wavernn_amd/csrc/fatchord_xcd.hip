@@ -358,23 +358,16 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
             const int goff = pg * 8 * kXF2Line * 8 + jp * 16;
             const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
             unsigned spins = 0;
-            float pa[8], pb[8];
+            // the polled pieces live in wr[0..7] (wave 0 holds no weights there), polled in place
+            // and read after the loop (the abort path zeroes them there: no copies on the exit)
+            u4v *v = reinterpret_cast<u4v *>(&wr[0]);
             for (;;) {
-                // the polled pieces live in wr[0..7] (wave 0 holds no weights there)
-                u4v *v = reinterpret_cast<u4v *>(&wr[0]);
 #pragma unroll
                 for (int m = 0; m < 8; ++m) v[m] = ld16_sc1(rf, goff + m * kXF2Line * 8);
                 bool ok = true;
 #pragma unroll
                 for (int m = 0; m < 8; ++m) ok &= (v[m].y == tag) & (v[m].w == tag);
-                if (__ballot(!ok) == 0) {   // wave-uniform exit: no exec-mask branches, no copies
-#pragma unroll
-                    for (int m = 0; m < 8; ++m) {
-                        pa[m] = __uint_as_float(v[m].x);
-                        pb[m] = __uint_as_float(v[m].z);
-                    }
-                    break;
-                }
+                if (__ballot(!ok) == 0) break;   // wave-uniform exit: no exec-mask branches
                 if ((++spins & 63u) == 0) {
                     const bool late = (long long)(__builtin_amdgcn_s_memrealtime() - c0) > a.timeout_ticks;
                     const bool other = __hip_atomic_load(&a.ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
@@ -382,10 +375,16 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
                         if (late) record_abort(a.ctl, -4, t, XH_F2, blockIdx.x);
                         *abort_flag = 1;
 #pragma unroll
-                        for (int m = 0; m < 8; ++m) pa[m] = pb[m] = 0.0f;
+                        for (int m = 0; m < 8; ++m) v[m] = u4v{0u, 0u, 0u, 0u};
                         break;
                     }
                 }
+            }
+            float pa[8], pb[8];
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                pa[m] = __uint_as_float(v[m].x);
+                pb[m] = __uint_as_float(v[m].z);
             }
             XSTAMP(7);
 #pragma unroll
@@ -396,7 +395,8 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
                     pb[m] += pb[m + n];
                 }
             // + the other producer groups (lanes l ^ 16, l ^ 32): identical bits in all four
-            const float la = cross_rows(pa[0]) + b3a, lb = cross_rows(pb[0]) + b3b;   // logits 2jp, 2jp+1
+            cross_rows_pair(pa[0], pb[0]);
+            const float la = pa[0] + b3a, lb = pb[0] + b3b;   // logits 2jp, 2jp+1
             x = mol_sample_pairs(la, lb, ua, ub, u10, jp);
             if (lane == 0) {
                 xs[t & 1] = x;

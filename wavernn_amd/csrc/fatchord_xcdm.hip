@@ -465,7 +465,8 @@ __device__ __forceinline__ float msample(const unsigned long long *f2, int n, ui
             pa[m] += pa[m + w];
             pb[m] += pb[m + w];
         }
-    const float la = cross_rows(pa[0]) + b3a, lb = cross_rows(pb[0]) + b3b;
+    cross_rows_pair(pa[0], pb[0]);
+    const float la = pa[0] + b3a, lb = pb[0] + b3b;   // logits 2jp, 2jp+1
     return mol_sample_pairs(la, lb, ua, ub, u10, jp);
 }
 

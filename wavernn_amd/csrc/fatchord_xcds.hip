@@ -557,7 +557,8 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
                         pa[m] += pa[m + n];
                         pb[m] += pb[m + n];
                     }
-                const float la = cross_rows(pa[0]) + b3a, lb = cross_rows(pb[0]) + b3b;   // logits 2jp, 2jp+1
+                cross_rows_pair(pa[0], pb[0]);
+                const float la = pa[0] + b3a, lb = pb[0] + b3b;   // logits 2jp, 2jp+1
                 x = mol_sample_pairs(la, lb, ua, ub, u10, jp);
                 if (lane == 0) {
                     xs[t & 1] = x;

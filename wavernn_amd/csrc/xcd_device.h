@@ -15,6 +15,9 @@ namespace wrnn {
 #ifndef WRNN_XCD_UNIFORM_WAVE
 #define WRNN_XCD_UNIFORM_WAVE 1   // the XCD kernels' wave index through readfirstlane (0: per-lane, A/B)
 #endif
+#ifndef WRNN_XCD_LEAN_SAMPLER
+#define WRNN_XCD_LEAN_SAMPLER 1   // sampler: both logit sums through one permlane chain, med3 clamps, max + DPP as one instruction
+#endif
 #ifndef WRNN_XCD_FAST_EXP
 #define WRNN_XCD_FAST_EXP 1     // sampler scale e^s by v_exp_f32 (A/B vs libm expf: 3.92 -> 3.88 us/step, parity unchanged)
 #endif
@@ -47,6 +50,44 @@ __device__ __forceinline__ float perm_sum32(float v) {   // + the same lane of t
 }
 // Σ over the 4 DPP rows of a wave (identical bits in the lanes it pairs)
 __device__ __forceinline__ float cross_rows(float v) { return perm_sum32(perm_sum16(v)); }
+// cross_rows of two values at once (the same sums, bit for bit: (r0 + r1) + (r2 + r3)): the
+// permlane16 swap of (a, b) leaves the row-pair sums of a in one row of each pair and those of b
+// in the other, permlane32 adds the pairs, a last permlane16 swap spreads each total to every row
+// (whichever way the swap pairs its rows, a ends in its first result).  3 permlanes + 2 adds
+// instead of 4 + 4.
+__device__ __forceinline__ void cross_rows2(float &a, float &b) {
+    const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    const float p = __uint_as_float(s[0]) + __uint_as_float(s[1]);
+    const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(p), __float_as_uint(p), false, false);
+    const float r = __uint_as_float(q[0]) + __uint_as_float(q[1]);
+    const auto t = __builtin_amdgcn_permlane16_swap(__float_as_uint(r), __float_as_uint(r), false, false);
+    a = __uint_as_float(t[0]);
+    b = __uint_as_float(t[1]);
+}
+__device__ __forceinline__ void cross_rows_pair(float &a, float &b) {
+    if (WRNN_XCD_LEAN_SAMPLER) {
+        cross_rows2(a, b);
+    } else {
+        a = cross_rows(a);
+        b = cross_rows(b);
+    }
+}
+// max over each 8-lane group (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror), one v_max_f32
+// with the DPP source per stage (hipcc emits mov_dpp + a canonicalising max + max); the s_nop 1
+// covers the VALU-write → DPP-read hazard the compiler does not see inside the asm
+__device__ __forceinline__ float max8_dpp(float v) {
+    float r;
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_max_f32_dpp %0, %1, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "s_nop 1\n\t"
+        "v_max_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "s_nop 1\n\t"
+        "v_max_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1"
+        : "=&v"(r)
+        : "v"(v));
+    return r;
+}
 
 // MoL sampler (utils/distribution.py:87-123) on logits held in pairs: lane jp (of every DPP row)
 // holds logits 2jp (la) and 2jp+1 (lb); ua / ub = log(-log u1) of those mixture indices (jp < 5).
@@ -55,17 +96,26 @@ __device__ __forceinline__ float cross_rows(float v) { return perm_sum32(perm_su
 // formed beside the argmax (lanes 5..9 hold the means of k = 2(jp − 5) + {0, 1}, row_shl:5 brings
 // the matching log-scales from lanes 10..14), so only a lane read follows it.  Result wave-uniform.
 __device__ __forceinline__ float mol_sample_pairs(float la, float lb, float ua, float ub, float u10, int jp) {
-    const float sa = fmaxf(WRNN_DPP(la, 0x105), -32.23619130191664f);   // row_shl:5: lane jp + 5
-    const float sb = fmaxf(WRNN_DPP(lb, 0x105), -32.23619130191664f);
+    // row_shl:5: lane jp + 5; max with the clamp bound (med3 with +inf: the same for every
+    // non-NaN value, without fmaxf's canonicalising extra max)
+    const float sa = WRNN_XCD_LEAN_SAMPLER ? __builtin_amdgcn_fmed3f(WRNN_DPP(la, 0x105), -32.23619130191664f, INFINITY)
+                                           : fmaxf(WRNN_DPP(la, 0x105), -32.23619130191664f);
+    const float sb = WRNN_XCD_LEAN_SAMPLER ? __builtin_amdgcn_fmed3f(WRNN_DPP(lb, 0x105), -32.23619130191664f, INFINITY)
+                                           : fmaxf(WRNN_DPP(lb, 0x105), -32.23619130191664f);
 #if WRNN_XCD_FAST_EXP
     float xa = la + fast_exp(sa) * u10, xb = lb + fast_exp(sb) * u10;
 #else
     float xa = la + expf(sa) * u10, xb = lb + expf(sb) * u10;
 #endif
-    xa = xa < -1.0f ? -1.0f : xa;
-    xa = xa > 1.0f ? 1.0f : xa;
-    xb = xb < -1.0f ? -1.0f : xb;
-    xb = xb > 1.0f ? 1.0f : xb;
+    if (WRNN_XCD_LEAN_SAMPLER) {   // (finite x: the same clamp)
+        xa = __builtin_amdgcn_fmed3f(xa, -1.0f, 1.0f);
+        xb = __builtin_amdgcn_fmed3f(xb, -1.0f, 1.0f);
+    } else {
+        xa = xa < -1.0f ? -1.0f : xa;
+        xa = xa > 1.0f ? 1.0f : xa;
+        xb = xb < -1.0f ? -1.0f : xb;
+        xb = xb > 1.0f ? 1.0f : xb;
+    }
     float v = -INFINITY;
     int i = 64;
     if (jp < 5) {
@@ -85,9 +135,14 @@ __device__ __forceinline__ float mol_sample_pairs(float la, float lb, float ua, 
         // the components grow with the lane (lane jp: 2jp, 2jp + 1), so the winner is the first of
         // lanes 0..4 holding the max: three value-only DPP stages cover lanes 0..7 (every DPP row
         // holds the same bits), a ballot finds the lane (wave_argmax_ordered, specialised)
-        float mv = fmaxf(v, WRNN_DPP(v, 0xB1));
-        mv = fmaxf(mv, WRNN_DPP(mv, 0x4E));
-        mv = fmaxf(mv, WRNN_DPP(mv, 0x141));
+        float mv;
+        if (WRNN_XCD_LEAN_SAMPLER) {
+            mv = max8_dpp(v);
+        } else {
+            mv = fmaxf(v, WRNN_DPP(v, 0xB1));
+            mv = fmaxf(mv, WRNN_DPP(mv, 0x4E));
+            mv = fmaxf(mv, WRNN_DPP(mv, 0x141));
+        }
         const float m = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, mv)));
         const unsigned long long hit = __ballot(v == m) & 0x1Full;
         if (hit != 0) {
