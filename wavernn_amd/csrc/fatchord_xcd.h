@@ -15,7 +15,8 @@ constexpr int kXFcRows = 16;        // fc1 / fc2 rows per workgroup (F / kXcdWgs
 // wave roles (all eight compute GRU1 and GRU2):
 //   0     samples (polls F2); W_hh1 rows 0..9; W_hh2 rows 24..27 in VGPRs
 //   1, 2  fc1 rows 8h..8h+7 (h = w − 1) from the polled y, weights in VGPRs; W_hh2 LDS rows
-//   3, 4  fc2 rows 8h..8h+7 (h = w − 3) from the polled f1 + their fc3 partials; W_hh1 rows
+//   3, 4  fc2 rows 8h..8h+7 (h = w − 3) from the polled f1 + their fc3 partials; W_hh1 rows;
+//         wave 4 then gathers a quarter of the next step's GRU1 terms
 //   5..7  W_hh2 rows 8(w − 5)..+7 in VGPRs; W_hh1 rows (5, 7), the h2 gather (6)
 constexpr int kXWaveFc1 = 1, kXWaveFc2 = 3;
 constexpr int kXH2RegRows = 28;     // W_hh2 rows 0..27 in VGPRs, 28..47 in LDS

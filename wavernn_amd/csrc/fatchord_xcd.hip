@@ -22,7 +22,8 @@
 //   redundantly and bit-identically in every workgroup) → x_t.
 // Off the critical path, waves 1..7: W_hh1·h1 (LDS weights) → the GRU1 terms of step t+1 →
 // publish (hop S, double-buffered), gather h2 (wave 6) → W_hh2·h2 (VGPR weights) for the next
-// GRU2, gather S (waves 5, 6), LDS-DMA of the conditioning terms and noise (wave 7).
+// GRU2, gather S (waves 1, 2, 5 and fc2 wave 4, a quarter each), the conditioning terms and
+// noise of step t+2 into the LDS ring (wave 7).
 //
 // Membership: each workgroup reads its XCC id from the hardware register and takes an index
 // from a per-XCD arrival counter, so correctness never depends on the dispatcher's placement
@@ -58,6 +59,15 @@ namespace wrnn {
 #define WRNN_XCD_PRIO 0         // s_setprio of wave 0 (the poller / sampler)
 #endif
 
+// the wave that gathers the fourth quarter of the next step's GRU1 terms: 4 (an fc2 wave, idle
+// after its fc3 hand-off) — wave 6 gathered it after h2, and its W_hh2·h2 then ended with the
+// sampler (both at the step-end barrier); 6: as before, 3: the other fc2 wave (A/B)
+#ifndef WRNN_XCD_SQ3_WAVE
+#define WRNN_XCD_SQ3_WAVE 4
+#endif
+#ifndef WRNN_XCD_STAMP_W13
+#define WRNN_XCD_STAMP_W13 5    // stamped builds: the wave whose W_hh2·h2 end is stamp 13 (6: the h2 gatherer)
+#endif
 #define XSTAMPW(kk, w)                                                                                        \
     do {                                                                                                      \
         if (kDbg && a.dbg && wave == (w) && lane == 0 && t - a.t0 < a.dbg_steps)                              \
@@ -207,9 +217,10 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
         const int rr = rb + 2 * li + eng;
         if (li < np) gh2s[rr] = li == 0 ? gh[0] : li == 1 ? gh[1] : li == 2 ? gh[2] : li == 3 ? gh[3] : gh[4];
     };
-    // a quarter of step t's GRU1 terms (waves 1, 2, 5, 6: 512 granules each, one poll round)
+    // a quarter of step t's GRU1 terms (waves 1, 2, 5, WRNN_XCD_SQ3_WAVE: 512 granules each, one
+    // poll round)
     auto gather_terms = [&](int t) {
-        const int qq = wave <= 2 ? wave - 1 : wave - 3;
+        const int qq = wave == 1 ? 0 : wave == 2 ? 1 : wave == 5 ? 2 : 3;
         xgather16<4>(XG(XH_S0 + (t & 1)) + qq * 512, (uint32_t)t + 1u, a.ctl, a.timeout_ticks, t, XH_S0 + (t & 1),
                      abort_flag, lane, [&](int i, float v0, float v1) {
                          *reinterpret_cast<f2v *>(sg + qq * 512 + i) = f2v{v0, v1};
@@ -254,7 +265,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
             const float z5[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
             publish_terms(0, z5);
         }
-        if (wave == 1 || wave == 2 || wave == 5 || wave == 6) {
+        if (wave == 1 || wave == 2 || wave == 5 || wave == WRNN_XCD_SQ3_WAVE) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             gather_terms(0);
         }
@@ -499,10 +510,17 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
                     xpub_b(xgr, XGI(XH_F2) + c * kXF2Line + lane, tag, p + __uint_as_float((uint32_t)pv));
                 XSTAMPW(6, 3);
             }
+            // the fourth quarter of the next step's GRU1 terms (this wave has polled F1 itself:
+            // the hop F1 window is over)
+            if ((WRNN_XCD_SQ3_WAVE == 3 || WRNN_XCD_SQ3_WAVE == 4) && wave == WRNN_XCD_SQ3_WAVE && more &&
+                !WRNN_XCD_SKIP_RECUR && !WRNN_XCD_SKIP_SG) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                gather_terms(t + 1);
+            }
         } else if (more) {
             // ---- waves 5..7: W_hh1 rows (5, 7) → after y gathered their terms and h2 out; after
-            // f1 gathered: h2 (wave 6, then flag), S quarters (5, 6), the ring (7); after h2
-            // gathered: W_hh2·h2 (VGPR rows)
+            // f1 gathered: h2 (wave 6, then flag), an S quarter (5; 6 with WRNN_XCD_SQ3_WAVE 6),
+            // the ring (7); after h2 gathered: W_hh2·h2 (VGPR rows)
             if (WRNN_XCD_SKIP_RECUR) {
                 if (wave == 7) {
                     wait_flag(f1got, tag);
@@ -535,7 +553,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
                 XSTAMPW(10, 6);
             }
             if (wave <= 6) {
-                if (!WRNN_XCD_SKIP_SG) {
+                if (!WRNN_XCD_SKIP_SG && (wave == 5 || WRNN_XCD_SQ3_WAVE == 6)) {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     gather_terms(t + 1);
                 }
@@ -558,7 +576,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
                 for (int p = 0; p < 4; ++p) gh[p] = e32dot(*reinterpret_cast<const f4v(*)[4]>(&wr[4 * p]), hx);
                 gh[4] = 0.0f;
                 gh2_store(8 * (wave - 5), 4, gh);
-                XSTAMPW(13, 5);
+                XSTAMPW(13, WRNN_XCD_STAMP_W13);
             }
         }
     step_end:
