@@ -2,7 +2,8 @@
 (s_memrealtime, 100 MHz, wave 0 of every workgroup).  For each step, times are relative to the
 earliest step start over the XCD's 32 workgroups; the table gives the median over steps of the
 min / median / max over the workgroups.
-    python tools/stamps_xcd.py [L] [sparse]     (sparse: the rnn-896 block-sparse kernel, fatchord_xcds.hip)"""
+    python tools/stamps_xcd.py [L] [sparse]     (sparse: the rnn-896 block-sparse kernel, fatchord_xcds.hip)
+(GRU2_STAMPS=1 / BAR_STAMPS=1 with TIME_DM_LIB: the labels of those diagnostic builds)"""
 import os
 import sys
 
@@ -33,6 +34,11 @@ def main(L=3000, sparse=0):
     labels = dict(SPARSE_STAMPS if sparse else STAMPS)
     if os.environ.get("GRU2_STAMPS"):   # the WRNN_XCDS_GRU2_STAMPS build: slots 12..14 inside GRU2
         labels.update({12: "w0: GRU2 block-row dots", 13: "w0: GRU2 z/n exchanged", 14: "w0: GRU2 gate math"})
+    if os.environ.get("BAR_STAMPS"):   # the WRNN_XCD_BAR_STAMPS build: every wave's step-end barrier arrival
+        for k in (3, 9, 10, 11, 12, 13, 14):
+            labels.pop(k, None)
+        labels.update({9 + i: f"w{1 + i}: at the end barrier" for i in range(6)})
+        labels[3] = "w7: at the end barrier"
     os.makedirs("gpurun_out", exist_ok=True)
     path = "gpurun_out/stamps_xcd.bin"
     os.environ["WRNN_DEBUG_STAMPS"] = str(L)

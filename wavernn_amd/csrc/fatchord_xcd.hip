@@ -70,10 +70,18 @@ namespace wrnn {
 #endif
 #define XSTAMPW(kk, w)                                                                                        \
     do {                                                                                                      \
-        if (kDbg && a.dbg && wave == (w) && lane == 0 && t - a.t0 < a.dbg_steps)                              \
+        if (kDbg && a.dbg && wave == (w) && lane == 0 && t - a.t0 < a.dbg_steps &&                            \
+            (!WRNN_XCD_BAR_STAMPS || ((kk) != 3 && ((kk) < 9 || (kk) > 14))))                                 \
             a.dbg[((size_t)mem * a.dbg_steps + (t - a.t0)) * kStamps + (kk)] = (unsigned)__builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #define XSTAMP(kk) XSTAMPW(kk, 0)
+// diagnostics (WRNN_XCD_BAR_STAMPS): waves 1..6 → stamps 9..14, wave 7 → stamp 3, at the step-end barrier
+#define XSTAMP_BAR()                                                                                          \
+    do {                                                                                                      \
+        if (WRNN_XCD_BAR_STAMPS && kDbg && a.dbg && wave > 0 && lane == 0 && t - a.t0 < a.dbg_steps)          \
+            a.dbg[((size_t)mem * a.dbg_steps + (t - a.t0)) * kStamps + (wave == 7 ? 3 : 8 + wave)] =          \
+                (unsigned)__builtin_amdgcn_s_memrealtime();                                                   \
+    } while (0)
 
 template <bool kDbg>
 __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
@@ -580,6 +588,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
             }
         }
     step_end:
+        XSTAMP_BAR();
         bar();
         // next step's x, GRU1 terms and the abort word: one LDS round trip
         const int ab = *abort_flag;

@@ -21,10 +21,12 @@
 // Four rows per fc wave (round 5; eight on two waves before: fc1's 8 × 7 weight pairs per lane
 // spilled 28 VGPRs).  Off the critical path, in each wave's idle windows: waves 0..3 (idle from
 // GRU2 until f1 arrives) W_hh1·h1 (LDS blocks, one engine per gate block-row, 21 = 16 + 5) → the
-// GRU1 terms of step t+1, published after "y gathered", and h2; waves 4..7 (idle from their f1
-// publish to the step's end) h2 out, after "f1 gathered": the h2 gather (wave 4), the four S
-// quarters, the ring (wave 7), then W_hh2·h2 (LDS blocks, 16 + 5 engines).  fp32, sums
-// re-associated (tolerance-checked).
+// GRU1 terms of step t+1, published after "y gathered", and h2; waves 1..3 after their fc3
+// hand-off and wave 6 the four quarters of the next S (round 5: on waves 4..7 before, which then
+// arrived last at the step-end barrier: 3.63 → 3.42 µs/step); waves 4..7 (idle from their f1
+// publish to the step's end) h2 out, after "f1 gathered": the h2 gather (wave 4), the ring
+// (wave 7), then W_hh2·h2 (LDS blocks, 16 + 5 engines).  fp32, sums re-associated
+// (tolerance-checked).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -152,12 +154,24 @@ __device__ __forceinline__ float sp_block_row(const f4v (&wa)[4], const f4v (&wb
 #endif
 }
 
+#ifndef WRNN_XCDS_SQ_EARLY
+#define WRNN_XCDS_SQ_EARLY 1   // S quarters on waves 1, 3, 6, 2 (0: on the fc1 waves 4..7, A/B)
+#endif
+
 #define XSTAMPW(kk, w)                                                                                        \
     do {                                                                                                      \
-        if (kDbg && a.dbg && wave == (w) && lane == 0 && t - a.t0 < a.dbg_steps)                              \
+        if (kDbg && a.dbg && wave == (w) && lane == 0 && t - a.t0 < a.dbg_steps &&                            \
+            (!WRNN_XCD_BAR_STAMPS || ((kk) != 3 && ((kk) < 9 || (kk) > 14))))                                 \
             a.dbg[((size_t)mem * a.dbg_steps + (t - a.t0)) * kStamps + (kk)] = (unsigned)__builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #define XSTAMP(kk) XSTAMPW(kk, 0)
+// diagnostics (WRNN_XCD_BAR_STAMPS): waves 1..6 → stamps 9..14, wave 7 → stamp 3, at the step-end barrier
+#define XSTAMP_BAR()                                                                                          \
+    do {                                                                                                      \
+        if (WRNN_XCD_BAR_STAMPS && kDbg && a.dbg && wave > 0 && lane == 0 && t - a.t0 < a.dbg_steps)          \
+            a.dbg[((size_t)mem * a.dbg_steps + (t - a.t0)) * kStamps + (wave == 7 ? 3 : 8 + wave)] =          \
+                (unsigned)__builtin_amdgcn_s_memrealtime();                                                   \
+    } while (0)
 
 template <bool kDbg>
 __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a) {
@@ -303,10 +317,13 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
             gh2s[(4 * ub + li) * 3 + q] = g;
         }
     };
-    // a quarter of step t's GRU1 terms (waves 4..7: 896 granules each, one poll round)
+    // a quarter of step t's GRU1 terms (896 granules each, one poll round): waves 1, 3, 6, 2
+    // (quarters 0..3; fc2 waves 1..3 are idle after their fc3 hand-off, the fc1 waves were the last
+    // at the step-end barrier) — WRNN_XCDS_SQ_EARLY 0: waves 4..7
+    auto sq_of = [&](int w) { return WRNN_XCDS_SQ_EARLY ? (w == 1 ? 0 : w == 3 ? 1 : w == 6 ? 2 : w == 2 ? 3 : -1) : w - 4; };
     auto gather_terms = [&](int t) {
         if (WRNN_XCDS_DIAG & 1) return;
-        const int qq = wave - 4;
+        const int qq = sq_of(wave);
         xgather16<kSPairs>(XG(XH_S0 + (t & 1)) + qq * R, (uint32_t)t + 1u, a.ctl, a.timeout_ticks, t,
                            XH_S0 + (t & 1), abort_flag, lane, [&](int i, float v0, float v1) {
                                *reinterpret_cast<f2v *>(sg + qq * R + i) = f2v{v0, v1};
@@ -369,7 +386,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
             publish_terms(0, br0, 0.0f);
             publish_terms(0, br1, 0.0f);
         }
-        if (wave >= 4) {
+        if (sq_of(wave) >= 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             gather_terms(0);
         }
@@ -492,6 +509,10 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
                 if (lane < 32)
                     __hip_atomic_store(f2p + (wave - 1) * 32 + lane, ((unsigned long long)tag << 32) | __float_as_uint(p),
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (WRNN_XCDS_SQ_EARLY && more) {   // a quarter of the next S (hop F1 polled: its window is over)
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    gather_terms(t + 1);
+                }
             } else {
                 // waves 1..3 store on every path (their polls are bounded); the abort word ends the
                 // wait too should that ever change
@@ -585,9 +606,10 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
             if ((lane & 15) == 0) xpub_b(xgr, XGI(XH_F1) + c * kXFcRows + rg, tag, A > 0.0f ? A : 0.0f);
             XSTAMPW(4, 4);
             if (more) {
-                // after f1 gathered: h2 (wave 4, then its flag), the four quarters of the next S, the
-                // ring (wave 7: step t+3's entries from the registers loaded a step ago, the load for
-                // t+4 lands during the next step); after h2 gathered: W_hh2·h2
+                // after f1 gathered: h2 (wave 4, then its flag), an S quarter (wave 6; all four with
+                // WRNN_XCDS_SQ_EARLY 0), the ring (wave 7: step t+3's entries from the registers
+                // loaded a step ago, the load for t+4 lands during the next step); after h2
+                // gathered: W_hh2·h2
                 wait_flag(f1got, tag);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (wave == 4) {
@@ -598,7 +620,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
                     set_flag(h2ready, tag);
                     XSTAMPW(10, 4);
                 }
-                gather_terms(t + 1);
+                if (sq_of(wave) >= 0) gather_terms(t + 1);
                 XSTAMPW(11, 5);
                 if (wave == 7) {
                     if (t + 3 <= t_terms && lane < kSTerms / 4) reinterpret_cast<f4v *>(RING(t + 3))[lane] = wg[0];
@@ -613,6 +635,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
                 if (!WRNN_XCDS_GRU2_STAMPS) XSTAMPW(13, 5);
             }
         }
+        XSTAMP_BAR();
         bar();
         // next step's x, GRU1 terms and the abort word: one LDS round trip
         const int ab = *abort_flag;

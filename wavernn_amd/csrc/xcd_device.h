@@ -15,6 +15,9 @@ namespace wrnn {
 #ifndef WRNN_XCD_UNIFORM_WAVE
 #define WRNN_XCD_UNIFORM_WAVE 1   // the XCD kernels' wave index through readfirstlane (0: per-lane, A/B)
 #endif
+#ifndef WRNN_XCD_BAR_STAMPS
+#define WRNN_XCD_BAR_STAMPS 0     // stamped diagnostic builds: each wave's arrival at the step-end barrier
+#endif
 #ifndef WRNN_XCD_LEAN_SAMPLER
 #define WRNN_XCD_LEAN_SAMPLER 1   // sampler: both logit sums through one permlane chain, med3 clamps, max + DPP as one instruction
 #endif
