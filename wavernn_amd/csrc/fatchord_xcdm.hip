@@ -813,12 +813,26 @@ __global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm
         // loads sit in waves that do not sample and store them before J)
         const int lt = kTwoLevel ? tid - 64 : kMThreads - 1 - tid;
         if (more && lt >= 0) {
+            // through a buffer descriptor on step t + 1's record (uniform) + a 32-bit offset, the
+            // segment offset by selects: the pointer form compiled to divergent branches and 64-bit
+            // address math, ≈ 50 instructions per load — it held the loader waves' fc2 epilogue
+            // (and with it the fc3 partials hop F2 waits for) ≈ 1 000 cycles behind wave 0's
+            const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<float *>(a.terms + (size_t)(t + 1 - a.t0) * a.nb * N), 0, 0x7fffffff, 0x00020000);
 #pragma unroll
             for (int i = 0; i < kRingLd; ++i) {
                 const int idx = lt + kLdThreads * i;
                 if (idx < RX * kRingF4) {
-                    const int n = idx / kRingF4, f = idx - n * kRingF4;
-                    rl[i] = *reinterpret_cast<const f4v *>(TERMS(t + 1, n) + mterm_off(c, 4 * f));
+                    const int n = idx / kRingF4, s4 = 4 * (idx - n * kRingF4);
+                    if constexpr (kRaw && NQ == 4) {   // (the RAW 4-quad head has no VGPRs to spare: as before)
+                        rl[i] = *reinterpret_cast<const f4v *>(TERMS(t + 1, n) + mterm_off(c, s4));
+                    } else {
+                        int off = kMG0 + c * 64 + s4;
+                        off = s4 >= MT_P2 ? kMG1 + c * 48 + (s4 - MT_P2) : off;
+                        off = s4 >= MT_V1 ? kMG2 + c * 32 + (s4 - MT_V1) : off;   // = mterm_off(c, s4)
+                        rl[i] = __builtin_bit_cast(
+                            f4v, __builtin_amdgcn_raw_buffer_load_b128(trs, ((k + kXcds * n) * N + off) * 4, 0, 0));
+                    }
                 }
             }
             if (!kRaw && lt < 11 * RX) {
