@@ -65,6 +65,13 @@ namespace wrnn {
 #ifndef WRNN_XCD_SQ3_WAVE
 #define WRNN_XCD_SQ3_WAVE 4
 #endif
+// y and h2 published per wave: lane 0 stores both engines' units (lanes 0 and 32 before, one in
+// each half of the wave) as one 16-byte pair — 1 row 3.36-3.37 → 3.31-3.33 µs/step,
+// profiles/r05_ab_xcd_pub16.log (the same pairing of the f1 rows / fc3 partials, already adjacent
+// lanes of one store: slower, not kept); 0: per engine (A/B)
+#ifndef WRNN_XCD_PUB16
+#define WRNN_XCD_PUB16 1
+#endif
 #ifndef WRNN_XCD_STAMP_W13
 #define WRNN_XCD_STAMP_W13 5    // stamped builds: the wave whose W_hh2·h2 end is stamp 13 (6: the h2 gatherer)
 #endif
@@ -336,7 +343,14 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
             h2own = hn;
             // y = (x_I + h1) + h2 (:212, :216)
             const float y = yb + hn;
-            if (li == 0) xpub_b(xgr, XGI(XH_Y) + c * kXUnits + ui, tag, y);   // h2: after hop Y (pub_h2)
+            if (WRNN_XCD_PUB16) {   // both engines' granules (units 2w, 2w + 1) in one 16-byte store
+                const float y1 = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(y), 32));
+                if (lane == 0)
+                    __builtin_amdgcn_raw_buffer_store_b128(u4v{__float_as_uint(y), tag, __float_as_uint(y1), tag}, xgr,
+                                                           (XGI(XH_Y) + c * kXUnits + 2 * wave) * 8, 0, 0);
+            } else if (li == 0) {
+                xpub_b(xgr, XGI(XH_Y) + c * kXUnits + ui, tag, y);   // h2: after hop Y (pub_h2)
+            }
         }
         XSTAMP(2);
         // Off-critical memory traffic (GRU1-term and h2 publishes, the S / h2 gathers, the ring)
@@ -347,7 +361,14 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcd_kernel(XcdArgs a) {
         //   after f1 gathered : gather h2 (wave 6), S (waves 1, 2, 5, 6), the ring (wave 7)
         //   after h2 gathered : W_hh2·h2 (waves 0, 1, 2, 5, 6, 7)
         auto pub_h2 = [&]() {
-            if (li == 0) xpub_b(xgr, XGI(XH_H2) + c * kXUnits + ui, tag, h2own);
+            if (WRNN_XCD_PUB16) {
+                const float h1o = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(h2own), 32));
+                if (lane == 0)
+                    __builtin_amdgcn_raw_buffer_store_b128(u4v{__float_as_uint(h2own), tag, __float_as_uint(h1o), tag},
+                                                           xgr, (XGI(XH_H2) + c * kXUnits + 2 * wave) * 8, 0, 0);
+            } else if (li == 0) {
+                xpub_b(xgr, XGI(XH_H2) + c * kXUnits + ui, tag, h2own);
+            }
         };
         // fc waves: lane l ends fc8_rows with row 8h + j + 2·(l >> 4) in o[j]; lanes with
         // (l & 15) < 2 publish row 8h + (l & 1) + 2·(l >> 4)
