@@ -228,6 +228,21 @@ int wrnn_melresnet(const wrnn_melresnet_cfg *cfg, const float *packed, const flo
 int wrnn_postprocess(const float *y, int rows, int steps, int batched, int overlap, int mu_law,
                      int n_classes, int wave_len, int fade_len, double *wave, void *stream);
 
+/* The sampler draws wrnn_generate takes when noise == NULL, materialised (round-6 addition, same
+ * ABI): out [steps][rows][K] (device fp32) = draw k of launch row j at step step0 + s, keyed
+ * (seed, row_offset + j, step0 + s, k) exactly as every loop kernel keys its in-kernel Philox, so
+ * passing `out` as `noise` reproduces the noise == NULL audio.  Philox-4x32-10 (Salmon et al.,
+ * SC'11), counter (k >> 2, step, row lo, row hi), key (seed lo, seed hi), word k & 3; the top 24
+ * bits m of the word map to
+ *   MOL (K = 11: u1[10], u2; utils/distribution.py:106,118): fma(1 − 2e-5, m·2^-24, 1e-5) in fp32,
+ *       i.e. U(1e-5, 1 − 1e-5);
+ *   RAW (K = n_classes) and DM (K = 2Q: q_coarse then q_fine): −log((m + 1)·2^-24), i.e. Exp(1)
+ *       (Categorical.sample ≡ argmax(probs / q), fatchord_version.py:232-235,
+ *       deepmind_version.py:130,150).
+ * Restated in numpy by oracle/philox.py (tests/test_philox.py, tests/test_gpu_philox.py). */
+int wrnn_philox_draws(uint64_t seed, int64_t row_offset, int rows, int step0, int steps, int K, int mode, float *out,
+                      void *stream);
+
 /* Message of the last failed stateless call on this thread. */
 const char *wrnn_cond_last_error(void);
 

@@ -19,6 +19,10 @@ GEN_CASES = ["gen_mol_unbatched", "gen_raw_batched_mulaw", "gen_mol_batched", "g
 # generate() at BASELINE sizes (configs 1, 2 unbatched and fold-batched, 3), written by the
 # reference itself; outputs stored strided / by row (make_golden.gen_case)
 GEN_BASELINE_CASES = ["gen_raw_1s_unbatched", "gen_mol_5s_unbatched", "gen_mol_5s_batched", "gen_mol_60s_batched"]
+# config 4's production route (rnn 896, 95 % 4x4 block-sparse GRU): one 5 s utterance through
+# generate(), and 8 utterances vocoded one by one (the 8-row generate_many launch)
+GEN_SPARSE_CASES = ["gen_sparse896_5s_unbatched"]
+GEN_MANY_CASES = ["gen_sparse896_8utt"]
 
 # MoL parity tolerance per sample under noise injection: ~50-100x the
 # 5e-8..1.8e-7 the C restatement shows against the reference.
@@ -57,15 +61,37 @@ def loop_inputs(fx: dict):
     return d, state, mels, aux, noise
 
 
+def _state_of(fx: dict, d):
+    state = syn.make_fatchord_state(d, int(fx["wseed"]))
+    if float(fx.get("prune", 0.0)) > 0:
+        from wavernn_amd.pruning import prune_state
+        state = prune_state(state, float(fx["prune"]))
+    return state
+
+
 def gen_inputs(fx: dict):
     d = dims_of(fx)
-    state = syn.make_fatchord_state(d, int(fx["wseed"]))
+    state = _state_of(fx, d)
     mel = syn.make_mel(d.feat_dims, int(fx["T"]), int(fx["mseed"]))
     noise = syn.make_noise(d.mode, int(fx["B"]), int(fx["Lf"]), d.n_classes, int(fx["nseed"]))
     assert syn.state_digest(state) == str(fx["state_sha"])
     assert syn.digest(mel) == str(fx["mel_sha"])
     assert syn.digest(noise) == str(fx["noise_sha"])
     return d, state, mel, noise
+
+
+def gen_many_inputs(fx: dict):
+    """(dims, state, mels [n_utt] of (feat, T), noise [Lf][n_utt][K]) of a `gen_many` fixture:
+    utterance i was vocoded alone by the reference with draws noise[:, i]."""
+    d = dims_of(fx)
+    state = _state_of(fx, d)
+    n, T = int(fx["n_utt"]), int(fx["T"])
+    mels = [syn.make_mel(d.feat_dims, T, int(fx["mseed0"]) + i) for i in range(n)]
+    noise = syn.make_noise(d.mode, n, int(fx["Lf"]), d.n_classes, int(fx["nseed"]))
+    assert syn.state_digest(state) == str(fx["state_sha"])
+    assert syn.digest(*mels) == str(fx["mel_sha"])
+    assert syn.digest(noise) == str(fx["noise_sha"])
+    return d, state, mels, noise
 
 
 def dm_inputs(fx: dict):

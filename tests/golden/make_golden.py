@@ -232,15 +232,19 @@ def dm_case(fv, name, d: syn.DeepmindDims, L: int, wseed=0, nseed=3):
 # ------------------------------------------------------------------------------ e2e cases
 def gen_case(fv, name, d: syn.FatchordDims, T: int, batched: bool, target: int, overlap: int,
              mu_law: bool, wseed=0, mseed=1, nseed=3, cond_stride=25, out_stride=1,
-             raw_rows=None, raw_stride=0):
+             raw_rows=None, raw_stride=0, prune=0.0):
     """Full reference generate(): pad → upsample → fold → loop → unfold/mu-law/fade.
 
     BASELINE-size cases keep the fixture small: `out_stride` stores every k-th output sample
     (float64), `raw_rows` keeps the per-step loop outputs of those fold rows only, and
     `raw_stride` > 0 additionally keeps every row at every raw_stride-th step.  Under MoL
     feedback a divergence at one step changes every later sample of its row, so a strided
-    view still catches it."""
+    view still catches it.  prune > 0: the GRU weights block-pruned to that sparsity first
+    (config 4's model, wavernn_amd/pruning.py); the reference runs the pre-masked dense weights."""
     state = syn.make_fatchord_state(d, wseed)
+    if prune > 0:
+        from wavernn_amd.pruning import prune_state
+        state = prune_state(state, prune)
     mel = syn.make_mel(d.feat_dims, T, mseed)
     L = d.hop_length * T
     B = fold_count(L, target, overlap) if batched else 1
@@ -265,7 +269,7 @@ def gen_case(fv, name, d: syn.FatchordDims, T: int, batched: bool, target: int, 
     up_a = captured["aux"][0].numpy()
     assert up_m.shape == (L, d.feat_dims)
     rec = dict(kind="gen", mode=d.mode, T=T, batched=batched, target=target, overlap=overlap,
-               mu_law=mu_law, B=B, Lf=Lf, wseed=wseed, mseed=mseed, nseed=nseed,
+               mu_law=mu_law, B=B, Lf=Lf, wseed=wseed, mseed=mseed, nseed=nseed, prune=prune,
                dims=np.array(repr(d)), ref_seconds=dt, state_sha=syn.state_digest(state),
                mel_sha=syn.digest(mel), noise_sha=syn.digest(noise),
                out_len=np.int64(len(out)), out_stride=np.int64(out_stride),
@@ -286,6 +290,40 @@ def gen_case(fv, name, d: syn.FatchordDims, T: int, batched: bool, target: int, 
             rec["raw_stride"] = np.int64(raw_stride)
             rec["raw_strided"] = raw[:, ::raw_stride].copy()
     return rec
+
+
+def gen_many_case(fv, name, d: syn.FatchordDims, T: int, n_utt: int, mseed0: int, target=11000,
+                  overlap=550, mu_law=True, wseed=0, nseed=3, prune=0.0, out_stride=1):
+    """A list of utterances vocoded ONE BY ONE by the reference generate(), as gen_wavernn.py:11-35
+    does (unbatched, the mode config 4 times).  Utterance i: mel seed mseed0 + i, draws
+    noise[:, i] of one [Lf][n_utt][K] array — the row order of a generate_many() launch over the
+    same list.  Stores every utterance's float64 output (strided) and per-step loop outputs."""
+    state = syn.make_fatchord_state(d, wseed)
+    if prune > 0:
+        from wavernn_amd.pruning import prune_state
+        state = prune_state(state, prune)
+    mels = [syn.make_mel(d.feat_dims, T, mseed0 + i) for i in range(n_utt)]
+    L = d.hop_length * T
+    noise = syn.make_noise(d.mode, n_utt, L, d.n_classes, nseed)
+    model = build_ref_model(fv, d, state)
+    outs, raws, dt = [], [], 0.0
+    for i, mel in enumerate(mels):
+        t0 = time.time()
+        with NoiseInjector(fv, d.mode, noise[:, i:i + 1].copy()) as inj:
+            out = model.generate(torch.from_numpy(mel)[None], "/dev/null", False, target, overlap, mu_law)
+        dt += time.time() - t0
+        assert inj.t == L, (inj.t, L)
+        outs.append(np.asarray(out, dtype=np.float64))
+        raws.append(np.stack(inj.samples).reshape(L))
+    out = np.stack(outs)
+    raw = np.stack(raws)
+    raw = raw.astype(np.int16) if d.mode == "RAW" else raw.astype(np.float32)
+    return dict(kind="gen_many", mode=d.mode, T=T, n_utt=n_utt, mseed0=mseed0, target=target,
+                overlap=overlap, mu_law=mu_law, Lf=L, wseed=wseed, nseed=nseed, prune=prune,
+                dims=np.array(repr(d)), ref_seconds=dt, state_sha=syn.state_digest(state),
+                mel_sha=syn.digest(*mels), noise_sha=syn.digest(noise),
+                out_len=np.int64(out.shape[1]), out_stride=np.int64(out_stride),
+                output=out[:, ::out_stride].copy(), out_sum=out.sum(1), raw=raw)
 
 
 # ---------------------------------------------------------------------- training forward
@@ -357,6 +395,14 @@ def cases():
         "gen_mol_60s_batched": ("gen", dict(d=M, T=4811, batched=True, target=11000, overlap=550,
                                             mu_law=True, cond_stride=2750, out_stride=32,
                                             raw_rows=(0, 57, 114), raw_stride=50)),
+        # config 4's production route (VERDICT r05 "do this" 1): the 95 %-pruned rnn-896 model
+        # through the whole generate() — one 5 s utterance, and 8 shorter ones one by one
+        # (gen_wavernn.py:11-35) for the 8-row generate_many launch bench.py times
+        "gen_sparse896_5s_unbatched": ("gen", dict(d=syn.SPARSE896_MOL, T=401, batched=False, target=11000,
+                                                   overlap=550, mu_law=True, cond_stride=275, out_stride=4,
+                                                   prune=0.95)),
+        "gen_sparse896_8utt": ("gen_many", dict(d=syn.SPARSE896_MOL, T=41, n_utt=8, mseed0=60, prune=0.95,
+                                                out_stride=2)),
         # the training-side teacher-forced forward + backward (§8(f)4)
         "train_mol": ("train", dict(d=M, out_stride=2)),
         "train_raw": ("train", dict(d=R, out_stride=16)),
@@ -374,7 +420,8 @@ def main(argv):
     names = argv or list(todo)
     for name in names:
         kind, kw = todo[name]
-        fn = {"loop": loop_case, "gen": gen_case, "dm": dm_case, "train": train_case}[kind]
+        fn = {"loop": loop_case, "gen": gen_case, "gen_many": gen_many_case, "dm": dm_case,
+              "train": train_case}[kind]
         rec = fn(fv, name, **kw)
         path = os.path.join(HERE, name + ".npz")
         np.savez_compressed(path, **{k: np.asarray(v) for k, v in rec.items()})

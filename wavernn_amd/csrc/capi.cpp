@@ -63,6 +63,7 @@ hipError_t launch_philox_fill(float *out, unsigned long long seed, long long row
                               hipStream_t st);
 hipError_t launch_dx(const DxArgs &a, hipStream_t st);
 hipError_t prepare_dx_kernel(int max_lds_bytes, bool *ok);
+int cond_fail(int code, const std::string &m);
 }  // namespace wrnn
 
 using namespace wrnn;
@@ -2609,6 +2610,20 @@ int wrnn_query(const wrnn_t *h, wrnn_info *info) {
 }
 
 const char *wrnn_last_error(const wrnn_t *h) { return h ? h->err.c_str() : "null handle"; }
+
+int wrnn_philox_draws(uint64_t seed, int64_t row_offset, int rows, int step0, int steps, int K, int mode, float *out,
+                      void *stream) {
+    if (!out || rows < 1 || steps < 1 || K < 1 || step0 < 0)
+        return cond_fail(WRNN_EINVAL, "need out, rows >= 1, steps >= 1, K >= 1, step0 >= 0");
+    if (mode != WRNN_MODE_RAW && mode != WRNN_MODE_MOL && mode != WRNN_MODE_DM)
+        return cond_fail(WRNN_EINVAL, "unknown mode");
+    if ((long long)steps * rows * K > (1LL << 31) - 256) return cond_fail(WRNN_EINVAL, "too many draws for one call");
+    if ((long long)step0 + steps > (1LL << 32)) return cond_fail(WRNN_EINVAL, "step index past 2^32");
+    if (launch_philox_fill(out, seed, row_offset, rows, step0, steps, K, mode == WRNN_MODE_MOL ? 1 : 0,
+                           (hipStream_t)stream) != hipSuccess)
+        return cond_fail(WRNN_EHIP, "philox fill launch failed");
+    return WRNN_OK;
+}
 
 void wrnn_destroy(wrnn_t *h) {
     if (!h) return;

@@ -216,12 +216,14 @@ __global__ void postprocess_kernel(PostArgs a) {
     a.wave[t] = v;
 }
 
-namespace {
+// error of the last failed stateless call on this thread (also capi.cpp's wrnn_philox_draws)
 thread_local std::string g_cond_err;
 int cond_fail(int code, const std::string &m) {
     g_cond_err = m;
     return code;
 }
+
+namespace {
 
 // fold geometry of fold_with_overlap (:317-330): folds, stride, window, padded length
 void fold_geometry(int L, int target, int overlap, int *nf, int *stride, int *win, int *Lp) {

@@ -82,6 +82,24 @@ def noise_width(mode: str, n_classes: int) -> int:
     return 11 if mode == "MOL" else n_classes
 
 
+def philox_draws(seed: int, row_offset: int, rows: int, steps: int, K: int, mode: str, step0: int = 0,
+                 device: int = 0, stream=None) -> torch.Tensor:
+    """The draws a loop launch takes with noise=None (C-ABI wrnn_philox_draws): [steps][rows][K]
+    fp32 on cuda:`device`, row j keyed row_offset + j, step s keyed step0 + s — usable as the
+    `noise` of the same launch (bit-identical audio).  mode "MOL": U(1e-5, 1 − 1e-5) (K = 11);
+    "RAW" / "DM": Exp(1)."""
+    m = {"RAW": nat.MODE_RAW, "MOL": nat.MODE_MOL, "DM": nat.MODE_DM}[mode]
+    dev = torch.device("cuda", device)
+    out = torch.empty(steps, rows, K, dtype=torch.float32, device=dev)
+    if stream is None:
+        stream = torch.cuda.current_stream(dev).cuda_stream
+    rc = nat.lib().wrnn_philox_draws(ctypes.c_uint64(seed & (2 ** 64 - 1)), row_offset, rows, step0, steps, K, m,
+                                     out.data_ptr(), stream)
+    if rc != 0:
+        raise nat.WrnnError(rc, nat.lib().wrnn_cond_last_error().decode())
+    return out
+
+
 class FatchordLoop:
     keys = LOOP_KEYS
 
@@ -179,7 +197,7 @@ class FatchordLoop:
         return out, labels
 
     def generate_frames(self, spec, mel: torch.Tensor, aux: torch.Tensor, target: int = 0, overlap: int = 0,
-                        noise: Optional[torch.Tensor] = None, seed: int = 0, row_offset: int = 0,
+                        noise: Optional[torch.Tensor] = None, seed: int = 0, row_offset: Optional[int] = None,
                         want_labels: bool = False, stream=None, check: bool = True,
                         rows: Optional[Tuple[int, int]] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
         """The loop from the generate() inputs at frame rate (C-ABI wrnn_generate_frames):
@@ -187,7 +205,9 @@ class FatchordLoop:
         `spec` the UpsampleNetwork's condition.UpsampleSpec → samples [rows][steps] (+ labels),
         rows / steps as condition.upsample_pack would lay them out (target <= 0: unbatched).
         `rows=(begin, count)`: only those rows of the launch (wrnn_generate_frames_rows; e.g. a
-        block of one utterance's folds), keyed row_offset + j."""
+        block of one utterance's folds), keyed row_offset + j.  row_offset=None keys launch row
+        j as its place in the whole launch (begin + j), so a block reproduces the same rows of
+        the whole launch; pass the global row id of `begin` when the launch is itself a shard."""
         for name, t in (("mel", mel), ("aux", aux)):
             if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.dim() == 3):
                 raise ValueError(f"{name} must be a contiguous fp32 CUDA tensor [U][C][T]")
@@ -205,6 +225,8 @@ class FatchordLoop:
         r0, rows = (0, n_rows) if rows is None else (int(rows[0]), int(rows[1]))
         if r0 < 0 or rows < 1 or r0 + rows > n_rows:
             raise ValueError(f"rows [{r0}, {r0 + rows}) outside the launch's {n_rows}")
+        if row_offset is None:
+            row_offset = r0
         if noise is not None:
             if not (noise.is_cuda and noise.dtype == torch.float32 and noise.is_contiguous()):
                 raise ValueError("noise must be a contiguous fp32 CUDA tensor [L][B][K]")

@@ -84,9 +84,12 @@ def gather_audio(local: Dict[int, np.ndarray], n_items: int, device: torch.devic
 
 def generate_sharded(model, mels: Sequence, batched: bool, target: int, overlap: int, mu_law: bool,
                      base_seed: int = 0, device: Optional[torch.device] = None, group=None,
-                     generate_fn: Optional[Callable] = None) -> Optional[List[np.ndarray]]:
+                     generate_fn: Optional[Callable] = None, noise=None) -> Optional[List[np.ndarray]]:
     """Generate every mel in `mels` across the process group; rank 0 returns the list of
     float64 waveforms in input order, other ranks return None.
+
+    `noise` (optional, parity testing): the injected draws of the WHOLE list, [L_max][rows][K]
+    in global row order (generate_many's layout on one GPU); each rank passes its rows' slice.
 
     A rank runs its block through ONE `generate_many` launch, seeded `base_seed` with its first
     loop row at the global row id of its first utterance (every rank knows every mel's row
@@ -99,8 +102,13 @@ def generate_sharded(model, mels: Sequence, batched: bool, target: int, overlap:
     idx = shard_indices(len(mels), rank, world)
     rows = [model.rows_of(np.shape(m)[-1], batched, target, overlap) for m in mels]
     row0 = int(sum(rows[:idx[0]])) if idx else 0
+    nz = None
+    if noise is not None and idx:
+        n_rows = int(sum(rows[i] for i in idx))
+        steps = max((target + 2 * overlap) if batched else np.shape(mels[i])[-1] * model.hop_length for i in idx)
+        nz = np.asarray(noise)[:steps, row0:row0 + n_rows]
     gen = generate_fn or (lambda ii, ms, r0: model.generate_many(ms, None, batched, target, overlap, mu_law,
-                                                                  seed=base_seed, row_offset=r0))
+                                                                  seed=base_seed, row_offset=r0, noise=nz))
     outs = gen(idx, [mels[i] for i in idx], row0) if idx else []
     return gather_audio(dict(zip(idx, outs)), len(mels), device, group)
 
