@@ -43,7 +43,9 @@ from wavernn_amd import synthetic as syn  # noqa: E402
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak (dense)
 MOL_MACS_PER_ROW_STEP = 3825152   # loop MACs per row-step, MoL rnn 512
-PMC_PROFILE = os.environ.get("WRNN_PMC_PROFILE", os.path.join(REPO, "profiles", "r03_v7_pmc_traffic.json"))
+# an explicitly named committed PMC summary replaces the live passes (labelled in traffic_from); by
+# default there is no fallback: when the live passes fail, roofline.traffic is null
+PMC_PROFILE = os.environ.get("WRNN_PMC_PROFILE")
 SPARSE896_BYTES_PER_STEP = 5536598   # config 4 sparse values + int16 block indices, fp32
 DM_BYTES_PER_STEP = 12200196         # config 5 deepmind weights, fp32
 DM_MACS_PER_ROW_STEP = 3045952
@@ -134,11 +136,23 @@ def pmc_live(timeout_s: float = 240.0):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
-def committed_pmc():
-    if not os.path.exists(PMC_PROFILE):
+def committed_pmc(path):
+    if not path or not os.path.exists(path):
         return None
-    with open(PMC_PROFILE) as f:
+    with open(path) as f:
         return json.load(f)
+
+
+def resolve_traffic(live, profile_path):
+    """(traffic record, traffic_from) for the roofline: this run's live PMC passes; else the
+    summary named by WRNN_PMC_PROFILE (labelled as such); else (None, reason) — never an older
+    kernel's traffic presented as this one's."""
+    if live is not None:
+        return live, "live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this run"
+    prof = committed_pmc(profile_path)
+    if prof is not None:
+        return prof, os.path.relpath(profile_path, REPO) + " (named by WRNN_PMC_PROFILE; live passes unavailable)"
+    return None, "unavailable: the live rocprofv3 passes did not run or failed (traffic null)"
 
 
 # ------------------------------------------------------------------------ other configs
@@ -410,6 +424,20 @@ def sharded_configs(dev, world: int, rank: int, warm: bool = True, cpu_steps: in
     return res
 
 
+def attach_traffic(rec: dict, traffic, traffic_from) -> None:
+    """Per-config HBM bytes per loop step (PMC) beside each secondary line's roofline: the
+    fold-batched line and every other_configs entry; null with the reason when unavailable."""
+    lines = dict(rec.get("other_configs", {}))
+    if "fold_batched" in rec:
+        lines["fold_batched"] = rec["fold_batched"]
+    for key, v in lines.items():
+        if "roofline" not in v:
+            continue
+        tr = (traffic or {}).get("other_configs", {}).get(key)
+        v["roofline"]["traffic_per_step"] = tr["bytes_per_step"] if tr is not None else None
+        v["roofline"]["traffic_from"] = traffic_from
+
+
 # ------------------------------------------------------------------------------- main
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
@@ -497,15 +525,11 @@ def main():
         args.steps, args.warmup, args.cpu_steps, args.fold_batched, args.pmc = 1, 0, 0, 0, 0
     # HBM traffic passes first, while this process has not touched the GPU (child processes)
     traffic, traffic_from = None, None
-    if args.pmc and rank == 0 and not args.batched and args.mode == "MOL" and abs(args.seconds - 5.0) < 1e-9:
+    headline_shape = not args.batched and args.mode == "MOL" and abs(args.seconds - 5.0) < 1e-9
+    if rank == 0 and headline_shape and not args.pmc_child:
         # rank 0 only (its GPU = the children's cuda:0); the other ranks wait in the rendezvous
-        live = pmc_live()
-        if live is not None:
-            traffic, traffic_from = live, "live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this run"
-    if traffic is None and not args.batched and args.mode == "MOL" and abs(args.seconds - 5.0) < 1e-9:
-        traffic = committed_pmc()
-        traffic_from = os.path.relpath(PMC_PROFILE, REPO) + " (committed profile; live passes unavailable)" \
-            if traffic else None
+        live = pmc_live() if args.pmc else None
+        traffic, traffic_from = resolve_traffic(live, PMC_PROFILE)
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -542,6 +566,9 @@ def main():
     loop_ms_max = float(lm[0])
 
     if args.pmc_child:
+        # the same order tools/pmc_summary.py attributes dispatches in: headline, fold-batched,
+        # then the other configs
+        model.generate(mel, None, True, target, overlap, True, seed=7, verbose=False)
         other_configs(dev, warm=False)
         sharded_configs(dev, 1, 0, warm=False)
         return
@@ -594,9 +621,9 @@ def main():
                 "note": "achieved = algorithmic bytes (all loop weights fp32 per step + 836 B/row-step) per launch "
                         "/ launch time (HIP events); the weights are LDS/VGPR-resident on one XCD's 32 CUs "
                         "(fatchord_xcd_kernel), the kernel is hand-off-latency bound. traffic = 2 x FETCH_SIZE + "
-                        "WRITE_SIZE bytes of the headline launch (gfx950 read correction; traffic_from says whether "
-                        "the passes ran in this bench or came from the committed profile): conditioning-terms "
-                        "reads; the hand-offs stay in the XCD's L2",
+                        "WRITE_SIZE bytes of the headline launch (gfx950 read correction; traffic_from says where "
+                        "it came from, null when the live passes failed): conditioning-terms reads; the "
+                        "hand-offs stay in the XCD's L2",
             },
         }
         if args.fold_batched and not args.batched and args.mode == "MOL":
@@ -606,12 +633,16 @@ def main():
             outb, dtb = _timed(lambda: model.generate(mel, None, True, target, overlap, True, seed=8, verbose=False))
             kb = model.loop_handle().elapsed_ms()
             condb, _ = model.conditioning(mel, True, target, overlap)
+            usb = kb * 1e3 / condb.shape[0]
             rec["fold_batched"] = {
                 "samples_per_s": outb.shape[0] / dtb, "rtf": outb.shape[0] / dtb / d.sample_rate,
                 "rows": int(condb.shape[1]), "loop_steps": int(condb.shape[0]), "device_ms": kb,
-                "us_per_loop_step": kb * 1e3 / condb.shape[0],
+                "us_per_loop_step": usb,
                 "kernel_path": model.loop_handle().info["last_path"],
                 "kernel": KERNELS.get(model.loop_handle().info["last_path"]),
+                "roofline": hbm_roofline(wbytes + int(condb.shape[1]) * COND_BYTES_PER_ROW_STEP, usb,
+                                         "algorithmic bytes per step (all loop weights once + 836 B per row) / step "
+                                         "time of the launch; weights resident as MFMA operands, latency-bound"),
                 "note": "same 5 s utterance, generate(batched=True) as gen_wavernn.py runs it with the 800k "
                         "hparams (10 folds in one launch) + conditioning-terms GEMM; rate over the whole "
                         "generate() wall time (upsample, loop, float64 post)",
@@ -620,11 +651,7 @@ def main():
             # single-GPU configs (1, 2 x 8 streams, 3) on rank 0's GPU, then the sharded legs' records
             rec["other_configs"] = other_configs(dev, cpu_steps=min(args.cpu_steps, 2000), threads=threads)
             rec["other_configs"].update(sharded)
-            for key, v in rec["other_configs"].items():
-                tr = (traffic or {}).get("other_configs", {}).get(key)
-                if tr is not None and "roofline" in v:
-                    v["roofline"]["traffic_per_step"] = tr["bytes_per_step"]   # HBM bytes per loop step (PMC)
-                    v["roofline"]["traffic_from"] = traffic_from
+        attach_traffic(rec, traffic, traffic_from)
         if args.cpu_steps > 0:
             # the reference's op sequence on this host's cores: PyTorch-CPU eager (oracle/torch_cpu.py),
             # whole pre/post + a bounded slice of the loop; and the C oracle on the same slice

@@ -218,6 +218,11 @@ typedef struct {
 int wrnn_melresnet_floats(const wrnn_melresnet_cfg *cfg);
 int wrnn_melresnet(const wrnn_melresnet_cfg *cfg, const float *packed, const float *mel, int U, int T, float *aux,
                    void *stream);
+/* The frames per workgroup tile wrnn_melresnet takes for U utterances of T frames on the current
+ * device (round-6 addition, same ABI): 16, or 4 when a 16-frame grid has fewer workgroups than the
+ * device has CUs (both forms sum every output in the same order: bit-identical); negative WRNN_E*
+ * as wrnn_melresnet would return. */
+int wrnn_melresnet_tile_frames(const wrnn_melresnet_cfg *cfg, int U, int T);
 
 /* generate()'s float64 post-processing on the device (fatchord_version.py:243-258):
  * decode_mu_law (utils/dsp.py:98-103, mu = n_classes) when `mu_law`, xfade_and_unfold

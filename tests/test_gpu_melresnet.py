@@ -20,8 +20,11 @@ def _model(d, seed):
     return m.eval()
 
 
-@pytest.mark.parametrize("d,U,T", [(syn.DEFAULT_MOL, 1, 405), (syn.DEFAULT_MOL, 3, 37), (syn.TINY_MOL, 2, 50)])
-def test_kernel_matches_the_module(d, U, T):
+@pytest.mark.parametrize("d,U,T,F", [(syn.DEFAULT_MOL, 1, 405, 4), (syn.DEFAULT_MOL, 3, 37, 4),
+                                     (syn.TINY_MOL, 2, 50, 4), (syn.DEFAULT_MOL, 1, 4815, 16)])
+def test_kernel_matches_the_module(d, U, T, F):
+    """F: the tile form the kernel takes for this grid on a 256-CU MI355X (4-frame tiles when the
+    16-frame grid has fewer workgroups than CUs)."""
     m = _model(d, 4)
     res = m.upsample.resnet
     g = torch.Generator().manual_seed(9)
@@ -32,7 +35,12 @@ def test_kernel_matches_the_module(d, U, T):
     x = torch.rand(U, d.feat_dims, T + 2 * d.pad, generator=g).to(DEV)
     with torch.no_grad():
         want = res(x)
-    got = condition.melresnet(condition.melresnet_cfg(res), condition.melresnet_pack(res), x)
+    import ctypes
+    from wavernn_amd import _native as nat
+    cfg = condition.melresnet_cfg(res)
+    assert torch.cuda.get_device_properties(DEV).multi_processor_count == 256
+    assert nat.lib().wrnn_melresnet_tile_frames(ctypes.byref(cfg), U, T) == F
+    got = condition.melresnet(cfg, condition.melresnet_pack(res), x)
     err = float((got - want).abs().max())
     print(f"max |Δ| {err:.3g} of {float(want.abs().max()):.3g}")
     assert got.shape == want.shape and err <= 1e-5 * float(want.abs().max())

@@ -27,16 +27,15 @@ BIG_SEED = (0xDEADBEEF << 32) | 0x12345678
 
 
 def _exp_close(got: np.ndarray, ref: np.ndarray, what: str):
-    """Device -logf(u) vs float64 -log(u) rounded to fp32: within 2 ulp of the reference value,
-    or 2^-24 absolute where the draw is tiny (u near 1: the log's absolute accuracy)."""
+    """Device -log(u) (float64 log, one rounding) vs numpy's: bit-equal but for the rare draw
+    whose float64 logs differ in their last bit across a float32 rounding boundary (~2^-29 per
+    draw): at most one fp32 ulp, on at most 1e-5 of the draws, with no bias."""
     ulp = np.spacing(np.abs(ref).astype(np.float32)).astype(np.float64)
     d = np.abs(got.astype(np.float64) - ref.astype(np.float64))
-    bad = d > np.maximum(2 * ulp, 2.0 ** -24)
     exact = float((got == ref).mean())
-    print(f"{what}: {exact:.4f} of {got.size} draws bit-equal, max {np.max(d / ulp):.2f} ulp")
-    assert not bad.any(), f"{what}: {int(bad.sum())} draws off, first {tuple(np.argwhere(bad)[0])}"
-    # no bias: the mean of the differences is far below a draw's ulp
-    assert abs(float((got.astype(np.float64) - ref).mean())) < 1e-8
+    print(f"{what}: {exact:.6f} of {got.size} draws bit-equal, max {np.max(d / ulp):.2f} ulp")
+    assert (d <= ulp).all(), f"{what}: first draw over 1 ulp at {tuple(np.argwhere(d > ulp)[0])}"
+    assert exact >= 1 - 1e-5, what
 
 
 @pytest.mark.parametrize("mode,K", [("MOL", 11), ("RAW", 512), ("DM", 512), ("RAW", 7)])

@@ -30,6 +30,7 @@ def test_summary_picks_the_headline_dispatch_and_sums_the_configs(tmp_path):
         _write(str(tmp_path / f"pmc_{counter}" / "pmc_counter_collection.csv"), [
             ("Cijk_gemm", 5.0 * scale, 10),
             (xcd, 100.0 * scale, 400),                                       # the headline (first)
+            ("void wrnn::fatchord_xcdm_kernel<1, false, false>(wrnn::XcdmArgs)", 3.0 * scale, 60),   # fold-batched
             (xcd, 900.0 * scale, 500),                                       # 8 utterances: longer, later
             ("void wrnn::fatchord_xcdm_kernel<1, false, true>(wrnn::XcdmArgs)", 7.0 * scale, 100),   # RAW
             ("void wrnn::fatchord_xcdm_kernel<4, false, false>(wrnn::XcdmArgs)", 40.0 * scale, 50),
@@ -45,6 +46,32 @@ def test_summary_picks_the_headline_dispatch_and_sums_the_configs(tmp_path):
     assert cfg["config2_8_streams"]["bytes_per_step"] == 1024.0 * (2 * 900.0 + 450.0) / 110275
     assert cfg["config3_mol_fold_60s"]["bytes_per_step"] == 1024.0 * (2 * 100.0 + 50.0) / 12100
     assert cfg["config2_32_streams"]["bytes_per_step"] == 1024.0 * (2 * 20.0 + 10.0) / 110275
+    assert cfg["fold_batched"]["bytes_per_step"] == 1024.0 * (2 * 3.0 + 1.5) / 12100
     assert cfg["config3_mol_fold_60s"]["kernel"] == "fatchord_xcdm_kernel"
     assert cfg["config4_sparse896_8utt"]["fetch_kib"] == 11.0
     assert cfg["config5_deepmind_32utt"]["write_kib"] == 6.5
+
+
+def test_bench_traffic_never_falls_back_to_an_unnamed_profile(tmp_path, monkeypatch):
+    """when the live passes fail, the headline's traffic is null with the reason
+    (no older kernel's profile presented as this one's); a profile named by WRNN_PMC_PROFILE is used
+    and labelled; the fold-batched line carries its own traffic_per_step."""
+    sys.path.insert(0, REPO)
+    import json
+    import bench
+    tr, src = bench.resolve_traffic(None, None)
+    assert tr is None and src.startswith("unavailable")
+    tr, src = bench.resolve_traffic(None, str(tmp_path / "missing.json"))
+    assert tr is None and src.startswith("unavailable")
+    prof = tmp_path / "named.json"
+    prof.write_text(json.dumps({"bytes": 123.0, "other_configs": {"fold_batched": {"bytes_per_step": 9.0}}}))
+    tr, src = bench.resolve_traffic(None, str(prof))
+    assert tr["bytes"] == 123.0 and "WRNN_PMC_PROFILE" in src
+    live = {"bytes": 1.0, "other_configs": {}}
+    assert bench.resolve_traffic(live, str(prof)) == (live, "live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this run")
+    rec = {"fold_batched": {"roofline": {}}, "other_configs": {"config3_mol_fold_60s": {"roofline": {}}, "x": {}}}
+    bench.attach_traffic(rec, tr, src)
+    assert rec["fold_batched"]["roofline"]["traffic_per_step"] == 9.0
+    assert rec["other_configs"]["config3_mol_fold_60s"]["roofline"]["traffic_per_step"] is None
+    assert rec["other_configs"]["config3_mol_fold_60s"]["roofline"]["traffic_from"] == src
+    assert bench.PMC_PROFILE == os.environ.get("WRNN_PMC_PROFILE")

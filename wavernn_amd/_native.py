@@ -19,7 +19,8 @@ STATUS = {0: "WRNN_OK", -1: "WRNN_EINVAL", -2: "WRNN_EHIP", -3: "WRNN_ENOWEIGHTS
 EXPORTS = ("wrnn_create", "wrnn_set_weights", "wrnn_generate", "wrnn_check", "wrnn_elapsed_ms",
            "wrnn_query", "wrnn_last_error", "wrnn_destroy", "wrnn_cond_shape", "wrnn_upsample_pack",
            "wrnn_postprocess", "wrnn_cond_last_error", "wrnn_generate_frames", "wrnn_generate_frames_rows",
-           "wrnn_frame_weights", "wrnn_melresnet_floats", "wrnn_melresnet", "wrnn_philox_draws")
+           "wrnn_frame_weights", "wrnn_melresnet_floats", "wrnn_melresnet", "wrnn_philox_draws",
+           "wrnn_melresnet_tile_frames")
 
 
 class MelResNetCfg(ctypes.Structure):
@@ -103,6 +104,8 @@ def lib() -> ctypes.CDLL:
     L.wrnn_melresnet_floats.restype = i32
     L.wrnn_melresnet.argtypes = [ctypes.POINTER(MelResNetCfg), vp, vp, i32, i32, vp, vp]
     L.wrnn_melresnet.restype = i32
+    L.wrnn_melresnet_tile_frames.argtypes = [ctypes.POINTER(MelResNetCfg), i32, i32]
+    L.wrnn_melresnet_tile_frames.restype = i32
     L.wrnn_philox_draws.argtypes = [u64, i64, i32, i32, i32, i32, i32, vp, vp]
     L.wrnn_philox_draws.restype = i32
     L.wrnn_cond_last_error.argtypes = []

@@ -14,10 +14,9 @@
 
 namespace wrnn {
 
-#ifndef WRNN_XCDM_WAVES
-#define WRNN_XCDM_WAVES 4
-#endif
-constexpr int kMWaves = WRNN_XCDM_WAVES;   // waves per workgroup (one per SIMD)
+// Four waves per workgroup, one per SIMD: the partial-sum epilogues (one float4 of wave partials
+// per output, fatchord_xcdm.hip) and the K windows are written for exactly that.
+constexpr int kMWaves = 4;                 // waves per workgroup (one per SIMD)
 constexpr int kMThreads = 64 * kMWaves;
 constexpr int kMQuadMax = 4;               // batch quads (4 rows) per XCD
 constexpr int kMRowsXcd = 4 * kMQuadMax;   // rows per XCD

@@ -62,12 +62,11 @@ __device__ __forceinline__ f4v kslice_sum(f4v d) {
     return f4v{cross_rows(d.x), cross_rows(d.y), cross_rows(d.z), cross_rows(d.w)};
 }
 
-// Σ of the waves' partials of one output, fixed order
+// Σ of the four waves' partials of one output, fixed order
 __device__ __forceinline__ float sum8(const float *p) {
+    static_assert(kMWaves == 4, "one float4 of wave partials per output");
     const f4v u = lds4(p);
-    if (kMWaves == 4) return (u.x + u.y) + (u.z + u.w);
-    const f4v v = lds4(p + 4);
-    return ((u.x + u.y) + (u.z + u.w)) + ((v.x + v.y) + (v.z + v.w));
+    return (u.x + u.y) + (u.z + u.w);
 }
 
 // A packed hop vector (fatchord_xcdm.h): the slot of step t, and its publish (a plain 4-byte
@@ -551,7 +550,7 @@ __device__ __forceinline__ int rsample(const unsigned long long *lg, int n, uint
 // operands in LDS) on the gathered f2 slice, the logits a sixth hop, rsample instead of msample;
 // the Exp(1) draws always come from `noise` (Philox pre-filled by the host).
 template <int NQ, bool kDbg, bool kRaw>
-__global__ __launch_bounds__(kMThreads, kMWaves == 8 ? 2 : 1) void fatchord_xcdm_kernel(XcdmArgs a) {
+__global__ __launch_bounds__(kMThreads, 1) void fatchord_xcdm_kernel(XcdmArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int NR = 4 * NQ;
     constexpr bool kTwoLevel = NQ >= 2;

@@ -223,7 +223,12 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
     //     this lane polls (r·7 + k); waves 0..3: fc2 rows 4w + r (r·4 + k); wave 0: the F2 poll
     //     buffer in wr[16..31]
     f4v wg[8];
-    f2v wr[32];
+    // 16-byte aligned: wave 0 reuses wr[16..31] as its F2 poll buffer (eight u4v)
+    alignas(16) f2v wr[32];
+    constexpr int kFc2Pairs = 4 * (512 / 128);   // fc2: 4 rows x 512 / (64 lanes x 2) pairs per lane
+    static_assert(kFc2Pairs <= 16, "wave 0's fc2 weights must fit wr[0..15]: wr[16..31] is its F2 poll buffer");
+    static_assert(4 * kSPairs <= 32, "fc1 rows of a wave must fit wr[]");
+    static_assert(sizeof(f2v) * 16 == 8 * sizeof(u4v), "the F2 poll buffer is eight 16-byte loads");
     int ja = 0, jb = 0;
     {
         const bool gw = wave < kSUB && eng < 3;
@@ -252,7 +257,7 @@ __global__ __launch_bounds__(kXThreads, 2) void fatchord_xcds_kernel(XcdsArgs a)
 #pragma unroll
         for (int i = 0; i < 32; ++i) {
             const int r = i >> 2, kk = i & 3;
-            wr[i] = i < 16 ? *reinterpret_cast<const f2v *>(W + r * 512 + 2 * (lane + 64 * kk)) : f2v{0.0f, 0.0f};
+            wr[i] = i < kFc2Pairs ? *reinterpret_cast<const f2v *>(W + r * 512 + 2 * (lane + 64 * kk)) : f2v{0.0f, 0.0f};
         }
     }
     // GRU1 of units tid and tid + 512 (tid < 384): x-coefficients

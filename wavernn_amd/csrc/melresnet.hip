@@ -158,14 +158,27 @@ int wrnn_melresnet_floats(const wrnn_melresnet_cfg *cfg) {
     return (int)(cfg->in_dims * K * C + C + cfg->res_blocks * 2 * (C * C + C) + C * R + R);
 }
 
-int wrnn_melresnet(const wrnn_melresnet_cfg *cfg, const float *packed, const float *mel, int U, int T, float *aux,
-                   void *stream) {
+namespace {
+// CUs of the current device, queried once per device (a partitioned part reports fewer)
+int mr_num_cus() {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cus[dev]) {
+        int n = 0;
+        cus[dev] = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
+    }
+    return cus[dev];
+}
+
+// The tile form for U utterances of T frames: 16-frame tiles, or 4-frame tiles when the 16-frame
+// grid has fewer workgroups than the device has CUs (WRNN_MR_FRAMES=16|4 forces one).  Sets the
+// frames-per-thread of the compute / output layers; false when the channel counts fit neither.
+bool mr_choose(const wrnn_melresnet_cfg *cfg, int U, int T, int *F_, int *fc_, int *fr_, size_t *lds_) {
     using namespace wrnn;
-    if (wrnn_melresnet_floats(cfg) < 0 || !packed || !mel || !aux || U < 1 || T < 1) return WRNN_EINVAL;
     const int K = 2 * cfg->pad + 1;
-    // small grids (fewer 16-frame tiles than CUs) take 4-frame tiles (WRNN_MR_FRAMES=16|4 forces one)
     const char *fe = std::getenv("WRNN_MR_FRAMES");
-    int F = (long long)U * ((T + kMrFBig - 1) / kMrFBig) >= 256 ? kMrFBig : kMrFSmall;
+    int F = (long long)U * ((T + kMrFBig - 1) / kMrFBig) >= mr_num_cus() ? kMrFBig : kMrFSmall;
     if (fe && (std::atoi(fe) == kMrFBig || std::atoi(fe) == kMrFSmall)) F = std::atoi(fe);
     int fc = mr_fpt(cfg->compute_dims, F), fr = mr_fpt(cfg->res_out_dims, F);
     if ((!fc || !fr) && F == kMrFSmall) {   // channel counts only the 16-frame form covers
@@ -175,7 +188,26 @@ int wrnn_melresnet(const wrnn_melresnet_cfg *cfg, const float *packed, const flo
     }
     const size_t lds = ((size_t)cfg->in_dims * (F + K - 1) + 2 * (size_t)cfg->compute_dims * F +
                         (size_t)kMrKc * std::max(cfg->compute_dims, cfg->res_out_dims)) * 4;
-    if (!fc || !fr || lds > 160 * 1024) return WRNN_EUNSUPPORTED;
+    *F_ = F, *fc_ = fc, *fr_ = fr, *lds_ = lds;
+    return fc && fr && lds <= 160 * 1024;
+}
+}  // namespace
+
+int wrnn_melresnet_tile_frames(const wrnn_melresnet_cfg *cfg, int U, int T) {
+    if (wrnn_melresnet_floats(cfg) < 0 || U < 1 || T < 1) return WRNN_EINVAL;
+    int F = 0, fc = 0, fr = 0;
+    size_t lds = 0;
+    return mr_choose(cfg, U, T, &F, &fc, &fr, &lds) ? F : WRNN_EUNSUPPORTED;
+}
+
+int wrnn_melresnet(const wrnn_melresnet_cfg *cfg, const float *packed, const float *mel, int U, int T, float *aux,
+                   void *stream) {
+    using namespace wrnn;
+    if (wrnn_melresnet_floats(cfg) < 0 || !packed || !mel || !aux || U < 1 || T < 1) return WRNN_EINVAL;
+    const int K = 2 * cfg->pad + 1;
+    int F = 0, fc = 0, fr = 0;
+    size_t lds = 0;
+    if (!mr_choose(cfg, U, T, &F, &fc, &fr, &lds)) return WRNN_EUNSUPPORTED;
     MrArgs a{packed, mel, aux, U, T, cfg->in_dims, cfg->compute_dims, cfg->res_out_dims, cfg->res_blocks, K};
     const dim3 grid((T + F - 1) / F, U);
     hipStream_t st = (hipStream_t)stream;

@@ -160,14 +160,17 @@ __device__ __forceinline__ uint32_t philox_word(unsigned long long seed, unsigne
     return w == 0 ? c0 : w == 1 ? c1 : w == 2 ? c2 : c3;
 }
 
-// Draw k of row/step in the reference distribution (MOL: U(1e-5, 1-1e-5); RAW: Exp(1)), from the
-// top 24 bits of the word.  The MoL map is one explicit FMA (what hipcc's contraction formed from
-// `1e-5f + c·u` anyway), so the host restatement (oracle/philox.py) is exact.
+// Draw k of row/step in the reference distribution (MOL: U(1e-5, 1-1e-5); RAW / DM: Exp(1)), from
+// the top 24 bits of the word.  Both maps are exactly restatable on the host (oracle/philox.py):
+// the MoL map is one explicit FMA (what hipcc's contraction formed from `1e-5f + c·u` anyway); the
+// Exp(1) map takes the log in float64 and rounds once — the fp32 logf (v_log_f32 + scaling) read
+// about one ulp high on a third of the draws (profiles/r06_philox_logf.log).  Only the fill kernel
+// and the fallback kernels evaluate it; the XCD-resident kernels load filled draws.
 __device__ __forceinline__ float philox_noise(unsigned long long seed, unsigned long long row,
                                               uint32_t step, uint32_t k, int mol) {
     const uint32_t w = philox_word(seed, row, step, k);
     if (mol) return __builtin_fmaf(1.0f - 2e-5f, (float)(w >> 8) * 0x1p-24f, 1e-5f);
-    return -logf((float)((w >> 8) + 1u) * 0x1p-24f);
+    return (float)(-::log((double)((w >> 8) + 1u) * 0x1p-24));
 }
 
 // ---------------------------------------------------------------------------- hand-off
