@@ -18,9 +18,10 @@ key = (seed & 0xffffffff, seed >> 32)).  Its top 24 bits m give
     the product of two fp32 values is exact in float64 and the sum too (it spans < 53 bits:
     2^0 .. 2^-48), so one rounding to fp32 is the FMA exactly;
   * RAW / deepmind (q ~ Exp(1); Categorical.sample ≡ argmax(probs / q),
-    fatchord_version.py:232-235, deepmind_version.py:130,150): -log((m + 1)·2^-24), here in
-    float64 rounded once to fp32 (the device's fp32 logf is within a few ulp of it; the tests
-    state the bound they check).
+    fatchord_version.py:232-235, deepmind_version.py:130,150): -log((m + 1)·2^-24) in float64,
+    rounded once to fp32, as the device computes it (two faithfully rounded float64 logs round
+    to different fp32 values only across a rounding boundary, ~2^-29 per draw; the tests state
+    the bound they check — observed bit-equal on every draw).
 """
 from __future__ import annotations
 
@@ -64,7 +65,7 @@ def philox_words(seed: int, row0: int, rows: int, step0: int, steps: int, K: int
     ctr = np.stack([Q, T, (R & _MASK).astype(np.uint32), (R >> _S32).astype(np.uint32)], axis=-1)
     key = np.array([seed & 0xFFFFFFFF, seed >> 32], dtype=np.uint32)
     out = philox4x32(ctr, key)                            # [steps][rows][nq][4]
-    return out.reshape(steps, rows, nq * 4)[:, :, k]
+    return np.ascontiguousarray(out.reshape(steps, rows, nq * 4)[:, :, k])
 
 
 def draws_from_words(w: np.ndarray, mol: bool) -> np.ndarray:
@@ -80,4 +81,4 @@ def draws_from_words(w: np.ndarray, mol: bool) -> np.ndarray:
 def philox_draws(seed: int, row0: int, rows: int, step0: int, steps: int, K: int, mol: bool) -> np.ndarray:
     """Draws [steps][rows][K] exactly as wrnn_philox_draws lays them out (the noise == NULL draws
     of every loop kernel; usable as injected `noise`)."""
-    return draws_from_words(philox_words(seed, row0, rows, step0, steps, K), mol)
+    return np.ascontiguousarray(draws_from_words(philox_words(seed, row0, rows, step0, steps, K), mol))
