@@ -60,29 +60,33 @@ def main():
         sk = np.concatenate(skews) / 100.0
         print(f"step-start skew over an XCD's workgroups: median {np.median(sk):.3f} us, 90th pct "
               f"{np.percentile(sk, 90):.3f} us, max {sk.max():.3f} us")
-    # the h_c hop in real time (10 ns ticks): last publish over the XCD's workgroups (slot 22, wave
-    # 0) → each wave's poll done (slot 21); and each workgroup's own publish after its step start
-    hop, own = [], []
-    for x in range(8):
-        m = (blk % 8) == x
-        if m.sum() < 2:
-            continue
-        pub = st[m, 0, :, 22]
-        last = pub.max(0)
-        for w in range(waves):
-            hop.append(st[m, w, :, 21] - last[None, :])
-        own.append(pub - st[m, 0, :, K - 1])
-    if hop:
-        hp, ow = np.concatenate(hop).ravel() / 100.0, np.concatenate(own).ravel() / 100.0
-        ok = (hp > -5) & (hp < 20)
-        print(f"h_c publish after the own step start: median {np.median(ow):.3f} us, max {ow.max():.3f} us; "
-              f"h_c poll done after the XCD's last publish: median {np.median(hp[ok]):.3f} us, "
-              f"90th pct {np.percentile(hp[ok], 90):.3f} us")
+    # the h_c and h_f hops in real time (10 ns ticks): last publish over the XCD's workgroups (wave 0:
+    # slot 22 / 23) → each wave's poll done (slot 21 / 24); each workgroup's own publish after its
+    # step start; and the spread of the publishes over the XCD (last − first)
+    for name, s_pub, s_done in (("h_c", 22, 21), ("h_f", 23, 24)):
+        hop, own, spread = [], [], []
+        for x in range(8):
+            m = (blk % 8) == x
+            if m.sum() < 2:
+                continue
+            pub = st[m, 0, :, s_pub]
+            last = pub.max(0)
+            spread.append(last - pub.min(0))
+            for w in range(waves):
+                hop.append(st[m, w, :, s_done] - last[None, :])
+            own.append(pub - st[m, 0, :, K - 1])
+        if hop:
+            hp, ow = np.concatenate(hop).ravel() / 100.0, np.concatenate(own).ravel() / 100.0
+            sp = np.concatenate(spread).ravel() / 100.0
+            ok = (hp > -5) & (hp < 20)
+            print(f"{name} publish after the own step start: median {np.median(ow):.3f} us, max {ow.max():.3f} us; "
+                  f"spread over the XCD median {np.median(sp):.3f} us; poll done after the XCD's last publish: "
+                  f"median {np.median(hp[ok]):.3f} us, 90th pct {np.percentile(hp[ok], 90):.3f} us")
     for w in range(waves):
         rel = st[:, w, :, :] - base[:, w]
         print(f"-- wave {w}")
         prev = 0.0
-        for k in [k for k in range(1, K - 1) if k not in (21, 22)]:
+        for k in [k for k in range(1, K - 1) if k not in (21, 22, 23, 24)]:
             v = rel[..., k]
             v = v[(v > 0) & (v < 10 * step)]
             if v.size == 0:

@@ -83,7 +83,7 @@ constexpr int kDxPR = 5 * kDxWaves * 16 * 20;       // R sets: [set][wave][row 1
 constexpr int kDxPRQ = kDxWaves * 4 * 4 * 16;       // R quarter set: [wave][row 4][n 4][16 k-slices]
 constexpr int kDxStateW = 4 * 2 * kDxU + kDxPR + kDxPRQ + 8;
 
-constexpr int kDxDbgSteps = 48, kDxDbgSkip = 16, kDxStamps = 24;
+constexpr int kDxDbgSteps = 48, kDxDbgSkip = 16, kDxStamps = 26;
 
 struct DxArgs {
     const float *slab;               // [256 workgroups][DxSlab.total]

@@ -648,12 +648,14 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             const float ee = tanh_((rr * Rg[2] + I[2]) + be);
             hf = uu * hf + (1.0f - uu) * ee;
             xpub(xg + kDxHopOff[DX_HF] + gn * kDxSP + kDxUP * c + gu, tag, hf);
+            DSTR(23);   // (the h_f hop in real time, as slots 22 / 21 for h_c)
         }
         DST(10);
         // ---- h_f slice → O3 → relu → o3
         {
             u4v v[4];
             dx_poll(hop_rsrc(xg + kDxHopOff[DX_HF]), wave, tag, a.ctl, a.timeout_ticks, t, DX_HF, abort_flag, lane, v);
+            DSTR(24);
             dx_stage(stg_of(0), lane, v);
         }
         DST(11);
