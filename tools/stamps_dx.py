@@ -27,7 +27,9 @@ def main():
     env = dict(os.environ, WRNN_DEBUG_STAMPS="1", WRNN_DEBUG_FILE=path)
     env.pop("WRNN_PATH", None)
     code = (
-        "import sys; sys.path.insert(0, '.')\n"
+        "import os, sys; sys.path.insert(0, '.')\n"
+        "from wavernn_amd import _native\n"
+        "if os.environ.get('TIME_DM_LIB'): _native.LIB_PATH = os.environ['TIME_DM_LIB']\n"
         "from wavernn_amd import synthetic as syn\nfrom wavernn_amd.loop import DeepmindLoop\n"
         f"d = syn.DEFAULT_DM; B, L = {B}, {L}\n"
         "loop = DeepmindLoop(d.hidden_size, d.quantisation)\n"

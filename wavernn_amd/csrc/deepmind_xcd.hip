@@ -40,6 +40,17 @@
 #ifndef WRNN_DX_GATE_WAVE
 #define WRNN_DX_GATE_WAVE 0   // the wave whose lanes run the coarse / fine gates (3: A/B, slower)
 #endif
+// hop publishes as plain buffer stores through one wave-uniform descriptor + a 32-bit granule
+// index (as fatchord_xcd.hip's xpub_b) instead of workgroup-scope atomic stores (global_store sc0)
+// through 64-bit per-lane addresses
+#ifndef WRNN_DX_PUB_BUF
+#define WRNN_DX_PUB_BUF 1
+#endif
+// A/B: each hop's pads published beside its data (the lanes 56..63 of the publishing wave, right
+// after the data) instead of all four at the step start
+#ifndef WRNN_DX_PAD_LATE
+#define WRNN_DX_PAD_LATE 0
+#endif
 #ifndef WRNN_DX_ORDERED_ARGMAX
 #define WRNN_DX_ORDERED_ARGMAX 1   // samplers: lane l holds classes 4l..4l+3, value-only max + ballot
 #endif
@@ -374,6 +385,12 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
     const int k = mem / kXcdWgs, c = mem - k * kXcdWgs;
     const int RX = min(kDxRowsXcd, (a.nb - k + kXcds - 1) / kXcds);   // rows n < RX: launch row k + 8n
     unsigned long long *xg = a.xg + (size_t)k * kDxXcdStride;
+    const __amdgpu_buffer_rsrc_t xgr = __builtin_amdgcn_make_buffer_rsrc(xg, 0, 0x7fffffff, 0x00020000);
+    // publish granule `gi` (index into the XCD's hop area) of this step
+    auto pub = [&](int gi, uint32_t tg, float v) {
+        if (WRNN_DX_PUB_BUF) xpub_b(xgr, gi, tg, v);
+        else xpub(xg + gi, tg, v);
+    };
     const float *S = a.slab + (size_t)(k * kXcdWgs + c) * a.s.total;
 
     // ---- register-resident A operands
@@ -459,13 +476,16 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         // the pads of this step's 448-wide hop rows (lanes 56..63 of wave 0: 4 rows × 2 per hop),
         // tagged like the data: every workgroup has finished polling step t − 1's vectors before
         // any workgroup starts step t (its logits came after those polls)
-        if (WRNN_DX_PAD && wave == 0 && lane >= 4 * kDxU) {
-            const int pl = lane - 4 * kDxU;
-            unsigned long long *pad = xg + (pl >> 1) * kDxSP + kDxUP * c + kDxU + (pl & 1);
-            xpub(pad + kDxHopOff[DX_HC], tag, 0.0f);
-            xpub(pad + kDxHopOff[DX_O1], tag, 0.0f);
-            xpub(pad + kDxHopOff[DX_HF], tag, 0.0f);
-            xpub(pad + kDxHopOff[DX_O3], tag, 0.0f);
+        const int pl = lane - 4 * kDxU;
+        const int pad = (pl >> 1) * kDxSP + kDxUP * c + kDxU + (pl & 1);   // (lanes 56..63 of wave 0)
+        auto pub_pad = [&](int hop) {
+            if (WRNN_DX_PAD && WRNN_DX_PAD_LATE && tid >= 4 * kDxU && tid < 64) pub(pad + kDxHopOff[hop], tag, 0.0f);
+        };
+        if (WRNN_DX_PAD && !WRNN_DX_PAD_LATE && wave == 0 && lane >= 4 * kDxU) {
+            pub(pad + kDxHopOff[DX_HC], tag, 0.0f);
+            pub(pad + kDxHopOff[DX_O1], tag, 0.0f);
+            pub(pad + kDxHopOff[DX_HF], tag, 0.0f);
+            pub(pad + kDxHopOff[DX_O3], tag, 0.0f);
         }
         // ---- coarse gates (:106-125): R·h_{t-1} (partials of the previous step), I_coarse(prev)
         if (gate) {
@@ -490,10 +510,11 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             const float rr = sigmoid_((Rg[1] + I[1]) + br);
             const float ee = tanh_((rr * Rg[2] + I[2]) + be);
             hc = uu * hc + (1.0f - uu) * ee;
-            xpub(xg + kDxHopOff[DX_HC] + gn * kDxSP + kDxUP * c + gu, tag, hc);
+            pub(kDxHopOff[DX_HC] + gn * kDxSP + kDxUP * c + gu, tag, hc);
             DST(19);
             DSTR(22);   // (s_memrealtime: the h_c hop measured across workgroups, tools/stamps_dx.py)
         }
+        pub_pad(DX_HC);
         // row group B (WG-local rows 48..83: fine gate rows only) of R·h_{t-1}, both halves from the
         // still-staged h_c(t-1) / h_f(t-1) slices: the other waves while the gate wave runs the
         // coarse gates, the gate wave in its h_c hop wait; partials → LDS (summed in this step's O2
@@ -533,7 +554,9 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         if (tid < 4 * kDxU) {
             const int r = tid % kDxU, n = tid / kDxU;
             const float o = dx_o13sum(po1, r, n) + bo1;
-            xpub(xg + kDxHopOff[DX_O1] + n * kDxSP + kDxUP * c + r, tag, o > 0.0f ? o : 0.0f);
+            pub(kDxHopOff[DX_O1] + n * kDxSP + kDxUP * c + r, tag, o > 0.0f ? o : 0.0f);
+        } else if (WRNN_DX_PAD_LATE && tid < 64) {
+            pub_pad(DX_O1);
         } else if (more && lt >= 0) {   // log q of step t + 1 → ring slot (t + 1) & 1
             float *slot = nzr + ((t + 1) & 1) * 4 * 2 * kDxQ;
 #pragma unroll
@@ -563,7 +586,7 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         DST(7);
         if (tid < 4 * kDxUO2) {
             const int r = tid % kDxUO2, n = tid / kDxUO2;
-            xpub(xg + kDxHopOff[DX_LC] + n * kDxQ + kDxUO2 * c + r, tag, dx_o24sum(po2, r, n) + bo2);
+            pub(kDxHopOff[DX_LC] + n * kDxQ + kDxUO2 * c + r, tag, dx_o24sum(po2, r, n) + bo2);
         } else if (tid >= 64 && t > a.t0) {
             r_sums(tid - 64, kDxThreads - 64, 48, 84);   // group B of R·h_{t-1} (partials from this step's start)
         }
@@ -647,9 +670,10 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             const float rr = sigmoid_((Rg[1] + I[1]) + br);
             const float ee = tanh_((rr * Rg[2] + I[2]) + be);
             hf = uu * hf + (1.0f - uu) * ee;
-            xpub(xg + kDxHopOff[DX_HF] + gn * kDxSP + kDxUP * c + gu, tag, hf);
+            pub(kDxHopOff[DX_HF] + gn * kDxSP + kDxUP * c + gu, tag, hf);
             DSTR(23);   // (the h_f hop in real time, as slots 22 / 21 for h_c)
         }
+        pub_pad(DX_HF);
         DST(10);
         // ---- h_f slice → O3 → relu → o3
         {
@@ -667,7 +691,9 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         if (tid < 4 * kDxU) {
             const int r = tid % kDxU, n = tid / kDxU;
             const float o = dx_o13sum(po3, r, n) + bo3;
-            xpub(xg + kDxHopOff[DX_O3] + n * kDxSP + kDxUP * c + r, tag, o > 0.0f ? o : 0.0f);
+            pub(kDxHopOff[DX_O3] + n * kDxSP + kDxUP * c + r, tag, o > 0.0f ? o : 0.0f);
+        } else {
+            pub_pad(DX_O3);
         }
         DST(13);
         // ---- R[rows 0..47, S:]·h_f finishes group A of R·h_t (the gates above have read R·h_{t-1})
@@ -687,7 +713,7 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         DST(16);
         if (tid < 4 * kDxUO2) {
             const int r = tid % kDxUO2, n = tid / kDxUO2;
-            xpub(xg + kDxHopOff[DX_LF] + n * kDxQ + kDxUO2 * c + r, tag, dx_o24sum(po4, r, n) + bo4);
+            pub(kDxHopOff[DX_LF] + n * kDxQ + kDxUO2 * c + r, tag, dx_o24sum(po4, r, n) + bo4);
         } else if (tid >= 64) {
             r_sums(tid - 64, kDxThreads - 64, 0, 48);   // group A of R·h_t (complete since the barrier)
         }
