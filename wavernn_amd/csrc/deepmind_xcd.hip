@@ -46,8 +46,9 @@
 #ifndef WRNN_DX_PUB_BUF
 #define WRNN_DX_PUB_BUF 1
 #endif
-// A/B: each hop's pads published beside its data (the lanes 56..63 of the publishing wave, right
-// after the data) instead of all four at the step start
+// A/B: 1 = each hop's pads published beside its data (the lanes 56..63 of the publishing wave,
+// right after the data) instead of all four at the step start; 2 = all four for step t + 1 at the
+// end of step t (after the fine sample: every workgroup has polled step t's vectors by then)
 #ifndef WRNN_DX_PAD_LATE
 #define WRNN_DX_PAD_LATE 0
 #endif
@@ -479,9 +480,10 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         const int pl = lane - 4 * kDxU;
         const int pad = (pl >> 1) * kDxSP + kDxUP * c + kDxU + (pl & 1);   // (lanes 56..63 of wave 0)
         auto pub_pad = [&](int hop) {
-            if (WRNN_DX_PAD && WRNN_DX_PAD_LATE && tid >= 4 * kDxU && tid < 64) pub(pad + kDxHopOff[hop], tag, 0.0f);
+            if (WRNN_DX_PAD && WRNN_DX_PAD_LATE == 1 && tid >= 4 * kDxU && tid < 64) pub(pad + kDxHopOff[hop], tag, 0.0f);
         };
-        if (WRNN_DX_PAD && !WRNN_DX_PAD_LATE && wave == 0 && lane >= 4 * kDxU) {
+        if (WRNN_DX_PAD && (WRNN_DX_PAD_LATE == 0 || (WRNN_DX_PAD_LATE == 2 && t == a.t0)) && wave == 0 &&
+            lane >= 4 * kDxU) {
             pub(pad + kDxHopOff[DX_HC], tag, 0.0f);
             pub(pad + kDxHopOff[DX_O1], tag, 0.0f);
             pub(pad + kDxHopOff[DX_HF], tag, 0.0f);
@@ -555,7 +557,7 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             const int r = tid % kDxU, n = tid / kDxU;
             const float o = dx_o13sum(po1, r, n) + bo1;
             pub(kDxHopOff[DX_O1] + n * kDxSP + kDxUP * c + r, tag, o > 0.0f ? o : 0.0f);
-        } else if (WRNN_DX_PAD_LATE && tid < 64) {
+        } else if (WRNN_DX_PAD_LATE == 1 && tid < 64) {
             pub_pad(DX_O1);
         } else if (more && lt >= 0) {   // log q of step t + 1 → ring slot (t + 1) & 1
             float *slot = nzr + ((t + 1) & 1) * 4 * 2 * kDxQ;
@@ -734,6 +736,12 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             }
         }
         DST(18);
+        if (WRNN_DX_PAD && WRNN_DX_PAD_LATE == 2 && more && wave == 0 && lane >= 4 * kDxU) {
+            pub(pad + kDxHopOff[DX_HC], tag + 1u, 0.0f);
+            pub(pad + kDxHopOff[DX_O1], tag + 1u, 0.0f);
+            pub(pad + kDxHopOff[DX_HF], tag + 1u, 0.0f);
+            pub(pad + kDxHopOff[DX_O3], tag + 1u, 0.0f);
+        }
         bar();
         if (*abort_flag) return;
     }
