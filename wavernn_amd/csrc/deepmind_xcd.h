@@ -83,7 +83,7 @@ constexpr int kDxPR = 5 * kDxWaves * 16 * 20;       // R sets: [set][wave][row 1
 constexpr int kDxPRQ = kDxWaves * 4 * 4 * 16;       // R quarter set: [wave][row 4][n 4][16 k-slices]
 constexpr int kDxStateW = 4 * 2 * kDxU + kDxPR + kDxPRQ + 8;
 
-constexpr int kDxDbgSteps = 48, kDxDbgSkip = 16, kDxStamps = 26;
+constexpr int kDxDbgSteps = 32, kDxDbgSkip = 16, kDxStamps = 26;
 
 struct DxArgs {
     const float *slab;               // [256 workgroups][DxSlab.total]
@@ -103,7 +103,7 @@ struct DxArgs {
 };
 
 struct DxLds {
-    int stg, ao, pr, prq, rs, po1, po3, po2, po4, nz, cst, lab, misc, dbg, total;
+    int stg, ao, pr, prq, rs, po1, po3, po2, po4, nz, cst, lab, misc, gbc, dbg, total;
 };
 constexpr int kDxST = kDxKW + 4;   // staged slice row stride (floats)
 // A operands read from LDS instead of registers (the quarter set and O2 / O4: 42 per lane and
@@ -125,6 +125,7 @@ __host__ __device__ inline DxLds dx_lds_layout(bool dbg = false) {
     l.cst = o;  o += kDxCst + 4;
     l.lab = o;  o += 16;                           // previous coarse [4], fine [4], c_t [4]
     l.misc = o; o += 8;                            // [0] abort flag, [1] member index
+    l.gbc = o;  o += kDxWaves * 3 * 4 * 64;        // R·h group B after its coarse half: [wave][set 3, 4, quarter][4][64]
     l.dbg = o;  o += dbg ? kDxDbgSteps * kDxWaves * kDxStamps : 0;
     l.total = o;
     return l;

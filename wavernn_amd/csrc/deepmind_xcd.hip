@@ -52,6 +52,21 @@
 #ifndef WRNN_DX_PAD_LATE
 #define WRNN_DX_PAD_LATE 0
 #endif
+// R·h group B (WG-local rows 48..83) of h_t in two places: its coarse half (h_c(t) columns) in step
+// t's h_f hop window, the accumulators parked in LDS, its fine half at the start of step t + 1 —
+// one MFMA chain as before (bit-identical sums).  0: both halves at the start of step t + 1, in
+// the h_c hop window (round 5), where the MFMA stream ahead of the h_c poll delayed it.  2: the
+// gate wave, which runs the fine gates in the h_f window, takes its coarse half in the coarse
+// logits hop's window instead (after publishing its logits, before its sampler's poll).
+#ifndef WRNN_DX_GB_SPLIT
+#define WRNN_DX_GB_SPLIT 1
+#endif
+// diagnostics (timing only, wrong results): 1 = R·h group B after the h_c poll instead of in its
+// window; 2 = the gate wave skips its share of group B; 3 / 4 = its coarse half skipped by the
+// non-gate waves / by every wave
+#ifndef WRNN_DX_GB_AFTER_POLL
+#define WRNN_DX_GB_AFTER_POLL 0
+#endif
 #ifndef WRNN_DX_ORDERED_ARGMAX
 #define WRNN_DX_ORDERED_ARGMAX 1   // samplers: lane l holds classes 4l..4l+3, value-only max + ballot
 #endif
@@ -451,10 +466,42 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
     __syncthreads();
 
     // R[rows 48..83, :]·h of the staged h_c (stg_of(2)) and h_f (stg_of(0)) slices → partials
-    auto r_group_b = [&]() {
+    float *gbc = smem + ll.gbc + wave * 3 * 4 * 64;   // this wave's parked group-B accumulators
+    // the coarse half of group B of R·h_t (h_c(t) staged in stg_of(2)) → gbc
+    auto r_group_b_coarse = [&]() {
         f4v bR[5], bQ;
         MPollNoneDx none;
         dx_rhalf<0, 3, 5, true>(AR, arq, stg_of(2), bR, bQ, lane, none);
+        mfma_drain_begin();
+        mfma_tie(bR[3]);
+        mfma_tie(bR[4]);
+        mfma_tie(bQ);
+        *reinterpret_cast<f4v *>(gbc + (0 * 64 + lane) * 4) = bR[3];
+        *reinterpret_cast<f4v *>(gbc + (1 * 64 + lane) * 4) = bR[4];
+        *reinterpret_cast<f4v *>(gbc + (2 * 64 + lane) * 4) = bQ;
+    };
+    // its fine half (h_f(t) in stg_of(0)) continuing the parked chains → partials
+    auto r_group_b_fine = [&]() {
+        f4v bR[5], bQ;
+        MPollNoneDx none;
+        bR[3] = lds4(gbc + (0 * 64 + lane) * 4);
+        bR[4] = lds4(gbc + (1 * 64 + lane) * 4);
+        bQ = lds4(gbc + (2 * 64 + lane) * 4);
+        dx_rhalf<1, 3, 5, true>(AR, arq, stg_of(0), bR, bQ, lane, none);
+        dx_rput<3, 5, true>(bR, bQ, pr, prq, lane, wave);
+    };
+    auto r_group_b = [&]() {
+        f4v bR[5], bQ;
+        MPollNoneDx none;
+        // (diagnostics 3 / 4: the coarse half skipped by the non-gate waves / by every wave)
+        const bool skip_c = WRNN_DX_GB_AFTER_POLL == 4 || (WRNN_DX_GB_AFTER_POLL == 3 && wave != WRNN_DX_GATE_WAVE);
+        if (skip_c) {
+#pragma unroll
+            for (int s = 0; s < 5; ++s) bR[s] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
+            bQ = f4v{0.0f, 0.0f, 0.0f, 0.0f};
+        } else {
+            dx_rhalf<0, 3, 5, true>(AR, arq, stg_of(2), bR, bQ, lane, none);
+        }
         dx_rhalf<1, 3, 5, true>(AR, arq, stg_of(0), bR, bQ, lane, none);
         dx_rput<3, 5, true>(bR, bQ, pr, prq, lane, wave);
     };
@@ -521,7 +568,10 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         // still-staged h_c(t-1) / h_f(t-1) slices: the other waves while the gate wave runs the
         // coarse gates, the gate wave in its h_c hop wait; partials → LDS (summed in this step's O2
         // epilogue window)
-        if (t > a.t0) r_group_b();
+        if ((WRNN_DX_GB_AFTER_POLL != 1 && (WRNN_DX_GB_AFTER_POLL != 2 || wave != WRNN_DX_GATE_WAVE)) && t > a.t0) {
+            if (WRNN_DX_GB_SPLIT) r_group_b_fine();
+            else r_group_b();
+        }
         DST(1);
         // ---- h_c slice → O1 → relu → o1
         {
@@ -532,6 +582,7 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             DSTR(21);
             dx_stage(stg_of(2), lane, v);
         }
+        if (WRNN_DX_GB_AFTER_POLL == 1 && t > a.t0) r_group_b();
         // the draws of step t + 1 → registers of waves 1..3; their logs go into the ring while
         // wave 0 publishes o1 (below)
         f4v nzl[kNzLd];
@@ -592,6 +643,7 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         } else if (tid >= 64 && t > a.t0) {
             r_sums(tid - 64, kDxThreads - 64, 48, 84);   // group B of R·h_{t-1} (partials from this step's start)
         }
+        if (WRNN_DX_GB_SPLIT == 2 && more && wave == WRNN_DX_GATE_WAVE) r_group_b_coarse();
         DST(8);
         // ---- sample c_t (:129-131): wave n samples row n
         auto sample_row = [&](int hop, int half) -> int {
@@ -676,6 +728,9 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             DSTR(23);   // (the h_f hop in real time, as slots 22 / 21 for h_c)
         }
         pub_pad(DX_HF);
+        // the coarse half of group B of R·h_t (the next step's fine half continues it): every wave
+        // in the h_f hop window (waves 1..3 idle there; the gate wave after publishing h_f)
+        if (WRNN_DX_GB_SPLIT && more && (WRNN_DX_GB_SPLIT == 1 || wave != WRNN_DX_GATE_WAVE)) r_group_b_coarse();
         DST(10);
         // ---- h_f slice → O3 → relu → o3
         {
