@@ -46,12 +46,6 @@
 #ifndef WRNN_DX_PUB_BUF
 #define WRNN_DX_PUB_BUF 1
 #endif
-// A/B: 1 = each hop's pads published beside its data (the lanes 56..63 of the publishing wave,
-// right after the data) instead of all four at the step start; 2 = all four for step t + 1 at the
-// end of step t (after the fine sample: every workgroup has polled step t's vectors by then)
-#ifndef WRNN_DX_PAD_LATE
-#define WRNN_DX_PAD_LATE 0
-#endif
 // R·h group B (WG-local rows 48..83) of h_t in two places: its coarse half (h_c(t) columns) in step
 // t's h_f hop window, the accumulators parked in LDS, its fine half at the start of step t + 1 —
 // one MFMA chain as before (bit-identical sums).  0: both halves at the start of step t + 1, in
@@ -524,13 +518,11 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         // the pads of this step's 448-wide hop rows (lanes 56..63 of wave 0: 4 rows × 2 per hop),
         // tagged like the data: every workgroup has finished polling step t − 1's vectors before
         // any workgroup starts step t (its logits came after those polls)
-        const int pl = lane - 4 * kDxU;
-        const int pad = (pl >> 1) * kDxSP + kDxUP * c + kDxU + (pl & 1);   // (lanes 56..63 of wave 0)
-        auto pub_pad = [&](int hop) {
-            if (WRNN_DX_PAD && WRNN_DX_PAD_LATE == 1 && tid >= 4 * kDxU && tid < 64) pub(pad + kDxHopOff[hop], tag, 0.0f);
-        };
-        if (WRNN_DX_PAD && (WRNN_DX_PAD_LATE == 0 || (WRNN_DX_PAD_LATE == 2 && t == a.t0)) && wave == 0 &&
-            lane >= 4 * kDxU) {
+        // (measured in round 6: the pads written beside each hop's data, or for step t + 1 at the end
+        // of step t, run no faster, profiles/r06_ab_dx_padlate.log)
+        if (WRNN_DX_PAD && wave == 0 && lane >= 4 * kDxU) {
+            const int pl = lane - 4 * kDxU;
+            const int pad = (pl >> 1) * kDxSP + kDxUP * c + kDxU + (pl & 1);
             pub(pad + kDxHopOff[DX_HC], tag, 0.0f);
             pub(pad + kDxHopOff[DX_O1], tag, 0.0f);
             pub(pad + kDxHopOff[DX_HF], tag, 0.0f);
@@ -563,7 +555,6 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             DST(19);
             DSTR(22);   // (s_memrealtime: the h_c hop measured across workgroups, tools/stamps_dx.py)
         }
-        pub_pad(DX_HC);
         // row group B (WG-local rows 48..83: fine gate rows only) of R·h_{t-1}, both halves from the
         // still-staged h_c(t-1) / h_f(t-1) slices: the other waves while the gate wave runs the
         // coarse gates, the gate wave in its h_c hop wait; partials → LDS (summed in this step's O2
@@ -608,8 +599,6 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             const int r = tid % kDxU, n = tid / kDxU;
             const float o = dx_o13sum(po1, r, n) + bo1;
             pub(kDxHopOff[DX_O1] + n * kDxSP + kDxUP * c + r, tag, o > 0.0f ? o : 0.0f);
-        } else if (WRNN_DX_PAD_LATE == 1 && tid < 64) {
-            pub_pad(DX_O1);
         } else if (more && lt >= 0) {   // log q of step t + 1 → ring slot (t + 1) & 1
             float *slot = nzr + ((t + 1) & 1) * 4 * 2 * kDxQ;
 #pragma unroll
@@ -727,7 +716,6 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             pub(kDxHopOff[DX_HF] + gn * kDxSP + kDxUP * c + gu, tag, hf);
             DSTR(23);   // (the h_f hop in real time, as slots 22 / 21 for h_c)
         }
-        pub_pad(DX_HF);
         // the coarse half of group B of R·h_t (the next step's fine half continues it): every wave
         // in the h_f hop window (waves 1..3 idle there; the gate wave after publishing h_f)
         if (WRNN_DX_GB_SPLIT && more && (WRNN_DX_GB_SPLIT == 1 || wave != WRNN_DX_GATE_WAVE)) r_group_b_coarse();
@@ -749,8 +737,6 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             const int r = tid % kDxU, n = tid / kDxU;
             const float o = dx_o13sum(po3, r, n) + bo3;
             pub(kDxHopOff[DX_O3] + n * kDxSP + kDxUP * c + r, tag, o > 0.0f ? o : 0.0f);
-        } else {
-            pub_pad(DX_O3);
         }
         DST(13);
         // ---- R[rows 0..47, S:]·h_f finishes group A of R·h_t (the gates above have read R·h_{t-1})
@@ -791,12 +777,6 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
             }
         }
         DST(18);
-        if (WRNN_DX_PAD && WRNN_DX_PAD_LATE == 2 && more && wave == 0 && lane >= 4 * kDxU) {
-            pub(pad + kDxHopOff[DX_HC], tag + 1u, 0.0f);
-            pub(pad + kDxHopOff[DX_O1], tag + 1u, 0.0f);
-            pub(pad + kDxHopOff[DX_HF], tag + 1u, 0.0f);
-            pub(pad + kDxHopOff[DX_O3], tag + 1u, 0.0f);
-        }
         bar();
         if (*abort_flag) return;
     }
