@@ -109,3 +109,55 @@ def test_shard_indices_partition():
             flat = [i for p in parts for i in p]
             assert flat == list(range(n))                    # contiguous blocks, in order
             assert max(map(len, parts)) - min(map(len, parts)) <= 1
+
+
+class _NoiseModel(_RowsModel):
+    """Stand-in model whose generate_many records the injected draws it receives (the slice of the
+    whole list's [L_max][rows][K] noise for the rank's rows); hop_length as WaveRNN's."""
+    hop_length = 275
+
+    def __init__(self):
+        self.got = []
+
+    def generate_many(self, ms, save_paths, batched, target, overlap, mu_law, *, seed, row_offset, noise):
+        self.got.append((row_offset, None if noise is None else np.asarray(noise).copy()))
+        return [fake_audio(int(row_offset) + j) for j in range(len(ms))]
+
+
+def _noise_worker(rank, world, port, batched, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        frames = [20, 27, 34, 41, 48]
+        mels = [np.zeros((1, 4, T)) for T in frames]
+        rows = [_RowsModel.rows_of(T, batched, 0, 0) for T in frames]
+        L = max(T * _NoiseModel.hop_length for T in frames) if not batched else 64
+        noise = np.arange(L * sum(rows) * 3, dtype=np.float32).reshape(L, sum(rows), 3)
+        m = _NoiseModel()
+        sharding.generate_sharded(m, mels, batched, 32, 16, False, device=torch.device("cpu"), noise=noise)
+        block = sharding.shard_indices(len(mels), rank, world)
+        r0, n = sum(rows[:block[0]]), sum(rows[i] for i in block)
+        steps = 32 + 2 * 16 if batched else max(frames[i] for i in block) * _NoiseModel.hop_length
+        (row_offset, got), = m.got
+        ok = row_offset == r0 and got.shape == (steps, n, 3) and np.array_equal(got, noise[:steps, r0:r0 + n])
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("batched", [False, True])
+def test_sharded_noise_injection_slices_the_rank_rows(batched):
+    """generate_sharded(noise=): each rank's one launch receives exactly its rows' draws of the whole
+    list's injected noise (global row order, steps trimmed to the rank's launch)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_noise_worker, args=(r, world, port, batched, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == {0: True, 1: True}
