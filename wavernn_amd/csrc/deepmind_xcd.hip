@@ -49,9 +49,9 @@
 // R·h group B (WG-local rows 48..83) of h_t in two places: its coarse half (h_c(t) columns) in step
 // t's h_f hop window, the accumulators parked in LDS, its fine half at the start of step t + 1 —
 // one MFMA chain as before (bit-identical sums).  0: both halves at the start of step t + 1, in
-// the h_c hop window (round 5), where the MFMA stream ahead of the h_c poll delayed it.  2: the
-// gate wave, which runs the fine gates in the h_f window, takes its coarse half in the coarse
-// logits hop's window instead (after publishing its logits, before its sampler's poll).
+// the h_c hop window (round 5), where the MFMA stream ahead of the h_c poll delayed it.  (Measured
+// in round 6 and not kept: the gate wave's coarse half in the coarse-logits window, and the fine
+// half behind group A's in the o3 window — DESIGN.md §4.3a.)
 #ifndef WRNN_DX_GB_SPLIT
 #define WRNN_DX_GB_SPLIT 1
 #endif
@@ -632,7 +632,6 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         } else if (tid >= 64 && t > a.t0) {
             r_sums(tid - 64, kDxThreads - 64, 48, 84);   // group B of R·h_{t-1} (partials from this step's start)
         }
-        if (WRNN_DX_GB_SPLIT == 2 && more && wave == WRNN_DX_GATE_WAVE) r_group_b_coarse();
         DST(8);
         // ---- sample c_t (:129-131): wave n samples row n
         auto sample_row = [&](int hop, int half) -> int {
@@ -718,7 +717,7 @@ __global__ __launch_bounds__(kDxThreads, 1) void deepmind_xcd_kernel(DxArgs a) {
         }
         // the coarse half of group B of R·h_t (the next step's fine half continues it): every wave
         // in the h_f hop window (waves 1..3 idle there; the gate wave after publishing h_f)
-        if (WRNN_DX_GB_SPLIT && more && (WRNN_DX_GB_SPLIT == 1 || wave != WRNN_DX_GATE_WAVE)) r_group_b_coarse();
+        if (WRNN_DX_GB_SPLIT && more) r_group_b_coarse();
         DST(10);
         // ---- h_f slice → O3 → relu → o3
         {
