@@ -396,6 +396,9 @@ __device__ __forceinline__ void mlayer_lds(const float (&A)[kMSets][kMJ], const 
 
 // quads polled beside an off-critical layer (all of them: ≤ 8 float4s per lane, the registers
 // the tagged form's two quads took), and the k-chunk at which its loads are issued
+#ifndef WRNN_XCDM_F1_ALL
+#define WRNN_XCDM_F1_ALL 1
+#endif
 #ifndef WRNN_XCDM_RIDE_AT
 #define WRNN_XCDM_RIDE_AT 3
 #endif
@@ -776,9 +779,25 @@ __global__ __launch_bounds__(kMThreads, 1) void fatchord_xcdm_kernel(XcdmArgs a)
         bar();
         MST(9);
         // ---- F: fc1 epilogue → f1; Σ W_hh1·h1 for the next GRU1
+        // The f1 store is issued by EVERY thread (WRNN_XCDM_F1_ALL): threads past the epilogue
+        // roles (rows ≥ NR, unused rows of the 16-row vector storage, never polled) store 0.  With
+        // the store only on the epilogue path, hipcc's wait-count merge at the join made the h2
+        // check below (its loads issued in fc1, before this store) wait vmcnt(0) — i.e. for this
+        // store's acknowledgement too — on the path that has the store; with one store on every
+        // path it waits vmcnt(1), for the loads alone.
+        if (WRNN_XCDM_F1_ALL) {
+            float f1v = 0.0f;
+            if (gru) {
+                const float f = mpart<NQ>(pfc1, gu, gn) + rg[gn * kMRing + MT_V1 + gu];
+                f1v = f > 0.0f ? f : 0.0f;
+            }
+            ppub(pvec(xg, MH_F1, t) + gn * 512 + 16 * c + gu, f1v);
+        }
         if (gru) {
-            const float f = mpart<NQ>(pfc1, gu, gn) + rg[gn * kMRing + MT_V1 + gu];
-            ppub(pvec(xg, MH_F1, t) + gn * 512 + 16 * c + gu, f > 0.0f ? f : 0.0f);
+            if (!WRNN_XCDM_F1_ALL) {
+                const float f = mpart<NQ>(pfc1, gu, gn) + rg[gn * kMRing + MT_V1 + gu];
+                ppub(pvec(xg, MH_F1, t) + gn * 512 + 16 * c + gu, f > 0.0f ? f : 0.0f);
+            }
             if (aux_w0 >= kMWaves) {
 #pragma unroll
                 for (int q = 0; q < 3; ++q) {
