@@ -263,9 +263,9 @@ __device__ __forceinline__ void mpart3(const float *P, int i0, int n, float (&ou
 
 // One layer: NS sets from S0 against every quad of the staged slice, the wave's partials to P.
 // MFMA order: k-chunk (4 columns) outer, then column, quad, set; NC accumulator chains per
-// (quad, set) (column j → chain j % NC) so that ≥ 8 independent chains interleave — the
-// dependent-accumulator latency of v_mfma_f32_4x4x1_16b_f32 is ≈ 52 cycles for an 8-cycle issue
-// (tools/mfma4_bench.hip), and one wave per SIMD has no partner to hide it.
+// (quad, set) (column j → chain j % NC).  A dependent v_mfma_f32_4x4x1_16b_f32 with srcC = the
+// previous dst costs no stall from three interleaved chains up (tools/xcdm_layer_bench.hip), and
+// one-set layers measured no faster with 3 or 4 chains than with 2.
 // kLdsA (RAW fc3, NS = 1): the set's A operands come from LDS ([kMJ / 4][64 lanes][4], AL = the
 // wave's image), read a k-chunk ahead like B.
 template <int NQ, int S0, int NS, int NC, typename Hook = MPollNone, bool kLdsA = false>
